@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Jacobi3D weak scaling, 512^3 cells per GPU, fp32, one process per GPU.
+
+Metric (BASELINE.json): "halo-exchange GB/s + Jacobi3D Gcells/s, 512^3/GPU weak scaling at 1/2/4/8 MI355X".
+`value` is the whole-job Jacobi3D throughput in Gcells/s (global cells x steps / time). One step is the
+reference's full iteration (bin/jacobi3d.cu:265-346): interior stencil overlapped with the halo exchange of all
+faces (periodic), exterior stencil, swap. The global grid follows the reference weak-scaling rule
+(512 * N^0.33333 per axis: 512/645/813/1024 for N=1/2/4/8), decomposed by the NodeAware placement.
+Secondary numbers in the JSON line: the halo-exchange GB/s of an exchange-only loop on the same decomposition
+(bin/bench_exchange.cu definition: aggregate halo bytes / time).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]     (N>1: launched by torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--per-gpu", type=int, default=512)
+    ap.add_argument("--exchange-iters", type=int, default=20)
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--methods", default="all")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import stencil2_amd as st
+
+    pg = st.init_process_group()
+    n = world
+    L = st.models.weak_scaled_size(args.per_gpu, n)
+    methods = st.MethodFlags.All
+    if args.methods != "all":
+        methods = st.MethodFlags.None_
+        for m in args.methods.split(","):
+            methods = methods | getattr(st.MethodFlags, {"staged": "Staged", "rccl": "Rccl", "colo": "Colocated",
+                                                          "peer": "PeerCopy", "kernel": "Kernel"}[m])
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    model = st.Jacobi3D((L, L, L), gpus=[local_rank], methods=methods, overlap=not args.no_overlap, group=pg)
+    model.init()
+    for _ in range(args.warmup):
+        model.step()
+    model.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.step()
+    model.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    cells = L ** 3
+    gcells = cells * args.steps / elapsed / 1e9
+
+    # exchange-only loop on the same decomposition (halo-exchange GB/s, bench_exchange definition)
+    dd = model.domain
+    xbytes = dd.exchange_bytes_for_method(st.MethodFlags.All)
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.exchange_iters):
+        dd.exchange()
+        dd.swap()
+    torch.cuda.synchronize()
+    xel = time.perf_counter() - t1
+    tx = torch.tensor([xel], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tx, op=dist.ReduceOp.MAX)
+    xel = float(tx.item())
+    xgbs = xbytes * args.exchange_iters / xel / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": "Jacobi3D Gcells/s (512^3/GPU weak scaling; halo-exchange GB/s in extra)",
+            "value": round(gcells, 3),
+            "unit": "Gcells/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (reference Jacobi3D initial condition: 0.5 + hot/cold spheres)",
+            "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": L,
+                       "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
+                       "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods),
+                       "overlap": not args.no_overlap},
+            "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
+                      "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
+                      "gcells_per_gpu": round(gcells / n, 3)},
+        }
+        print(json.dumps(out), flush=True)
+    del model
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

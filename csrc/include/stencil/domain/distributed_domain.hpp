@@ -1,0 +1,157 @@
+#pragma once
+// DistributedDomain: the public API of the runtime.
+// Parity: reference include/stencil/stencil.hpp:29-354 + src/stencil.cu:1-939
+//   MethodFlags / set_methods / set_placement / set_gpus / set_radius / add_data<T> / realize / exchange / swap /
+//   get_interior / get_exterior / get_compute_region / exchange_bytes_for_method / write_paraview / setup timers.
+//
+// MI355X-first transport ladder (same priority order as reference src/stencil.cu:163-194):
+//   Kernel    same process, same GPU      -> one fused descriptor copy kernel per device (periodic self-wrap and
+//                                            co-resident sub-domains), no intermediate buffer
+//   PeerCopy  same process, peer GPU      -> the same kernel storing directly into the peer's halo over xGMI
+//   Colocated other process, same node    -> HIP IPC: the pack kernel stores into the receiver's (uncached, double
+//                                            buffered) inbox over xGMI, device flags signal arrival and credits
+//                                            (no host round trip, fixes the reference's missing ack)
+//   Rccl      any other rank              -> RCCL ncclSend/ncclRecv grouped per device on a high-priority stream
+//   Staged    fallback / CPU backend      -> pack, D2H, TCP (native process group), H2D, unpack
+// Exchange is stream-ordered: exchange_async() enqueues everything on per-device comm streams after the events
+// given to record_ready(); wait_exchange() makes a compute stream wait for the halos. exchange() keeps the
+// reference's blocking semantics.
+#include <array>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "stencil/comm/proc_group.hpp"
+#include "stencil/domain/local_domain.hpp"
+#include "stencil/rt/stream.hpp"
+#include "stencil/topo/placement.hpp"
+
+namespace stencil {
+
+enum class MethodFlags : int {
+  None = 0,
+  Staged = 1,    // reference CudaMpi
+  Rccl = 2,      // reference CudaAwareMpi (GPU-aware remote path)
+  Colocated = 4, // reference CudaMpiColocated
+  PeerCopy = 8,  // reference CudaMemcpyPeer
+  Kernel = 16,   // reference CudaKernel
+  All = 31,
+};
+inline MethodFlags operator|(MethodFlags a, MethodFlags b) { return MethodFlags(int(a) | int(b)); }
+inline MethodFlags &operator|=(MethodFlags &a, MethodFlags b) { return a = a | b; }
+inline MethodFlags operator&(MethodFlags a, MethodFlags b) { return MethodFlags(int(a) & int(b)); }
+inline bool operator&&(MethodFlags a, MethodFlags b) { return (int(a) & int(b)) != 0; }
+inline bool any(MethodFlags a) { return a != MethodFlags::None; }
+std::string to_string(MethodFlags m);
+
+// one halo message: sent along `dir` from sub-domain srcId (on the sending rank) to dstId (on the receiving rank)
+struct Message {
+  Dim3 dir;
+  int srcId, dstId;
+  bool operator<(const Message &o) const { return dir < o.dir; }
+  bool operator==(const Message &o) const { return dir == o.dir && srcId == o.srcId && dstId == o.dstId; }
+};
+
+struct ExchangePlanEntry {
+  MethodFlags method;
+  Dim3 srcIdx, dstIdx;
+  int srcRank, dstRank;
+  int srcDev, dstDev;
+  Dim3 dir;
+  int64_t bytes;
+};
+
+class DistributedDomain {
+public:
+  DistributedDomain(int64_t x, int64_t y, int64_t z, std::shared_ptr<comm::ProcGroup> pg = nullptr);
+  ~DistributedDomain();
+  DistributedDomain(const DistributedDomain &) = delete;
+  DistributedDomain &operator=(const DistributedDomain &) = delete;
+
+  // ---- configuration (before realize) ----
+  void set_radius(int64_t r) { radius_ = Radius::constant(r); }
+  void set_radius(const Radius &r) { radius_ = r; }
+  const Radius &radius() const { return radius_; }
+  template <typename T> DataHandle<T> add_data(const std::string &name = "") {
+    return DataHandle<T>(add_data(int64_t(sizeof(T)), name, dtype_of<T>()), name);
+  }
+  int64_t add_data(int64_t elemSize, const std::string &name, DType dtype);
+  void set_methods(MethodFlags f) { flags_ = f; }
+  MethodFlags methods() const { return flags_; }
+  bool any_methods(MethodFlags m) const { return (m && flags_); }
+  void set_placement(PlacementStrategy s) { strategy_ = s; }
+  void set_gpus(const std::vector<int> &gpus) { gpus_ = gpus; }
+  const std::vector<int> &gpus() const { return gpus_; }
+  void set_backend(Backend b) { backend_ = b; backendSet_ = true; }
+  Backend backend() const { return backend_; }
+  // write plan_<rank>.txt during realize (reference src/stencil.cu:259-353); default on, off with STENCIL_PLAN_FILE=0
+  void set_plan_file(const std::string &prefix) { planPrefix_ = prefix; }
+  void set_padding(bool p) { pad_ = p; }
+
+  void realize();
+  bool realized() const { return realized_; }
+
+  // ---- queries ----
+  const Dim3 &size() const { return size_; }
+  int rank() const { return pg_->rank(); }
+  int world_size() const { return pg_->size(); }
+  comm::ProcGroup &group() { return *pg_; }
+  std::vector<LocalDomain> &domains() { return domains_; }
+  const std::vector<LocalDomain> &domains() const { return domains_; }
+  const Dim3 &get_origin(int64_t i) const { return domains_.at(size_t(i)).origin(); }
+  Rect3 get_compute_region() const { return Rect3(Dim3(0, 0, 0), size_); }
+  std::vector<Rect3> get_interior() const;
+  std::vector<std::vector<Rect3>> get_exterior() const;
+  const Placement &placement() const { return *placement_; }
+  Dim3 subdomain_idx(int64_t di) const { return placement_->get_idx(rank(), int(di)); }
+  uint64_t exchange_bytes_for_method(MethodFlags m) const; // summed over all ranks, per exchange
+  const std::vector<ExchangePlanEntry> &plan() const { return plan_; }
+  std::string plan_summary() const;
+
+  // ---- exchange ----
+  void exchange();       // blocking: returns when every halo of every local domain is valid
+  void exchange_async(); // enqueue on the comm streams; only the staged (host) path blocks the caller
+  // make the next exchange wait for the work currently enqueued on `s` (which touches domain di)
+  void record_ready(size_t di, hipStream_t s);
+  // make `s` wait until the halos of domain di from the last exchange are written
+  void wait_exchange(size_t di, hipStream_t s);
+  // block the host until the last exchange is complete (checks device-side timeouts)
+  void sync_exchange();
+  hipStream_t comm_stream(size_t di) const;
+  void swap();
+
+  // ---- output ----
+  void write_paraview(const std::string &prefix, bool zeroNaNs = false);
+
+  // ---- setup / exchange timers (max over ranks, seconds), reference stencil.hpp:106-131 ----
+  double timeMpiTopo_ = 0, timeNodeGpus_ = 0, timePeerEn_ = 0, timePlacement_ = 0, timePlan_ = 0, timeRealize_ = 0,
+         timeCreate_ = 0;
+  double timeExchange_ = 0, timeSwap_ = 0;
+  bool exchangeStats_ = false; // STENCIL_EXCHANGE_STATS=1: barrier + time every exchange/swap
+
+  struct Impl;
+
+private:
+  Dim3 size_;
+  std::shared_ptr<comm::ProcGroup> pg_;
+  Radius radius_;
+  std::vector<int> gpus_;
+  std::vector<int64_t> elemSize_;
+  std::vector<std::string> names_;
+  std::vector<DType> dtypes_;
+  MethodFlags flags_ = MethodFlags::All;
+  PlacementStrategy strategy_ = PlacementStrategy::NodeAware;
+  Backend backend_ = Backend::Device;
+  bool backendSet_ = false;
+  bool realized_ = false;
+  bool pad_ = true;
+  std::string planPrefix_ = "plan";
+  std::unique_ptr<Placement> placement_;
+  std::vector<LocalDomain> domains_;
+  std::vector<ExchangePlanEntry> plan_;
+  std::array<uint64_t, 5> bytesPerMethod_{}; // indexed by log2(method)
+  std::unique_ptr<Impl> impl_;
+};
+
+} // namespace stencil

@@ -1,0 +1,67 @@
+#pragma once
+// Descriptor-driven strided box copies: the single primitive behind pack, unpack, same-GPU translate,
+// direct xGMI peer stores and region->host dumps.
+//
+// Reference equivalents (one CUDA launch per message, make_block_dim shapes, per-element memcpy fallback):
+//   grid_pack/pack_kernel        include/stencil/pack_kernel.cuh:5-46
+//   unpack/translate/multi_*     include/stencil/copy.cuh:13-145
+//   dev_packer_pack_domain       include/stencil/packer.cuh:52-69
+//   dev_unpacker_unpack_domain   include/stencil/packer.cuh:233-250
+// Here every message x quantity of one exchange step becomes one CopySeg and ONE launch walks them all:
+// rows are split into the widest aligned vector unit (16/8/4/2/1 B) so face copies move 1 KiB per wave
+// instruction, and the launch is sized for the whole chip (>= 2 waves/SIMD) instead of per-message blocks.
+#include <cstdint>
+#include <vector>
+
+#include "stencil/core/geometry.hpp"
+
+#if defined(__HIPCC__) || defined(__HIP_PLATFORM_AMD__)
+#include <hip/hip_runtime_api.h>
+#else
+#include <hip/hip_runtime_api.h>
+#endif
+
+namespace stencil {
+
+// Address of element (x,y,z) of a strided box: base + x*elem + y*ystride + z*zstride (bytes).
+struct StridedBox {
+  char *base = nullptr;
+  int64_t ystride = 0;
+  int64_t zstride = 0;
+};
+
+struct CopySeg {
+  char *src;
+  char *dst;
+  int64_t src_ystride, src_zstride;
+  int64_t dst_ystride, dst_zstride;
+  uint32_t row_units; // vector units per row
+  uint32_t ny;        // rows per z-plane
+  uint32_t vec;       // bytes per unit (16, 8, 4, 2 or 1)
+  uint32_t pad_;
+  uint64_t unit_begin; // exclusive prefix sum of units over previous segments
+  uint64_t units;      // row_units * ny * nz
+};
+
+// Build a segment copying a box of extent `ext` elements of `elemSize` bytes.
+CopySeg make_copy_seg(const StridedBox &src, const StridedBox &dst, const Dim3 &ext, int64_t elemSize);
+
+// Assign unit_begin prefix sums; returns total units.
+uint64_t finalize_segs(std::vector<CopySeg> &segs);
+
+// Host execution (CPU backend and reference for tests).
+void copy_segs_host(const std::vector<CopySeg> &segs);
+
+// Device execution. `dsegs` is a device-resident copy of the finalized segment list.
+void copy_segs_device(const CopySeg *dsegs, int nsegs, uint64_t totalUnits, hipStream_t stream);
+
+// ---- cross-process signalling for the IPC transport (device flags, see DistributedDomain colocated path) ----
+// Lane i polls *flags[i] (relaxed, system scope, s_sleep back-off) until >= target, then one system-scope
+// acquire. A bounded spin: on timeout it stores `code` into *err (host-mapped) and exits, so the grid always drains.
+void wait_flags_device(const std::vector<uint64_t *> &flags, uint64_t target, int *err, int code, double timeout_s,
+                       hipStream_t stream);
+// System-scope release, then lane i stores *flags[i] = value (flags may be IPC-mapped peer memory).
+void signal_flags_device(const std::vector<uint64_t *> &flags, uint64_t value, hipStream_t stream);
+constexpr int kMaxFlagsPerLaunch = 64;
+
+} // namespace stencil

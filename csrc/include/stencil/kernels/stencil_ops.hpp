@@ -1,0 +1,60 @@
+#pragma once
+// Compute kernels of the reference apps, written for CDNA4.
+// Reference kernels:
+//   Jacobi3D  init_kernel / stencil_kernel (6-neighbour mean + hot/cold spheres)   bin/jacobi3d.cu:18-87
+//   Astaroth  init_kernel (sin wave, halo -10) / stencil_kernel (6-neighbour mean)  bin/astaroth_sim.cu:14-83
+// The device kernel is a 2.5D z-march: each lane owns one 16-B x-chunk (4 fp32 / 2 fp64) of TY consecutive rows and
+// walks z keeping planes z-1, z, z+1 in registers, so every interior cell is read from HBM ~once per sweep
+// (y-halo rows are shared through L1/L2 by the 4 waves of a block, x-neighbours come from adjacent lanes by
+// ds_bpermute). Blocks are remapped XCD-aware so y/z-adjacent tiles share an XCD's L2. Summation order and the
+// division by 6 are the reference's, so results are bitwise identical to a sequential fp32 evaluation.
+#include <cstdint>
+
+#include "stencil/core/geometry.hpp"
+#include "stencil/domain/local_domain.hpp"
+
+namespace stencil {
+
+enum class StencilKind : int {
+  Jacobi = 0,   // sum order +x,-x,+y,-y,+z,-z then /6, hot/cold spheres
+  Astaroth = 1, // sum order -x,-y,-z,+x,+y,+z then /6
+};
+
+struct Spheres {
+  bool enabled = false;
+  Dim3 hot, cold;     // global coordinates of the sphere centres
+  int64_t radius = 0; // cell is inside iff floor(sqrt(|p-c|^2)) <= radius  <=>  |p-c|^2 < (radius+1)^2
+  // reference placement (bin/jacobi3d.cu:45-50) for a global compute region
+  static Spheres jacobi(const Rect3 &cReg) {
+    Spheres s;
+    s.enabled = true;
+    s.hot = Dim3(cReg.lo.x + (cReg.hi.x - cReg.lo.x) / 3, (cReg.lo.y + cReg.hi.y) / 2, (cReg.lo.z + cReg.hi.z) / 2);
+    s.cold = Dim3(cReg.lo.x + (cReg.hi.x - cReg.lo.x) * 2 / 3, (cReg.lo.y + cReg.hi.y) / 2, (cReg.lo.z + cReg.hi.z) / 2);
+    s.radius = (cReg.hi.x - cReg.lo.x) / 10;
+    return s;
+  }
+};
+
+struct StencilTune {
+  int ty = 8;     // rows per lane (4 or 8)
+  int zchunk = 0; // planes per block (0 = auto)
+  bool xcdRemap = true;
+  bool nontemporal = true;
+};
+
+// dst(region) = stencil(src) for one quantity of one LocalDomain. `region` is in global coordinates and must lie in
+// the domain's compute region; face radii must be >= 1. `currIsSrc` selects curr->next (true) or next->curr.
+void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
+                    hipStream_t stream, const StencilTune &tune = StencilTune());
+// same for several regions in one call (e.g. the exterior slabs)
+void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
+                            const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());
+
+// Jacobi init: curr = 0.5 on `region` (reference bin/jacobi3d.cu:18-29)
+void jacobi_init(const LocalDomain &dom, int64_t qi, const Rect3 &region, hipStream_t stream);
+// Astaroth init: interior = sin(2*pi/period*(origin+x+y+z)) (x,y,z raw indices), halo = -10 (astaroth_sim.cu:14-61)
+void astaroth_init(const LocalDomain &dom, int64_t qi, double period, hipStream_t stream);
+// fill every cell of the full region (halo included) of curr with a value
+void fill_value(const LocalDomain &dom, int64_t qi, double value, bool curr, hipStream_t stream);
+
+} // namespace stencil

@@ -1,0 +1,65 @@
+#pragma once
+// Iterated 7-point stencil applications on a DistributedDomain: the Jacobi3D and Astaroth-proxy "models".
+// Reference apps: bin/jacobi3d.cu:89-385 (hot loop :265-346) and bin/astaroth_sim.cu:150-284.
+//
+// One step() (overlap mode) is fully stream-ordered, no host synchronisation:
+//   compute[d]: interior(curr -> next)                               (overlaps the exchange)
+//   comm[dev] : exchange(curr halos)  after ready[d] of the previous step
+//   compute[d]: wait(exchange done) -> exterior slabs(curr -> next) -> record ready
+//   host      : swap curr/next pointers
+// The reference instead host-synchronises every compute stream each iteration (jacobi3d.cu:331-337).
+#include <memory>
+#include <vector>
+
+#include "stencil/domain/distributed_domain.hpp"
+#include "stencil/kernels/stencil_ops.hpp"
+
+namespace stencil {
+
+struct StencilModelConfig {
+  Dim3 size{512, 512, 512};
+  StencilKind kind = StencilKind::Jacobi;
+  int64_t radius = 1;          // face radius (Jacobi 1; Astaroth 3 in all 26 directions)
+  bool allDirections = false;  // true: radius in all 26 directions (Astaroth), false: faces only (Jacobi)
+  int quantities = 1;
+  bool fp64 = false;
+  MethodFlags methods = MethodFlags::All;
+  PlacementStrategy placement = PlacementStrategy::NodeAware;
+  std::vector<int> gpus;       // empty = automatic
+  bool overlap = true;
+  bool setBackend = false;
+  Backend backend = Backend::Device;
+  StencilTune tune;
+  double astarothPeriod = 10.0;
+};
+
+class StencilModel {
+public:
+  explicit StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::ProcGroup> pg = nullptr);
+  ~StencilModel();
+
+  void init();                  // realize + initial condition; blocks until done
+  void step();                  // one iteration, asynchronous
+  void run(int iters) {
+    for (int i = 0; i < iters; ++i) step();
+  }
+  void synchronize();           // wait for all enqueued work (and check exchange errors)
+  DistributedDomain &domain() { return *dd_; }
+  const StencilModelConfig &config() const { return cfg_; }
+  int64_t cells() const { return cfg_.size.flatten(); } // global cells updated per step
+  int64_t local_cells() const;
+  hipStream_t compute_stream(size_t di) const;
+  int64_t steps_done() const { return steps_; }
+  const Spheres &spheres() const { return sph_; }
+
+private:
+  StencilModelConfig cfg_;
+  std::unique_ptr<DistributedDomain> dd_;
+  std::vector<Stream> compute_;
+  std::vector<Rect3> interiors_;
+  std::vector<std::vector<Rect3>> exteriors_;
+  Spheres sph_;
+  int64_t steps_ = 0;
+};
+
+} // namespace stencil

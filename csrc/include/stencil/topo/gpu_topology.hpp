@@ -1,0 +1,33 @@
+#pragma once
+// GPU topology: distance/bandwidth between devices and peer-access management.
+// Parity: reference include/stencil/gpu_topology.hpp + src/gpu_topology.cpp:17-139
+//   (NVML distance: same 0.1, NVLink 1, PCIe levels 2-7; bandwidth = 1/distance; cached enable_peer / peer).
+// MI355X: the link type and hop count come from hipExtGetLinkTypeAndHopCount (xGMI vs PCIe), so a fully
+// connected 8-GPU xGMI node is a uniform mesh: distance 1.0 for every pair, 0.1 for self.
+#include <string>
+#include <vector>
+
+namespace stencil {
+namespace gpu_topo {
+
+int device_count(); // 0 when no GPU runtime/device is present
+
+// relative distance between two devices of this node (smaller is closer)
+double distance(int src, int dst);
+inline double bandwidth(int src, int dst) { return 1.0 / distance(src, dst); }
+
+// try to enable peer access src->dst (cached). Returns whether src can access dst memory.
+bool enable_peer(int src, int dst);
+// cached answer of enable_peer (enables on first use)
+bool peer(int src, int dst);
+
+struct LinkInfo {
+  int src, dst;
+  std::string type; // "self", "xgmi", "pcie", "unknown"
+  int hops;
+  double distance;
+};
+std::vector<LinkInfo> links();
+
+} // namespace gpu_topo
+} // namespace stencil

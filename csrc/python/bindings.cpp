@@ -1,0 +1,546 @@
+// pybind11 bindings for stencil2_amd (module stencil2_amd._C).
+// Quantity buffers are exported zero-copy as DLPack capsules (kDLROCM device tensors, or kDLCPU for the host
+// backend) so Python sees torch tensors aliasing the runtime's halo-padded allocations.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "stencil/comm/proc_group.hpp"
+#include "stencil/domain/distributed_domain.hpp"
+#include "stencil/kernels/copy.hpp"
+#include "stencil/kernels/stencil_ops.hpp"
+#include "stencil/models/stencil_model.hpp"
+#include "stencil/rt/statistics.hpp"
+#include "stencil/topo/gpu_topology.hpp"
+#include "stencil/topo/partition.hpp"
+#include "stencil/topo/placement.hpp"
+#include "stencil/topo/qap.hpp"
+
+namespace py = pybind11;
+using namespace stencil;
+
+// ---------------- minimal DLPack ABI (v0.8) ----------------
+extern "C" {
+struct DLDevice {
+  int32_t device_type;
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code;
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void *data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t *shape;
+  int64_t *strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void *manager_ctx;
+  void (*deleter)(DLManagedTensor *self);
+};
+}
+static constexpr int32_t kDLCPU = 1, kDLROCM = 10;
+
+struct DLCtx {
+  std::shared_ptr<void> keepAlive;
+  int64_t shape[3];
+  int64_t strides[3];
+};
+
+static DLDataType dl_dtype(DType t, int64_t es) {
+  switch (t) {
+  case DType::F32:
+    return {2, 32, 1};
+  case DType::F64:
+    return {2, 64, 1};
+  case DType::F16:
+    return {2, 16, 1};
+  case DType::BF16:
+    return {4, 16, 1};
+  case DType::I32:
+    return {0, 32, 1};
+  case DType::I64:
+    return {0, 64, 1};
+  case DType::I8:
+    return {0, 8, 1};
+  case DType::U8:
+    return {1, 8, 1};
+  case DType::U32:
+    return {1, 32, 1};
+  case DType::U64:
+    return {1, 64, 1};
+  default:
+    return {1, uint8_t(8 * es), 1};
+  }
+}
+
+static py::capsule make_capsule(std::shared_ptr<void> keep, const LocalDomain &d, int64_t qi, bool curr) {
+  auto *mt = new DLManagedTensor();
+  auto *ctx = new DLCtx();
+  ctx->keepAlive = std::move(keep);
+  const Dim3 raw = d.raw_size(), p = d.pitch(qi);
+  ctx->shape[0] = raw.z;
+  ctx->shape[1] = raw.y;
+  ctx->shape[2] = raw.x;
+  ctx->strides[0] = p.x * p.y;
+  ctx->strides[1] = p.x;
+  ctx->strides[2] = 1;
+  mt->dl_tensor.data = curr ? d.curr_data(qi) : d.next_data(qi);
+  mt->dl_tensor.device = d.backend() == Backend::Device ? DLDevice{kDLROCM, d.gpu()} : DLDevice{kDLCPU, 0};
+  mt->dl_tensor.ndim = 3;
+  mt->dl_tensor.dtype = dl_dtype(d.dtype(qi), d.elem_size(qi));
+  if (d.dtype(qi) == DType::Bytes && d.elem_size(qi) > 8) {
+    // opaque element: expose as bytes with an extra trailing dimension is not expressible in 3D; refuse
+    throw std::runtime_error("cannot export opaque element types wider than 8 bytes");
+  }
+  mt->dl_tensor.shape = ctx->shape;
+  mt->dl_tensor.strides = ctx->strides;
+  mt->dl_tensor.byte_offset = 0;
+  mt->manager_ctx = ctx;
+  mt->deleter = [](DLManagedTensor *self) {
+    delete static_cast<DLCtx *>(self->manager_ctx);
+    delete self;
+  };
+  return py::capsule(mt, "dltensor", [](PyObject *cap) {
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto *m = static_cast<DLManagedTensor *>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (m && m->deleter) m->deleter(m);
+    }
+  });
+}
+
+static Dim3 to_dim3(py::handle h) {
+  if (py::isinstance<Dim3>(h)) return h.cast<Dim3>();
+  auto t = h.cast<std::vector<int64_t>>();
+  if (t.size() != 3) throw std::runtime_error("expected 3 coordinates");
+  return Dim3(t[0], t[1], t[2]);
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "stencil2_amd native runtime (HIP/gfx950)";
+  py::register_exception<stencil::Error>(m, "StencilError", PyExc_RuntimeError);
+
+  py::class_<Dim3>(m, "Dim3")
+      .def(py::init<>())
+      .def(py::init<int64_t, int64_t, int64_t>())
+      .def_readwrite("x", &Dim3::x)
+      .def_readwrite("y", &Dim3::y)
+      .def_readwrite("z", &Dim3::z)
+      .def("flatten", &Dim3::flatten)
+      .def("wrap", &Dim3::wrap)
+      .def("max", &Dim3::max)
+      .def("min", &Dim3::min)
+      .def("__add__", [](const Dim3 &a, const Dim3 &b) { return a + b; })
+      .def("__sub__", [](const Dim3 &a, const Dim3 &b) { return a - b; })
+      .def("__mul__", [](const Dim3 &a, const Dim3 &b) { return a * b; })
+      .def("__mul__", [](const Dim3 &a, int64_t s) { return a * s; })
+      .def("__floordiv__", [](const Dim3 &a, const Dim3 &b) { return a / b; })
+      .def("__mod__", [](const Dim3 &a, const Dim3 &b) { return a % b; })
+      .def("__neg__", [](const Dim3 &a) { return -a; })
+      .def("__eq__", [](const Dim3 &a, const Dim3 &b) { return a == b; })
+      .def("__ne__", [](const Dim3 &a, const Dim3 &b) { return a != b; })
+      .def("__lt__", [](const Dim3 &a, const Dim3 &b) { return a < b; })
+      .def("__hash__", [](const Dim3 &a) { return py::hash(py::make_tuple(a.x, a.y, a.z)); })
+      .def("__iter__", [](const Dim3 &a) { return py::iter(py::make_tuple(a.x, a.y, a.z)); })
+      .def("tolist", [](const Dim3 &a) { return std::vector<int64_t>{a.x, a.y, a.z}; })
+      .def("__repr__", [](const Dim3 &a) {
+        return "Dim3(" + std::to_string(a.x) + ", " + std::to_string(a.y) + ", " + std::to_string(a.z) + ")";
+      });
+  py::implicitly_convertible<py::tuple, Dim3>();
+  py::implicitly_convertible<py::list, Dim3>();
+
+  py::class_<Rect3>(m, "Rect3")
+      .def(py::init<>())
+      .def(py::init<Dim3, Dim3>())
+      .def_readwrite("lo", &Rect3::lo)
+      .def_readwrite("hi", &Rect3::hi)
+      .def("extent", &Rect3::extent)
+      .def("empty", &Rect3::empty)
+      .def("contains", &Rect3::contains)
+      .def("__eq__", [](const Rect3 &a, const Rect3 &b) { return a == b; })
+      .def("__repr__", [](const Rect3 &r) {
+        std::ostringstream s;
+        s << "Rect3(" << r.lo << ", " << r.hi << ")";
+        return s.str();
+      });
+
+  py::class_<Radius>(m, "Radius")
+      .def(py::init<>())
+      .def_static("constant", &Radius::constant)
+      .def_static("face_edge_corner", &Radius::face_edge_corner)
+      .def("dir", [](const Radius &r, int x, int y, int z) { return r.dir(x, y, z); })
+      .def("set_dir", [](Radius &r, int x, int y, int z, int64_t v) { r.dir(x, y, z) = v; })
+      .def("x", &Radius::x)
+      .def("y", &Radius::y)
+      .def("z", &Radius::z)
+      .def("set_face", &Radius::set_face)
+      .def("set_edge", &Radius::set_edge)
+      .def("set_corner", &Radius::set_corner)
+      .def("max", &Radius::max)
+      .def("__eq__", [](const Radius &a, const Radius &b) { return a == b; })
+      .def("__copy__", [](const Radius &r) { return Radius(r); });
+
+  py::enum_<MethodFlags>(m, "MethodFlags", py::arithmetic())
+      .value("None_", MethodFlags::None)
+      .value("Staged", MethodFlags::Staged)
+      .value("Rccl", MethodFlags::Rccl)
+      .value("Colocated", MethodFlags::Colocated)
+      .value("PeerCopy", MethodFlags::PeerCopy)
+      .value("Kernel", MethodFlags::Kernel)
+      .value("All", MethodFlags::All)
+      .def("__or__", [](MethodFlags a, MethodFlags b) { return a | b; })
+      .def("__and__", [](MethodFlags a, MethodFlags b) { return a & b; });
+  m.def("methods_to_string", [](MethodFlags f) { return to_string(f); });
+  py::enum_<PlacementStrategy>(m, "PlacementStrategy")
+      .value("NodeAware", PlacementStrategy::NodeAware)
+      .value("Trivial", PlacementStrategy::Trivial);
+  py::enum_<Backend>(m, "Backend").value("Host", Backend::Host).value("Device", Backend::Device);
+  py::enum_<DType>(m, "DType")
+      .value("Bytes", DType::Bytes)
+      .value("F32", DType::F32)
+      .value("F64", DType::F64)
+      .value("I32", DType::I32)
+      .value("I64", DType::I64)
+      .value("U8", DType::U8)
+      .value("I8", DType::I8)
+      .value("F16", DType::F16)
+      .value("BF16", DType::BF16)
+      .value("U32", DType::U32)
+      .value("U64", DType::U64);
+  py::enum_<StencilKind>(m, "StencilKind").value("Jacobi", StencilKind::Jacobi).value("Astaroth", StencilKind::Astaroth);
+
+  // ---------------- process group ----------------
+  py::class_<comm::ProcGroup, std::shared_ptr<comm::ProcGroup>>(m, "ProcGroup")
+      .def("rank", &comm::ProcGroup::rank)
+      .def("size", &comm::ProcGroup::size)
+      .def("hostname", &comm::ProcGroup::hostname)
+      .def("barrier", &comm::ProcGroup::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_max", &comm::ProcGroup::allreduce_max, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_sum", &comm::ProcGroup::allreduce_sum, py::call_guard<py::gil_scoped_release>())
+      .def("colocated_ranks", &comm::ProcGroup::colocated_ranks)
+      .def("colocated_rank", &comm::ProcGroup::colocated_rank)
+      .def("colocated_size", &comm::ProcGroup::colocated_size)
+      .def("num_nodes", &comm::ProcGroup::num_nodes)
+      .def("send_bytes",
+           [](comm::ProcGroup &g, int dst, uint32_t tag, py::bytes b) {
+             std::string s = b;
+             py::gil_scoped_release r;
+             g.send(dst, tag, s.data(), s.size());
+           })
+      .def("recv_bytes",
+           [](comm::ProcGroup &g, int src, uint32_t tag, size_t n) {
+             std::string s(n, '\0');
+             {
+               py::gil_scoped_release r;
+               g.recv(src, tag, &s[0], n);
+             }
+             return py::bytes(s);
+           })
+      .def("allgather_bytes", [](comm::ProcGroup &g, py::bytes b) {
+        std::string s = b;
+        std::string out(s.size() * size_t(g.size()), '\0');
+        {
+          py::gil_scoped_release r;
+          g.allgather(s.data(), s.size(), &out[0]);
+        }
+        py::list l;
+        for (int i = 0; i < g.size(); ++i) l.append(py::bytes(out.substr(i * s.size(), s.size())));
+        return l;
+      });
+  m.def("make_single_group", &comm::make_single_group);
+  m.def("make_tcp_group", &comm::make_tcp_group, py::arg("rank"), py::arg("size"), py::arg("master_addr"),
+        py::arg("master_port"), py::arg("timeout_s") = 600.0, py::call_guard<py::gil_scoped_release>());
+  m.def("make_group_from_env", &comm::make_group_from_env, py::call_guard<py::gil_scoped_release>());
+  m.def("default_group", &comm::default_group, py::call_guard<py::gil_scoped_release>());
+  m.def("set_default_group", &comm::set_default_group);
+  m.def("find_free_port", &comm::find_free_port);
+
+  // ---------------- topology / placement ----------------
+  m.def("prime_factors", &prime_factors_desc);
+  py::class_<RankPartition>(m, "RankPartition")
+      .def(py::init<const Dim3 &, int64_t>())
+      .def("dim", &RankPartition::dim)
+      .def("subdomain_size", &RankPartition::subdomain_size)
+      .def("subdomain_origin", &RankPartition::subdomain_origin)
+      .def("linearize", &RankPartition::linearize)
+      .def("dimensionize", &RankPartition::dimensionize);
+  py::class_<NodePartition>(m, "NodePartition")
+      .def(py::init<const Dim3 &, const Radius &, int64_t, int64_t>())
+      .def("dim", &NodePartition::dim)
+      .def("sys_dim", &NodePartition::sys_dim)
+      .def("node_dim", &NodePartition::node_dim)
+      .def("subdomain_size", &NodePartition::subdomain_size)
+      .def("subdomain_origin", &NodePartition::subdomain_origin)
+      .def("global_idx", &NodePartition::global_idx);
+  py::class_<Placement>(m, "Placement")
+      .def("get_idx", &Placement::get_idx)
+      .def("get_rank", &Placement::get_rank)
+      .def("get_subdomain_id", &Placement::get_subdomain_id)
+      .def("get_device", &Placement::get_device)
+      .def("subdomain_size", &Placement::subdomain_size)
+      .def("subdomain_origin", &Placement::subdomain_origin)
+      .def("dim", &Placement::dim);
+  py::class_<TrivialPlacement, Placement>(m, "TrivialPlacement")
+      .def(py::init([](const Dim3 &size, std::shared_ptr<comm::ProcGroup> pg, const std::vector<int> &devs) {
+             return new TrivialPlacement(size, *pg, devs);
+           }),
+           py::keep_alive<1, 3>());
+  py::class_<NodeAwarePlacement, Placement>(m, "NodeAwarePlacement")
+      .def(py::init([](const Dim3 &size, std::shared_ptr<comm::ProcGroup> pg, const Radius &r,
+                       const std::vector<int> &devs, std::function<double(int, int)> bw) {
+             return new NodeAwarePlacement(size, *pg, r, devs, bw);
+           }),
+           py::keep_alive<1, 3>());
+  m.def("halo_volume", &halo_volume);
+  m.def("qap_solve", [](const std::vector<std::vector<double>> &w, const std::vector<std::vector<double>> &d) {
+    Mat2D<double> W, D;
+    for (auto &r : w) W.push_back(r);
+    for (auto &r : d) D.push_back(r);
+    double c = 0;
+    auto f = qap::solve(W, D, &c);
+    return py::make_tuple(f, c);
+  });
+  m.def("qap_solve_catch", [](const std::vector<std::vector<double>> &w, const std::vector<std::vector<double>> &d) {
+    Mat2D<double> W, D;
+    for (auto &r : w) W.push_back(r);
+    for (auto &r : d) D.push_back(r);
+    double c = 0;
+    auto f = qap::solve_catch(W, D, &c);
+    return py::make_tuple(f, c);
+  });
+  m.def("qap_cost", [](const std::vector<std::vector<double>> &w, const std::vector<std::vector<double>> &d,
+                       const std::vector<size_t> &f) {
+    Mat2D<double> W, D;
+    for (auto &r : w) W.push_back(r);
+    for (auto &r : d) D.push_back(r);
+    return qap::detail::cost(W, D, f);
+  });
+  m.def("make_reciprocal", [](const std::vector<std::vector<double>> &w) {
+    Mat2D<double> W;
+    for (auto &r : w) W.push_back(r);
+    Mat2D<double> R = make_reciprocal(W);
+    std::vector<std::vector<double>> out(R.rows(), std::vector<double>(R.cols()));
+    for (size_t i = 0; i < R.rows(); ++i)
+      for (size_t j = 0; j < R.cols(); ++j) out[i][j] = R.at(i, j);
+    return out;
+  });
+  m.def("device_count", &gpu_topo::device_count);
+  m.def("gpu_distance", &gpu_topo::distance);
+  m.def("gpu_bandwidth", &gpu_topo::bandwidth);
+  m.def("enable_peer", &gpu_topo::enable_peer);
+  m.def("gpu_links", []() {
+    py::list l;
+    for (auto &li : gpu_topo::links())
+      l.append(py::dict(py::arg("src") = li.src, py::arg("dst") = li.dst, py::arg("type") = li.type,
+                        py::arg("hops") = li.hops, py::arg("distance") = li.distance));
+    return l;
+  });
+
+  // ---------------- statistics ----------------
+  py::class_<Statistics>(m, "Statistics")
+      .def(py::init<>())
+      .def("insert", &Statistics::insert)
+      .def("count", &Statistics::count)
+      .def("avg", &Statistics::avg)
+      .def("min", &Statistics::min)
+      .def("max", &Statistics::max)
+      .def("trimean", &Statistics::trimean)
+      .def("med", &Statistics::med)
+      .def("stddev", &Statistics::stddev);
+
+  // ---------------- LocalDomain (owned by DistributedDomain; exposed by reference) ----------------
+  py::class_<LocalDomain>(m, "LocalDomain")
+      .def("size", &LocalDomain::size)
+      .def("origin", &LocalDomain::origin)
+      .def("radius", &LocalDomain::radius)
+      .def("gpu", &LocalDomain::gpu)
+      .def("backend", &LocalDomain::backend)
+      .def("num_data", &LocalDomain::num_data)
+      .def("elem_size", &LocalDomain::elem_size)
+      .def("dtype", &LocalDomain::dtype)
+      .def("name", &LocalDomain::name)
+      .def("raw_size", &LocalDomain::raw_size)
+      .def("pitch", &LocalDomain::pitch)
+      .def("pad_x", &LocalDomain::pad_x)
+      .def("get_compute_region", &LocalDomain::get_compute_region)
+      .def("get_full_region", &LocalDomain::get_full_region)
+      .def("halo_pos", &LocalDomain::halo_pos)
+      .def("halo_coords", &LocalDomain::halo_coords)
+      .def("halo_extent", py::overload_cast<const Dim3 &>(&LocalDomain::halo_extent, py::const_))
+      .def("halo_bytes", &LocalDomain::halo_bytes)
+      .def("accessor_origin", &LocalDomain::accessor_origin)
+      .def("parity", &LocalDomain::parity)
+      .def("curr_ptr", [](const LocalDomain &d, int64_t q) { return reinterpret_cast<uintptr_t>(d.curr_data(q)); })
+      .def("next_ptr", [](const LocalDomain &d, int64_t q) { return reinterpret_cast<uintptr_t>(d.next_data(q)); })
+      .def("region_to_host",
+           [](const LocalDomain &d, const Dim3 &pos, const Dim3 &ext, int64_t q, bool curr) {
+             auto v = d.region_to_host(pos, ext, q, curr);
+             return py::bytes(reinterpret_cast<const char *>(v.data()), v.size());
+           },
+           py::arg("pos"), py::arg("ext"), py::arg("qi"), py::arg("curr") = true)
+      .def("region_from_host",
+           [](LocalDomain &d, const Dim3 &pos, const Dim3 &ext, int64_t q, py::bytes b, bool curr) {
+             std::string s = b;
+             STENCIL_REQUIRE(int64_t(s.size()) == ext.flatten() * d.elem_size(q), "byte count mismatch");
+             d.region_from_host(pos, ext, q, s.data(), curr);
+           },
+           py::arg("pos"), py::arg("ext"), py::arg("qi"), py::arg("data"), py::arg("curr") = true)
+      .def("interior_to_host", [](const LocalDomain &d, int64_t q) {
+        auto v = d.interior_to_host(q);
+        return py::bytes(reinterpret_cast<const char *>(v.data()), v.size());
+      })
+      .def("quantity_to_host", [](const LocalDomain &d, int64_t q) {
+        auto v = d.quantity_to_host(q);
+        return py::bytes(reinterpret_cast<const char *>(v.data()), v.size());
+      })
+      .def("fill_bytes", &LocalDomain::fill_bytes);
+
+  // ---------------- DistributedDomain ----------------
+  py::class_<ExchangePlanEntry>(m, "ExchangePlanEntry")
+      .def_readonly("method", &ExchangePlanEntry::method)
+      .def_readonly("src_idx", &ExchangePlanEntry::srcIdx)
+      .def_readonly("dst_idx", &ExchangePlanEntry::dstIdx)
+      .def_readonly("src_rank", &ExchangePlanEntry::srcRank)
+      .def_readonly("dst_rank", &ExchangePlanEntry::dstRank)
+      .def_readonly("src_dev", &ExchangePlanEntry::srcDev)
+      .def_readonly("dst_dev", &ExchangePlanEntry::dstDev)
+      .def_readonly("dir", &ExchangePlanEntry::dir)
+      .def_readonly("bytes", &ExchangePlanEntry::bytes);
+
+  py::class_<DistributedDomain, std::shared_ptr<DistributedDomain>>(m, "DistributedDomain")
+      .def(py::init([](int64_t x, int64_t y, int64_t z, std::shared_ptr<comm::ProcGroup> pg) {
+             py::gil_scoped_release r;
+             return std::make_shared<DistributedDomain>(x, y, z, pg);
+           }),
+           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("group") = nullptr)
+      .def("set_radius", py::overload_cast<int64_t>(&DistributedDomain::set_radius))
+      .def("set_radius", py::overload_cast<const Radius &>(&DistributedDomain::set_radius))
+      .def("radius", &DistributedDomain::radius)
+      .def("add_data",
+           [](DistributedDomain &d, int64_t es, const std::string &name, DType dt) { return d.add_data(es, name, dt); },
+           py::arg("elem_size"), py::arg("name") = "", py::arg("dtype") = DType::Bytes)
+      .def("set_methods", &DistributedDomain::set_methods)
+      .def("methods", &DistributedDomain::methods)
+      .def("set_placement", &DistributedDomain::set_placement)
+      .def("set_gpus", &DistributedDomain::set_gpus)
+      .def("gpus", &DistributedDomain::gpus)
+      .def("set_backend", &DistributedDomain::set_backend)
+      .def("backend", &DistributedDomain::backend)
+      .def("set_plan_file", &DistributedDomain::set_plan_file)
+      .def("set_padding", &DistributedDomain::set_padding)
+      .def("realize", &DistributedDomain::realize, py::call_guard<py::gil_scoped_release>())
+      .def("realized", &DistributedDomain::realized)
+      .def("size", &DistributedDomain::size)
+      .def("rank", &DistributedDomain::rank)
+      .def("world_size", &DistributedDomain::world_size)
+      .def("num_domains", [](DistributedDomain &d) { return d.domains().size(); })
+      .def("domain", [](DistributedDomain &d, size_t i) -> LocalDomain & { return d.domains().at(i); },
+           py::return_value_policy::reference_internal)
+      .def("get_origin", &DistributedDomain::get_origin)
+      .def("get_compute_region", &DistributedDomain::get_compute_region)
+      .def("get_interior", &DistributedDomain::get_interior)
+      .def("get_exterior", &DistributedDomain::get_exterior)
+      .def("subdomain_idx", &DistributedDomain::subdomain_idx)
+      .def("placement_dim", [](DistributedDomain &d) { return d.placement().dim(); })
+      .def("exchange_bytes_for_method", &DistributedDomain::exchange_bytes_for_method)
+      .def("plan", &DistributedDomain::plan)
+      .def("plan_summary", &DistributedDomain::plan_summary)
+      .def("exchange", &DistributedDomain::exchange, py::call_guard<py::gil_scoped_release>())
+      .def("exchange_async", &DistributedDomain::exchange_async, py::call_guard<py::gil_scoped_release>())
+      .def("sync_exchange", &DistributedDomain::sync_exchange, py::call_guard<py::gil_scoped_release>())
+      .def("record_ready",
+           [](DistributedDomain &d, size_t di, uintptr_t s) { d.record_ready(di, reinterpret_cast<hipStream_t>(s)); })
+      .def("wait_exchange",
+           [](DistributedDomain &d, size_t di, uintptr_t s) { d.wait_exchange(di, reinterpret_cast<hipStream_t>(s)); })
+      .def("comm_stream", [](DistributedDomain &d, size_t di) { return reinterpret_cast<uintptr_t>(d.comm_stream(di)); })
+      .def("swap", &DistributedDomain::swap)
+      .def("write_paraview", &DistributedDomain::write_paraview, py::arg("prefix"), py::arg("zero_nans") = false,
+           py::call_guard<py::gil_scoped_release>())
+      .def("dlpack",
+           [](std::shared_ptr<DistributedDomain> self, size_t di, int64_t q, bool curr) {
+             return make_capsule(self, self->domains().at(di), q, curr);
+           },
+           py::arg("domain"), py::arg("qi"), py::arg("curr") = true)
+      .def_property_readonly("timers", [](DistributedDomain &d) {
+        py::dict t;
+        t["mpi_topo"] = d.timeMpiTopo_;
+        t["node_gpus"] = d.timeNodeGpus_;
+        t["peer_en"] = d.timePeerEn_;
+        t["placement"] = d.timePlacement_;
+        t["plan"] = d.timePlan_;
+        t["realize"] = d.timeRealize_;
+        t["create"] = d.timeCreate_;
+        t["exchange"] = d.timeExchange_;
+        t["swap"] = d.timeSwap_;
+        return t;
+      });
+
+  // ---------------- kernels ----------------
+  m.def("stencil7_apply",
+        [](DistributedDomain &dd, size_t di, int64_t q, const Rect3 &region, StencilKind kind, bool spheres,
+           uintptr_t stream) {
+          const Spheres s = spheres ? Spheres::jacobi(dd.get_compute_region()) : Spheres();
+          stencil7_apply(dd.domains().at(di), q, region, kind, s, reinterpret_cast<hipStream_t>(stream));
+        },
+        py::arg("dd"), py::arg("domain"), py::arg("qi"), py::arg("region"), py::arg("kind"), py::arg("spheres"),
+        py::arg("stream") = 0);
+  m.def("jacobi_spheres", [](const Rect3 &cReg) {
+    Spheres s = Spheres::jacobi(cReg);
+    return py::make_tuple(s.hot, s.cold, s.radius);
+  });
+
+  // ---------------- models ----------------
+  py::class_<StencilTune>(m, "StencilTune")
+      .def(py::init<>())
+      .def_readwrite("ty", &StencilTune::ty)
+      .def_readwrite("zchunk", &StencilTune::zchunk)
+      .def_readwrite("xcd_remap", &StencilTune::xcdRemap)
+      .def_readwrite("nontemporal", &StencilTune::nontemporal);
+  py::class_<StencilModelConfig>(m, "StencilModelConfig")
+      .def(py::init<>())
+      .def_readwrite("size", &StencilModelConfig::size)
+      .def_readwrite("kind", &StencilModelConfig::kind)
+      .def_readwrite("radius", &StencilModelConfig::radius)
+      .def_readwrite("all_directions", &StencilModelConfig::allDirections)
+      .def_readwrite("quantities", &StencilModelConfig::quantities)
+      .def_readwrite("fp64", &StencilModelConfig::fp64)
+      .def_readwrite("methods", &StencilModelConfig::methods)
+      .def_readwrite("placement", &StencilModelConfig::placement)
+      .def_readwrite("gpus", &StencilModelConfig::gpus)
+      .def_readwrite("overlap", &StencilModelConfig::overlap)
+      .def_property(
+          "backend", [](const StencilModelConfig &c) { return c.backend; },
+          [](StencilModelConfig &c, Backend b) {
+            c.backend = b;
+            c.setBackend = true;
+          })
+      .def_readwrite("tune", &StencilModelConfig::tune)
+      .def_readwrite("astaroth_period", &StencilModelConfig::astarothPeriod);
+  py::class_<StencilModel, std::shared_ptr<StencilModel>>(m, "StencilModel")
+      .def(py::init([](const StencilModelConfig &c, std::shared_ptr<comm::ProcGroup> pg) {
+             py::gil_scoped_release r;
+             return std::make_shared<StencilModel>(c, pg);
+           }),
+           py::arg("config"), py::arg("group") = nullptr)
+      .def("init", &StencilModel::init, py::call_guard<py::gil_scoped_release>())
+      .def("step", &StencilModel::step, py::call_guard<py::gil_scoped_release>())
+      .def("run", &StencilModel::run, py::call_guard<py::gil_scoped_release>())
+      .def("synchronize", &StencilModel::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("cells", &StencilModel::cells)
+      .def("local_cells", &StencilModel::local_cells)
+      .def("steps_done", &StencilModel::steps_done)
+      .def("compute_stream", [](StencilModel &mdl, size_t di) { return reinterpret_cast<uintptr_t>(mdl.compute_stream(di)); })
+      .def("domain",
+           [](std::shared_ptr<StencilModel> mdl) {
+             // aliasing shared_ptr: the DistributedDomain lives as long as the model
+             return std::shared_ptr<DistributedDomain>(mdl, &mdl->domain());
+           });
+}

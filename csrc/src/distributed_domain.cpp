@@ -1,0 +1,1022 @@
+// DistributedDomain implementation: placement, message planning, transport setup and the exchange engine.
+// See distributed_domain.hpp for the design; reference call stacks: SURVEY §3.2 (realize) and §3.3 (exchange).
+#include "stencil/domain/distributed_domain.hpp"
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <set>
+#include <sstream>
+
+#include "stencil/rt/hip_check.hpp"
+#include "stencil/rt/trace.hpp"
+#include "stencil/topo/gpu_topology.hpp"
+
+#define NCCL_CHECK(stmt)                                                                                           \
+  do {                                                                                                             \
+    ncclResult_t _r = (stmt);                                                                                      \
+    if (_r != ncclSuccess) LOG_FATAL("RCCL error " << int(_r) << " (" << ncclGetErrorString(_r) << ") in `" #stmt "`"); \
+  } while (0)
+
+namespace stencil {
+
+std::string to_string(MethodFlags m) {
+  std::string s;
+  auto add = [&](MethodFlags f, const char *n) {
+    if (m && f) s += (s.empty() ? "" : "/") + std::string(n);
+  };
+  add(MethodFlags::Staged, "staged");
+  add(MethodFlags::Rccl, "rccl");
+  add(MethodFlags::Colocated, "colo");
+  add(MethodFlags::PeerCopy, "peer");
+  add(MethodFlags::Kernel, "kernel");
+  return s.empty() ? "none" : s;
+}
+
+static int method_slot(MethodFlags m) {
+  switch (m) {
+  case MethodFlags::Staged:
+    return 0;
+  case MethodFlags::Rccl:
+    return 1;
+  case MethodFlags::Colocated:
+    return 2;
+  case MethodFlags::PeerCopy:
+    return 3;
+  case MethodFlags::Kernel:
+    return 4;
+  default:
+    LOG_FATAL("not a single method: " << int(m));
+  }
+}
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------------------------------------
+// internal state
+// ------------------------------------------------------------------------------------------------
+
+// segment list with up to 4 variants (domain parity x inbox slot), host and device copies
+struct SegList {
+  std::vector<CopySeg> host[4];
+  CopySeg *dev[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t units[4] = {0, 0, 0, 0};
+  bool empty() const { return host[0].empty() && host[1].empty() && host[2].empty() && host[3].empty(); }
+  void upload(int device) {
+    for (int v = 0; v < 4; ++v) {
+      units[v] = finalize_segs(host[v]);
+      if (device >= 0 && !host[v].empty()) {
+        HIP_CHECK(hipSetDevice(device));
+        HIP_CHECK(hipMalloc(&dev[v], sizeof(CopySeg) * host[v].size()));
+        HIP_CHECK(hipMemcpy(dev[v], host[v].data(), sizeof(CopySeg) * host[v].size(), hipMemcpyHostToDevice));
+      }
+    }
+  }
+  void run_device(int v, hipStream_t s) const { copy_segs_device(dev[v], int(host[v].size()), units[v], s); }
+  void run_host(int v) const { copy_segs_host(host[v]); }
+  void release() {
+    for (auto &d : dev)
+      if (d) {
+        (void)hipFree(d);
+        d = nullptr;
+      }
+  }
+};
+
+struct Channel {
+  MethodFlags method = MethodFlags::None;
+  bool send = true;
+  int localDom = -1;
+  Dim3 localIdx, remoteIdx;
+  int remoteRank = -1, remoteId = -1, remoteDev = -1;
+  int localDev = -1;
+  std::vector<Message> msgs; // sorted by dir
+  int64_t bytes = 0;         // packed bytes (reference wire layout)
+  uint32_t tag = 0;
+  int64_t orderKey = 0; // canonical (src, dst) order for RCCL matching
+  char *dbuf = nullptr; // device staging buffer (Rccl, Staged)
+  char *hbuf = nullptr; // pinned host (Staged, device backend)
+  std::vector<char> hostBuf; // host backend
+  // Colocated (IPC)
+  char *ownBlock = nullptr;    // recv: [arrived flag | slot0 | slot1]; send: [credit flag]
+  char *remoteBlock = nullptr; // opened IPC mapping of the peer's block
+  int64_t slotStride = 0;
+};
+
+struct DevCtx {
+  int dev = -1;
+  Stream comm;
+  Event done, translated;
+  std::vector<int> doms;
+  SegList translate;              // Kernel + PeerCopy originating here (variant = parity)
+  std::set<int> peerWriters;      // devices whose translate writes into this device
+  std::vector<int> coloSend, coloRecv, rcclSend, rcclRecv, stagedSend, stagedRecv;
+  SegList coloPack, coloUnpack;   // variant = parity*2 + slot
+  SegList rcclPack, rcclUnpack;   // variant = parity
+  SegList stagedPack, stagedUnpack;
+  ncclComm_t nccl = nullptr;
+};
+
+struct DistributedDomain::Impl {
+  std::vector<Channel> chans;
+  std::vector<DevCtx> devs;            // device backend: one per distinct local device
+  std::map<int, int> devIndex;         // device id -> index into devs
+  std::vector<Event> ready;            // per local domain
+  std::vector<bool> readyPending;
+  uint64_t epoch = 0;
+  int *errHost = nullptr; // host-mapped timeout word
+  int *errDev = nullptr;
+  double waitTimeout = 60.0;
+  // host backend
+  SegList hostTranslate, hostStagedPack, hostStagedUnpack;
+  bool rccl = false;
+};
+
+// ------------------------------------------------------------------------------------------------
+// construction / configuration
+// ------------------------------------------------------------------------------------------------
+DistributedDomain::DistributedDomain(int64_t x, int64_t y, int64_t z, std::shared_ptr<comm::ProcGroup> pg)
+    : size_(x, y, z), pg_(pg ? pg : comm::default_group()), impl_(new Impl) {
+  radius_ = Radius::constant(0);
+  if (const char *e = std::getenv("STENCIL_EXCHANGE_STATS")) exchangeStats_ = std::atoi(e) != 0;
+  if (const char *e = std::getenv("STENCIL_PLAN_FILE"))
+    if (std::atoi(e) == 0) planPrefix_.clear();
+  if (const char *e = std::getenv("STENCIL_WAIT_TIMEOUT")) impl_->waitTimeout = std::atof(e);
+}
+
+DistributedDomain::~DistributedDomain() {
+  if (!impl_) return;
+  try {
+    for (auto &d : impl_->devs) {
+      (void)HIP_TRY(hipSetDevice(d.dev));
+      (void)HIP_TRY(hipStreamSynchronize(d.comm));
+    }
+  } catch (...) {
+  }
+  for (auto &c : impl_->chans) {
+    if (c.dbuf) (void)hipFree(c.dbuf);
+    if (c.hbuf) (void)hipHostFree(c.hbuf);
+    if (c.remoteBlock) (void)hipIpcCloseMemHandle(c.remoteBlock);
+  }
+  // make sure peers closed their mappings of our blocks before freeing them
+  try {
+    if (realized_ && pg_->size() > 1) pg_->barrier();
+  } catch (...) {
+  }
+  for (auto &c : impl_->chans)
+    if (c.ownBlock) (void)hipFree(c.ownBlock);
+  for (auto &d : impl_->devs) {
+    d.translate.release();
+    d.coloPack.release();
+    d.coloUnpack.release();
+    d.rcclPack.release();
+    d.rcclUnpack.release();
+    d.stagedPack.release();
+    d.stagedUnpack.release();
+    if (d.nccl) ncclCommDestroy(d.nccl);
+  }
+  if (impl_->errHost) (void)hipHostFree(impl_->errHost);
+}
+
+int64_t DistributedDomain::add_data(int64_t elemSize, const std::string &name, DType dtype) {
+  STENCIL_REQUIRE(!realized_, "add_data after realize");
+  elemSize_.push_back(elemSize);
+  names_.push_back(name);
+  dtypes_.push_back(dtype);
+  return int64_t(elemSize_.size()) - 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// segment builders (reference wire layout: messages sorted by dir, each quantity aligned to its element size,
+// reference packer.cuh:136-160)
+// ------------------------------------------------------------------------------------------------
+static StridedBox dense_box(char *base, const Dim3 &ext, int64_t es) {
+  StridedBox b;
+  b.base = base;
+  b.ystride = ext.x * es;
+  b.zstride = ext.x * ext.y * es;
+  return b;
+}
+
+static int64_t packed_size(const LocalDomain &dom, const std::vector<Message> &msgs) {
+  int64_t off = 0;
+  for (const auto &m : msgs)
+    for (int64_t q = 0; q < dom.num_data(); ++q) {
+      off = round_up(off, dom.elem_size(q));
+      off += dom.halo_bytes(-m.dir, q);
+    }
+  return off;
+}
+
+// pack: interior slab on the `dir` side -> dense buffer. `curr`: which physical buffer is "curr" in this variant.
+static void build_pack(const LocalDomain &dom, const std::vector<Message> &msgs, char *buf, bool curr,
+                       std::vector<CopySeg> &out) {
+  int64_t off = 0;
+  for (const auto &m : msgs)
+    for (int64_t q = 0; q < dom.num_data(); ++q) {
+      const int64_t es = dom.elem_size(q);
+      off = round_up(off, es);
+      const Dim3 ext = dom.halo_extent(-m.dir);
+      out.push_back(make_copy_seg(dom.box(q, curr, dom.halo_pos(m.dir, false)), dense_box(buf + off, ext, es), ext, es));
+      off += es * ext.flatten();
+    }
+}
+
+// unpack: dense buffer -> the -dir halo (message sent along dir lands on our -dir side)
+static void build_unpack(const LocalDomain &dom, const std::vector<Message> &msgs, char *buf, bool curr,
+                         std::vector<CopySeg> &out) {
+  int64_t off = 0;
+  for (const auto &m : msgs)
+    for (int64_t q = 0; q < dom.num_data(); ++q) {
+      const int64_t es = dom.elem_size(q);
+      off = round_up(off, es);
+      const Dim3 ext = dom.halo_extent(-m.dir);
+      out.push_back(make_copy_seg(dense_box(buf + off, ext, es), dom.box(q, curr, dom.halo_pos(-m.dir, true)), ext, es));
+      off += es * ext.flatten();
+    }
+}
+
+// direct translate src interior slab -> dst halo (same process)
+static void build_translate(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
+                            std::vector<CopySeg> &out) {
+  for (int64_t q = 0; q < src.num_data(); ++q) {
+    const int64_t es = src.elem_size(q);
+    const Dim3 ext = src.halo_extent(-dir);
+    out.push_back(make_copy_seg(src.box(q, curr, src.halo_pos(dir, false)), dst.box(q, curr, dst.halo_pos(-dir, true)),
+                                ext, es));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// realize
+// ------------------------------------------------------------------------------------------------
+void DistributedDomain::realize() {
+  STENCIL_REQUIRE(!realized_, "realize() called twice");
+  STENCIL_REQUIRE(!elemSize_.empty(), "add_data() before realize()");
+  TraceRange tr0("DistributedDomain::realize");
+  Impl &I = *impl_;
+  comm::ProcGroup &pg = *pg_;
+  const int myRank = pg.rank();
+
+  if (!backendSet_) backend_ = gpu_topo::device_count() > 0 ? Backend::Device : Backend::Host;
+  const bool dev = backend_ == Backend::Device;
+  if (dev) STENCIL_REQUIRE(gpu_topo::device_count() > 0, "Device backend requested but no GPU is visible");
+
+  // ---- node topology / GPU selection (reference stencil.hpp:158-245) ----
+  double t0 = now_s();
+  const int coloSize = pg.colocated_size();
+  const int coloRank = pg.colocated_rank();
+  timeMpiTopo_ = pg.allreduce_max(now_s() - t0);
+  t0 = now_s();
+  if (gpus_.empty()) {
+    if (dev) {
+      const int n = gpu_topo::device_count();
+      if (coloSize >= n) {
+        gpus_ = {coloRank % n};
+      } else {
+        const int per = n / coloSize;
+        for (int i = 0; i < per; ++i) gpus_.push_back(coloRank * per + i);
+      }
+    } else {
+      gpus_ = {0};
+    }
+  }
+  timeNodeGpus_ = pg.allreduce_max(now_s() - t0);
+  t0 = now_s();
+  if (dev) {
+    for (int a : gpus_)
+      for (int b : gpus_)
+        if (a != b) gpu_topo::enable_peer(a, b);
+  }
+  timePeerEn_ = pg.allreduce_max(now_s() - t0);
+
+  // ---- placement ----
+  t0 = now_s();
+  {
+    TraceRange tr("placement");
+    if (strategy_ == PlacementStrategy::NodeAware) {
+      BandwidthFn bw = dev ? BandwidthFn([](int a, int b) { return gpu_topo::bandwidth(a, b); })
+                           : BandwidthFn([](int a, int b) { return a == b ? 10.0 : 1.0; });
+      placement_.reset(new NodeAwarePlacement(size_, pg, radius_, gpus_, bw));
+    } else {
+      placement_.reset(new TrivialPlacement(size_, pg, gpus_));
+    }
+  }
+  timePlacement_ = pg.allreduce_max(now_s() - t0);
+
+  // ---- local domains ----
+  t0 = now_s();
+  domains_.reserve(gpus_.size());
+  for (size_t di = 0; di < gpus_.size(); ++di) {
+    const Dim3 idx = placement_->get_idx(myRank, int(di));
+    const int device = placement_->get_device(idx);
+    domains_.emplace_back(placement_->subdomain_size(idx), placement_->subdomain_origin(idx), dev ? device : -1, backend_);
+    LocalDomain &d = domains_.back();
+    d.set_radius(radius_);
+    d.set_padding(pad_);
+    for (size_t q = 0; q < elemSize_.size(); ++q) d.add_data(elemSize_[q], names_[q], dtypes_[q]);
+    LOG_INFO("rank " << myRank << " domain " << di << " idx " << idx << " size " << d.size() << " origin " << d.origin()
+                     << " device " << device);
+  }
+  for (auto &d : domains_) d.realize();
+  timeRealize_ = pg.allreduce_max(now_s() - t0);
+
+  // ---- plan messages (reference src/stencil.cu:132-239) ----
+  t0 = now_s();
+  const Dim3 gdim = placement_->dim();
+  const int64_t numSub = gdim.flatten();
+  auto can_access = [&](int a, int b) {
+    if (a == b) return true;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return can != 0;
+  };
+  auto choose = [&](int srcRank, int srcDev, int dstRank, int dstDev) -> MethodFlags {
+    const bool sameRank = srcRank == dstRank;
+    if (!dev) {
+      if (sameRank && (any_methods(MethodFlags::Kernel) || any_methods(MethodFlags::PeerCopy)))
+        return srcDev == dstDev && any_methods(MethodFlags::Kernel) ? MethodFlags::Kernel : MethodFlags::PeerCopy;
+      if (any_methods(MethodFlags::Staged)) return MethodFlags::Staged;
+      return MethodFlags::None;
+    }
+    if (any_methods(MethodFlags::Kernel) && sameRank && srcDev == dstDev) return MethodFlags::Kernel;
+    if (any_methods(MethodFlags::PeerCopy) && sameRank && gpu_topo::peer(srcDev, dstDev)) return MethodFlags::PeerCopy;
+    if (any_methods(MethodFlags::Colocated) && !sameRank && pg.hostname(srcRank) == pg.hostname(dstRank) &&
+        can_access(srcDev, dstDev))
+      return MethodFlags::Colocated;
+    if (any_methods(MethodFlags::Rccl)) return MethodFlags::Rccl;
+    if (any_methods(MethodFlags::Staged)) return MethodFlags::Staged;
+    return MethodFlags::None;
+  };
+
+  // channel maps: (method, localDom, remoteLinear) -> channel index
+  std::map<std::tuple<int, int, int64_t>, int> sendKey, recvKey;
+  std::vector<std::tuple<int, int, Dim3>> localTranslates; // (srcDom, dstDom, dir)
+  plan_.clear();
+  for (size_t di = 0; di < domains_.size(); ++di) {
+    const Dim3 myIdx = placement_->get_idx(myRank, int(di));
+    const int myDev = placement_->get_device(myIdx);
+    for (int i = 0; i < 27; ++i) {
+      const Dim3 dir = dir_from_index(i);
+      if (dir == Dim3(0, 0, 0) || radius_.dir(-dir) == 0) continue;
+      // send
+      {
+        const Dim3 dstIdx = (myIdx + dir).wrap(gdim);
+        const int dstRank = placement_->get_rank(dstIdx), dstId = placement_->get_subdomain_id(dstIdx),
+                  dstDev = placement_->get_device(dstIdx);
+        const MethodFlags m = choose(myRank, myDev, dstRank, dstDev);
+        if (m == MethodFlags::None) LOG_FATAL("no method available to send " << myIdx << " -> " << dstIdx << " dir " << dir);
+        int64_t bytes = 0;
+        for (int64_t q = 0; q < domains_[di].num_data(); ++q) bytes += domains_[di].halo_bytes(-dir, q);
+        plan_.push_back({m, myIdx, dstIdx, myRank, dstRank, myDev, dstDev, dir, bytes});
+        bytesPerMethod_[method_slot(m)] += uint64_t(bytes);
+        if (m == MethodFlags::Kernel || m == MethodFlags::PeerCopy) {
+          localTranslates.emplace_back(int(di), dstId, dir);
+        } else {
+          const auto key = std::make_tuple(int(m), int(di), linearize(dstIdx, gdim));
+          auto it = sendKey.find(key);
+          int ci;
+          if (it == sendKey.end()) {
+            ci = int(I.chans.size());
+            sendKey[key] = ci;
+            Channel c;
+            c.method = m;
+            c.send = true;
+            c.localDom = int(di);
+            c.localIdx = myIdx;
+            c.remoteIdx = dstIdx;
+            c.remoteRank = dstRank;
+            c.remoteId = dstId;
+            c.remoteDev = dstDev;
+            c.localDev = myDev;
+            const int64_t sl = linearize(myIdx, gdim), dl = linearize(dstIdx, gdim);
+            c.orderKey = sl * numSub + dl;
+            c.tag = uint32_t(c.orderKey & 0x0fffffff);
+            I.chans.push_back(c);
+          } else {
+            ci = it->second;
+          }
+          I.chans[ci].msgs.push_back(Message{dir, int(di), dstId});
+        }
+      }
+      // recv
+      {
+        const Dim3 srcIdx = (myIdx - dir).wrap(gdim);
+        const int srcRank = placement_->get_rank(srcIdx), srcId = placement_->get_subdomain_id(srcIdx),
+                  srcDev = placement_->get_device(srcIdx);
+        const MethodFlags m = choose(srcRank, srcDev, myRank, myDev);
+        if (m == MethodFlags::None) LOG_FATAL("no method available to recv " << srcIdx << " -> " << myIdx);
+        if (m == MethodFlags::Kernel || m == MethodFlags::PeerCopy) continue; // written by the sender directly
+        const auto key = std::make_tuple(int(m), int(di), linearize(srcIdx, gdim));
+        auto it = recvKey.find(key);
+        int ci;
+        if (it == recvKey.end()) {
+          ci = int(I.chans.size());
+          recvKey[key] = ci;
+          Channel c;
+          c.method = m;
+          c.send = false;
+          c.localDom = int(di);
+          c.localIdx = myIdx;
+          c.remoteIdx = srcIdx;
+          c.remoteRank = srcRank;
+          c.remoteId = srcId;
+          c.remoteDev = srcDev;
+          c.localDev = myDev;
+          const int64_t sl = linearize(srcIdx, gdim), dl = linearize(myIdx, gdim);
+          c.orderKey = sl * numSub + dl;
+          c.tag = uint32_t(c.orderKey & 0x0fffffff);
+          I.chans.push_back(c);
+        } else {
+          ci = it->second;
+        }
+        I.chans[ci].msgs.push_back(Message{dir, srcId, int(di)});
+      }
+    }
+  }
+  for (auto &c : I.chans) {
+    std::sort(c.msgs.begin(), c.msgs.end());
+    c.bytes = packed_size(domains_[c.localDom], c.msgs);
+  }
+  for (int s = 0; s < 5; ++s) bytesPerMethod_[s] = pg.allreduce_sum_u64(bytesPerMethod_[s]);
+  timePlan_ = pg.allreduce_max(now_s() - t0);
+
+  if (!planPrefix_.empty()) {
+    std::ofstream f(planPrefix_ + "_" + std::to_string(myRank) + ".txt");
+    f << plan_summary();
+  }
+
+  // ---- create transports ----
+  t0 = now_s();
+  TraceRange trc("DistributedDomain::realize: create");
+  if (!dev) {
+    // host backend: translate + staged only, all executed on the host
+    for (const auto &t : localTranslates) {
+      const LocalDomain &s = domains_[std::get<0>(t)], &d = domains_[std::get<1>(t)];
+      for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, I.hostTranslate.host[p]);
+    }
+    for (auto &c : I.chans) {
+      STENCIL_REQUIRE(c.method == MethodFlags::Staged, "host backend supports only Kernel/Staged transports");
+      c.hostBuf.resize(size_t(std::max<int64_t>(c.bytes, 1)));
+      for (int p = 0; p < 2; ++p) {
+        if (c.send)
+          build_pack(domains_[c.localDom], c.msgs, c.hostBuf.data(), p == 0, I.hostStagedPack.host[p]);
+        else
+          build_unpack(domains_[c.localDom], c.msgs, c.hostBuf.data(), p == 0, I.hostStagedUnpack.host[p]);
+      }
+    }
+    I.hostTranslate.upload(-1);
+    I.hostStagedPack.upload(-1);
+    I.hostStagedUnpack.upload(-1);
+  } else {
+    // per-device contexts
+    for (size_t di = 0; di < domains_.size(); ++di) {
+      const int d = domains_[di].gpu();
+      if (!I.devIndex.count(d)) {
+        I.devIndex[d] = int(I.devs.size());
+        I.devs.emplace_back();
+        DevCtx &c = I.devs.back();
+        c.dev = d;
+        c.comm = Stream(d, Priority::HIGH);
+        c.done = Event(d);
+        c.translated = Event(d);
+      }
+      I.devs[I.devIndex[d]].doms.push_back(int(di));
+      I.ready.emplace_back(d);
+      I.readyPending.push_back(false);
+    }
+    HIP_CHECK(hipHostMalloc((void **)&I.errHost, sizeof(int), hipHostMallocMapped));
+    *I.errHost = 0;
+    HIP_CHECK(hipHostGetDevicePointer((void **)&I.errDev, I.errHost, 0));
+
+    // same-process direct stores
+    for (const auto &t : localTranslates) {
+      const LocalDomain &s = domains_[std::get<0>(t)], &d = domains_[std::get<1>(t)];
+      DevCtx &ctx = I.devs[I.devIndex[s.gpu()]];
+      for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, ctx.translate.host[p]);
+      if (d.gpu() != s.gpu()) I.devs[I.devIndex[d.gpu()]].peerWriters.insert(s.gpu());
+    }
+
+    // channel buffers
+    for (int ci = 0; ci < int(I.chans.size()); ++ci) {
+      Channel &c = I.chans[ci];
+      DevCtx &ctx = I.devs[I.devIndex[c.localDev]];
+      HIP_CHECK(hipSetDevice(c.localDev));
+      const size_t nb = size_t(std::max<int64_t>(c.bytes, 1));
+      if (c.method == MethodFlags::Staged) {
+        HIP_CHECK(hipMalloc(&c.dbuf, nb));
+        HIP_CHECK(hipHostMalloc((void **)&c.hbuf, nb, hipHostMallocDefault));
+        (c.send ? ctx.stagedSend : ctx.stagedRecv).push_back(ci);
+      } else if (c.method == MethodFlags::Rccl) {
+        HIP_CHECK(hipMalloc(&c.dbuf, nb));
+        (c.send ? ctx.rcclSend : ctx.rcclRecv).push_back(ci);
+      } else if (c.method == MethodFlags::Colocated) {
+        // receiver owns [arrived flag (256 B) | slot0 | slot1] in uncached memory; sender owns [credit flag]
+        c.slotStride = round_up(int64_t(nb), 256);
+        const size_t blockBytes = c.send ? 256 : size_t(256 + 2 * c.slotStride);
+        hipError_t e = hipExtMallocWithFlags((void **)&c.ownBlock, blockBytes, hipDeviceMallocUncached);
+        if (e != hipSuccess) {
+          (void)hipGetLastError();
+          LOG_WARN("uncached allocation failed (" << hipGetErrorString(e) << "), using fine-grained memory");
+          HIP_CHECK(hipExtMallocWithFlags((void **)&c.ownBlock, blockBytes, hipDeviceMallocFinegrained));
+        }
+        HIP_CHECK(hipMemset(c.ownBlock, 0, blockBytes));
+        (c.send ? ctx.coloSend : ctx.coloRecv).push_back(ci);
+      }
+    }
+    HIP_CHECK(hipDeviceSynchronize());
+
+    // IPC handshake for colocated channels: every side sends its handle first (non-blocking), then receives
+    {
+      TraceRange tri("ipc handshake");
+      for (auto &c : I.chans) {
+        if (c.method != MethodFlags::Colocated) continue;
+        hipIpcMemHandle_t h;
+        HIP_CHECK(hipSetDevice(c.localDev));
+        HIP_CHECK(hipIpcGetMemHandle(&h, c.ownBlock));
+        pg.send(c.remoteRank, c.tag | (c.send ? 0x20000000u : 0x10000000u), &h, sizeof(h));
+      }
+      for (auto &c : I.chans) {
+        if (c.method != MethodFlags::Colocated) continue;
+        hipIpcMemHandle_t h;
+        // a sender needs the receiver's inbox (tagged 0x1...), a receiver the sender's credit block (0x2...)
+        pg.recv(c.remoteRank, c.tag | (c.send ? 0x10000000u : 0x20000000u), &h, sizeof(h));
+        HIP_CHECK(hipSetDevice(c.localDev));
+        HIP_CHECK(hipIpcOpenMemHandle((void **)&c.remoteBlock, h, hipIpcMemLazyEnablePeerAccess));
+      }
+      pg.barrier();
+    }
+
+    // segment lists per device
+    for (auto &ctx : I.devs) {
+      for (int ci : ctx.coloSend) {
+        Channel &c = I.chans[ci];
+        const LocalDomain &dom = domains_[c.localDom];
+        for (int p = 0; p < 2; ++p)
+          for (int slot = 0; slot < 2; ++slot)
+            build_pack(dom, c.msgs, c.remoteBlock + 256 + slot * c.slotStride, p == 0, ctx.coloPack.host[p * 2 + slot]);
+      }
+      for (int ci : ctx.coloRecv) {
+        Channel &c = I.chans[ci];
+        const LocalDomain &dom = domains_[c.localDom];
+        for (int p = 0; p < 2; ++p)
+          for (int slot = 0; slot < 2; ++slot)
+            build_unpack(dom, c.msgs, c.ownBlock + 256 + slot * c.slotStride, p == 0, ctx.coloUnpack.host[p * 2 + slot]);
+      }
+      for (int ci : ctx.rcclSend)
+        for (int p = 0; p < 2; ++p)
+          build_pack(domains_[I.chans[ci].localDom], I.chans[ci].msgs, I.chans[ci].dbuf, p == 0, ctx.rcclPack.host[p]);
+      for (int ci : ctx.rcclRecv)
+        for (int p = 0; p < 2; ++p)
+          build_unpack(domains_[I.chans[ci].localDom], I.chans[ci].msgs, I.chans[ci].dbuf, p == 0, ctx.rcclUnpack.host[p]);
+      for (int ci : ctx.stagedSend)
+        for (int p = 0; p < 2; ++p)
+          build_pack(domains_[I.chans[ci].localDom], I.chans[ci].msgs, I.chans[ci].dbuf, p == 0, ctx.stagedPack.host[p]);
+      for (int ci : ctx.stagedRecv)
+        for (int p = 0; p < 2; ++p)
+          build_unpack(domains_[I.chans[ci].localDom], I.chans[ci].msgs, I.chans[ci].dbuf, p == 0,
+                       ctx.stagedUnpack.host[p]);
+      ctx.translate.upload(ctx.dev);
+      ctx.coloPack.upload(ctx.dev);
+      ctx.coloUnpack.upload(ctx.dev);
+      ctx.rcclPack.upload(ctx.dev);
+      ctx.rcclUnpack.upload(ctx.dev);
+      ctx.stagedPack.upload(ctx.dev);
+      ctx.stagedUnpack.upload(ctx.dev);
+      // RCCL matching order: canonical (src, dst) sub-domain order on both sides of every pair
+      auto byKey = [&](int a, int b) { return I.chans[a].orderKey < I.chans[b].orderKey; };
+      std::sort(ctx.rcclSend.begin(), ctx.rcclSend.end(), byKey);
+      std::sort(ctx.rcclRecv.begin(), ctx.rcclRecv.end(), byKey);
+    }
+
+    // RCCL communicator over all (rank, device) pairs, created only if some rank needs it
+    int64_t rcclChans = 0;
+    for (auto &c : I.chans) rcclChans += c.method == MethodFlags::Rccl;
+    if (pg.allreduce_sum_u64(uint64_t(rcclChans)) > 0) {
+      TraceRange trr("rccl init");
+      const int nLocal = int(I.devs.size());
+      std::vector<int> counts(pg.size());
+      pg.allgather(&nLocal, sizeof(int), counts.data());
+      int first = 0, total = 0;
+      for (int r = 0; r < pg.size(); ++r) {
+        if (r < myRank) first += counts[r];
+        total += counts[r];
+      }
+      // device slot of every rank's devices, for peer rank lookup
+      std::vector<int> myDevs;
+      for (auto &d : I.devs) myDevs.push_back(d.dev);
+      int maxN = 0;
+      for (int c : counts) maxN = std::max(maxN, c);
+      std::vector<int> padded(maxN, -1), allDevs(size_t(maxN) * pg.size());
+      std::copy(myDevs.begin(), myDevs.end(), padded.begin());
+      pg.allgather(padded.data(), sizeof(int) * maxN, allDevs.data());
+      ncclUniqueId id;
+      if (myRank == 0) NCCL_CHECK(ncclGetUniqueId(&id));
+      pg.bcast(&id, sizeof(id), 0);
+      NCCL_CHECK(ncclGroupStart());
+      for (int k = 0; k < nLocal; ++k) {
+        HIP_CHECK(hipSetDevice(I.devs[k].dev));
+        NCCL_CHECK(ncclCommInitRank(&I.devs[k].nccl, total, id, first + k));
+      }
+      NCCL_CHECK(ncclGroupEnd());
+      // translate remote (rank, device) into RCCL ranks: stash in remoteId's high bits is confusing; keep a map
+      std::vector<int> firstOf(pg.size(), 0);
+      for (int r = 1; r < pg.size(); ++r) firstOf[r] = firstOf[r - 1] + counts[r - 1];
+      for (auto &c : I.chans) {
+        if (c.method != MethodFlags::Rccl) continue;
+        int slot = -1;
+        for (int k = 0; k < counts[c.remoteRank]; ++k)
+          if (allDevs[size_t(c.remoteRank) * maxN + k] == c.remoteDev) slot = k;
+        STENCIL_REQUIRE(slot >= 0, "RCCL peer device not found");
+        c.tag = uint32_t(firstOf[c.remoteRank] + slot); // reuse tag as the RCCL peer rank
+      }
+      I.rccl = true;
+    }
+  }
+  timeCreate_ = pg.allreduce_max(now_s() - t0);
+  realized_ = true;
+  pg.barrier();
+}
+
+std::string DistributedDomain::plan_summary() const {
+  std::ostringstream ss;
+  ss << "rank=" << rank() << "\n\n== domains ==\n";
+  for (size_t di = 0; di < domains_.size(); ++di)
+    ss << di << ":dev" << domains_[di].gpu() << ":" << placement_->get_idx(rank(), int(di)) << " sz=" << domains_[di].size()
+       << " origin=" << domains_[di].origin() << "\n";
+  const MethodFlags order[] = {MethodFlags::Kernel, MethodFlags::PeerCopy, MethodFlags::Colocated, MethodFlags::Rccl,
+                               MethodFlags::Staged};
+  for (MethodFlags m : order) {
+    ss << "\n== " << to_string(m) << " ==\n";
+    for (const auto &e : plan_)
+      if (e.method == m)
+        ss << e.srcIdx << "(r" << e.srcRank << " dev" << e.srcDev << ") -> " << e.dstIdx << "(r" << e.dstRank << " dev"
+           << e.dstDev << ") dir=" << e.dir << " " << e.bytes << "B\n";
+  }
+  ss << "\n== bytes per exchange (all ranks) ==\n";
+  for (MethodFlags m : order) ss << to_string(m) << " " << bytesPerMethod_[method_slot(m)] << "\n";
+  return ss.str();
+}
+
+uint64_t DistributedDomain::exchange_bytes_for_method(MethodFlags m) const {
+  uint64_t r = 0;
+  const MethodFlags all[] = {MethodFlags::Staged, MethodFlags::Rccl, MethodFlags::Colocated, MethodFlags::PeerCopy,
+                             MethodFlags::Kernel};
+  for (MethodFlags f : all)
+    if (m && f) r += bytesPerMethod_[method_slot(f)];
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// interior / exterior (reference src/stencil.cu:567-666)
+// ------------------------------------------------------------------------------------------------
+std::vector<Rect3> DistributedDomain::get_interior() const {
+  std::vector<Rect3> ret(domains_.size());
+  for (size_t di = 0; di < domains_.size(); ++di) {
+    const Rect3 com = domains_[di].get_compute_region();
+    Rect3 in = com;
+    for (int i = 0; i < 27; ++i) {
+      const Dim3 d = dir_from_index(i);
+      if (d == Dim3(0, 0, 0)) continue;
+      const int64_t r = radius_.dir(d);
+      if (d.x < 0) in.lo.x = std::max(com.lo.x + r, in.lo.x);
+      if (d.x > 0) in.hi.x = std::min(com.hi.x - r, in.hi.x);
+      if (d.y < 0) in.lo.y = std::max(com.lo.y + r, in.lo.y);
+      if (d.y > 0) in.hi.y = std::min(com.hi.y - r, in.hi.y);
+      if (d.z < 0) in.lo.z = std::max(com.lo.z + r, in.lo.z);
+      if (d.z > 0) in.hi.z = std::min(com.hi.z - r, in.hi.z);
+    }
+    ret[di] = in;
+  }
+  return ret;
+}
+
+std::vector<std::vector<Rect3>> DistributedDomain::get_exterior() const {
+  std::vector<std::vector<Rect3>> ret(domains_.size());
+  const auto ins = get_interior();
+  for (size_t di = 0; di < domains_.size(); ++di) {
+    const Rect3 &in = ins[di];
+    Rect3 c = domains_[di].get_compute_region();
+    if (in.hi.x != c.hi.x) {
+      ret[di].push_back(Rect3(Dim3(in.hi.x, c.lo.y, c.lo.z), c.hi));
+      c.hi.x = in.hi.x;
+    }
+    if (in.hi.y != c.hi.y) {
+      ret[di].push_back(Rect3(Dim3(c.lo.x, in.hi.y, c.lo.z), c.hi));
+      c.hi.y = in.hi.y;
+    }
+    if (in.hi.z != c.hi.z) {
+      ret[di].push_back(Rect3(Dim3(c.lo.x, c.lo.y, in.hi.z), c.hi));
+      c.hi.z = in.hi.z;
+    }
+    if (in.lo.x != c.lo.x) {
+      ret[di].push_back(Rect3(c.lo, Dim3(in.lo.x, c.hi.y, c.hi.z)));
+      c.lo.x = in.lo.x;
+    }
+    if (in.lo.y != c.lo.y) {
+      ret[di].push_back(Rect3(c.lo, Dim3(c.hi.x, in.lo.y, c.hi.z)));
+      c.lo.y = in.lo.y;
+    }
+    if (in.lo.z != c.lo.z) {
+      ret[di].push_back(Rect3(c.lo, Dim3(c.hi.x, c.hi.y, in.lo.z)));
+      c.lo.z = in.lo.z;
+    }
+  }
+  return ret;
+}
+
+// ------------------------------------------------------------------------------------------------
+// exchange
+// ------------------------------------------------------------------------------------------------
+void DistributedDomain::record_ready(size_t di, hipStream_t s) {
+  STENCIL_REQUIRE(realized_, "record_ready before realize");
+  if (backend_ != Backend::Device) return;
+  impl_->ready.at(di).record(s);
+  impl_->readyPending[di] = true;
+}
+
+void DistributedDomain::wait_exchange(size_t di, hipStream_t s) {
+  if (backend_ != Backend::Device) return;
+  const DevCtx &ctx = impl_->devs[impl_->devIndex.at(domains_.at(di).gpu())];
+  ctx.done.wait_on(s);
+}
+
+hipStream_t DistributedDomain::comm_stream(size_t di) const {
+  if (backend_ != Backend::Device) return nullptr;
+  return impl_->devs[impl_->devIndex.at(domains_.at(di).gpu())].comm;
+}
+
+void DistributedDomain::sync_exchange() {
+  if (backend_ != Backend::Device) return;
+  for (auto &d : impl_->devs) {
+    HIP_CHECK(hipSetDevice(d.dev));
+    HIP_CHECK(hipStreamSynchronize(d.comm));
+  }
+  if (*impl_->errHost) {
+    const int code = *impl_->errHost;
+    LOG_FATAL("halo exchange timed out waiting for a colocated peer (code " << code << ", epoch " << impl_->epoch
+                                                                           << "); a peer rank is stalled or dead");
+  }
+}
+
+void DistributedDomain::exchange() {
+  double t0 = 0;
+  if (exchangeStats_) {
+    pg_->barrier();
+    t0 = now_s();
+  }
+  exchange_async();
+  sync_exchange();
+  if (exchangeStats_) timeExchange_ += pg_->allreduce_max(now_s() - t0);
+}
+
+void DistributedDomain::exchange_async() {
+  STENCIL_REQUIRE(realized_, "exchange before realize");
+  TraceRange tr("DD::exchange()");
+  Impl &I = *impl_;
+  comm::ProcGroup &pg = *pg_;
+  const int parity = domains_.empty() ? 0 : domains_[0].parity();
+  for (auto &d : domains_) STENCIL_REQUIRE(d.parity() == parity, "local domains out of swap() lockstep");
+  ++I.epoch;
+
+  if (backend_ == Backend::Host) {
+    {
+      TraceRange t("host translate");
+      I.hostTranslate.run_host(parity);
+    }
+    TraceRange t("host staged");
+    I.hostStagedPack.run_host(parity);
+    for (auto &c : I.chans)
+      if (c.send) pg.send(c.remoteRank, c.tag, c.hostBuf.data(), size_t(c.bytes));
+    for (auto &c : I.chans)
+      if (!c.send) pg.recv(c.remoteRank, c.tag, c.hostBuf.data(), size_t(c.bytes));
+    I.hostStagedUnpack.run_host(parity);
+    return;
+  }
+
+  // (0) dependencies: the comm streams start after every local domain's producer work
+  {
+    bool anyMissing = false;
+    for (size_t di = 0; di < domains_.size(); ++di) anyMissing |= !I.readyPending[di];
+    if (anyMissing) {
+      for (auto &d : I.devs) {
+        HIP_CHECK(hipSetDevice(d.dev));
+        HIP_CHECK(hipDeviceSynchronize());
+      }
+    }
+    for (auto &ctx : I.devs) {
+      HIP_CHECK(hipSetDevice(ctx.dev));
+      for (size_t di = 0; di < domains_.size(); ++di)
+        if (I.readyPending[di]) I.ready[di].wait_on(ctx.comm);
+    }
+    for (size_t di = 0; di < domains_.size(); ++di) I.readyPending[di] = false;
+  }
+
+  const int slot = int(I.epoch & 1);
+  const int cv = parity * 2 + slot;
+
+  // (1) same-process direct stores (Kernel + PeerCopy)
+  for (auto &ctx : I.devs) {
+    HIP_CHECK(hipSetDevice(ctx.dev));
+    TraceRange t("kernel/peer translate");
+    if (!ctx.translate.host[parity].empty()) ctx.translate.run_device(parity, ctx.comm);
+    ctx.translated.record(ctx.comm);
+  }
+
+  // (2) colocated sends: wait for inbox credit (slot reuse distance 2), pack into the peer's inbox over xGMI,
+  //     then raise the peer's arrival flag
+  for (auto &ctx : I.devs) {
+    if (ctx.coloSend.empty()) continue;
+    HIP_CHECK(hipSetDevice(ctx.dev));
+    TraceRange t("colo send");
+    if (I.epoch > 2) {
+      std::vector<uint64_t *> credits;
+      for (int ci : ctx.coloSend) credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownBlock));
+      wait_flags_device(credits, I.epoch - 2, I.errDev, 1, I.waitTimeout, ctx.comm);
+    }
+    ctx.coloPack.run_device(cv, ctx.comm);
+    std::vector<uint64_t *> arrived;
+    for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
+    signal_flags_device(arrived, I.epoch, ctx.comm);
+  }
+
+  // (3) RCCL: pack, one group of send/recv over every local device, unpack
+  if (I.rccl) {
+    TraceRange t("rccl");
+    for (auto &ctx : I.devs) {
+      if (ctx.rcclSend.empty()) continue;
+      HIP_CHECK(hipSetDevice(ctx.dev));
+      ctx.rcclPack.run_device(parity, ctx.comm);
+    }
+    NCCL_CHECK(ncclGroupStart());
+    for (auto &ctx : I.devs) {
+      for (int ci : ctx.rcclSend)
+        NCCL_CHECK(ncclSend(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, int(I.chans[ci].tag), ctx.nccl,
+                            ctx.comm));
+      for (int ci : ctx.rcclRecv)
+        NCCL_CHECK(ncclRecv(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, int(I.chans[ci].tag), ctx.nccl,
+                            ctx.comm));
+    }
+    NCCL_CHECK(ncclGroupEnd());
+    for (auto &ctx : I.devs) {
+      if (ctx.rcclRecv.empty()) continue;
+      HIP_CHECK(hipSetDevice(ctx.dev));
+      ctx.rcclUnpack.run_device(parity, ctx.comm);
+    }
+  }
+
+  // (4) host-staged fallback (blocks the host)
+  {
+    bool anyStaged = false;
+    for (auto &ctx : I.devs) anyStaged |= !ctx.stagedSend.empty() || !ctx.stagedRecv.empty();
+    if (anyStaged) {
+      TraceRange t("staged");
+      for (auto &ctx : I.devs) {
+        if (ctx.stagedSend.empty()) continue;
+        HIP_CHECK(hipSetDevice(ctx.dev));
+        ctx.stagedPack.run_device(parity, ctx.comm);
+        for (int ci : ctx.stagedSend)
+          HIP_CHECK(hipMemcpyAsync(I.chans[ci].hbuf, I.chans[ci].dbuf, size_t(I.chans[ci].bytes), hipMemcpyDeviceToHost,
+                                   ctx.comm));
+      }
+      for (auto &ctx : I.devs) {
+        if (ctx.stagedSend.empty()) continue;
+        HIP_CHECK(hipSetDevice(ctx.dev));
+        HIP_CHECK(hipStreamSynchronize(ctx.comm));
+        for (int ci : ctx.stagedSend) pg.send(I.chans[ci].remoteRank, I.chans[ci].tag, I.chans[ci].hbuf, size_t(I.chans[ci].bytes));
+      }
+      for (auto &ctx : I.devs) {
+        if (ctx.stagedRecv.empty()) continue;
+        HIP_CHECK(hipSetDevice(ctx.dev));
+        for (int ci : ctx.stagedRecv) {
+          pg.recv(I.chans[ci].remoteRank, I.chans[ci].tag, I.chans[ci].hbuf, size_t(I.chans[ci].bytes));
+          HIP_CHECK(hipMemcpyAsync(I.chans[ci].dbuf, I.chans[ci].hbuf, size_t(I.chans[ci].bytes), hipMemcpyHostToDevice,
+                                   ctx.comm));
+        }
+        ctx.stagedUnpack.run_device(parity, ctx.comm);
+      }
+    }
+  }
+
+  // (5) colocated receives: wait for arrival, unpack from our inbox, return the credit to the sender
+  for (auto &ctx : I.devs) {
+    if (ctx.coloRecv.empty()) continue;
+    HIP_CHECK(hipSetDevice(ctx.dev));
+    TraceRange t("colo recv");
+    std::vector<uint64_t *> arrived, credits;
+    for (int ci : ctx.coloRecv) {
+      arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownBlock));
+      credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
+    }
+    wait_flags_device(arrived, I.epoch, I.errDev, 2, I.waitTimeout, ctx.comm);
+    ctx.coloUnpack.run_device(cv, ctx.comm);
+    signal_flags_device(credits, I.epoch, ctx.comm);
+  }
+
+  // (6) halos written by peer devices of this process
+  for (auto &ctx : I.devs) {
+    HIP_CHECK(hipSetDevice(ctx.dev));
+    for (int src : ctx.peerWriters) I.devs[I.devIndex[src]].translated.wait_on(ctx.comm);
+    ctx.done.record(ctx.comm);
+  }
+}
+
+void DistributedDomain::swap() {
+  double t0 = 0;
+  if (exchangeStats_) {
+    pg_->barrier();
+    t0 = now_s();
+  }
+  TraceRange tr("swap");
+  for (auto &d : domains_) d.swap();
+  if (exchangeStats_) timeSwap_ += pg_->allreduce_max(now_s() - t0);
+}
+
+// ------------------------------------------------------------------------------------------------
+// ParaView CSV (reference src/stencil.cu:866-939), quantity names preserved
+// ------------------------------------------------------------------------------------------------
+void DistributedDomain::write_paraview(const std::string &prefix, bool zeroNaNs) {
+  TraceRange tr("write_paraview");
+  if (backend_ == Backend::Device) sync_exchange();
+  for (size_t di = 0; di < domains_.size(); ++di) {
+    const LocalDomain &d = domains_[di];
+    const int64_t id = int64_t(rank()) * int64_t(domains_.size()) + int64_t(di);
+    const std::string path = prefix + "_" + std::to_string(id) + ".txt";
+    std::vector<std::vector<unsigned char>> qs;
+    for (int64_t q = 0; q < d.num_data(); ++q) qs.push_back(d.interior_to_host(q));
+    FILE *f = std::fopen(path.c_str(), "w");
+    STENCIL_REQUIRE(f, "cannot open " << path);
+    std::fprintf(f, "Z,Y,X");
+    for (int64_t q = 0; q < d.num_data(); ++q) {
+      std::string n = d.name(q);
+      if (n.empty()) n = "data" + std::to_string(q);
+      std::fprintf(f, ",%s", n.c_str());
+    }
+    std::fprintf(f, "\n");
+    const Dim3 sz = d.size(), o = d.origin();
+    std::string line;
+    char buf[64];
+    for (int64_t z = 0; z < sz.z; ++z)
+      for (int64_t y = 0; y < sz.y; ++y)
+        for (int64_t x = 0; x < sz.x; ++x) {
+          line.clear();
+          std::snprintf(buf, sizeof(buf), "%ld,%ld,%ld", long(o.z + z), long(o.y + y), long(o.x + x));
+          line += buf;
+          const int64_t li = x + sz.x * (y + sz.y * z);
+          for (int64_t q = 0; q < d.num_data(); ++q) {
+            const unsigned char *p = qs[q].data() + li * d.elem_size(q);
+            switch (d.dtype(q)) {
+            case DType::F64: {
+              double v;
+              std::memcpy(&v, p, 8);
+              if (zeroNaNs && std::isnan(v)) v = 0;
+              std::snprintf(buf, sizeof(buf), ",%f", v);
+              break;
+            }
+            case DType::I32: {
+              int32_t v;
+              std::memcpy(&v, p, 4);
+              std::snprintf(buf, sizeof(buf), ",%d", v);
+              break;
+            }
+            case DType::I64: {
+              int64_t v;
+              std::memcpy(&v, p, 8);
+              std::snprintf(buf, sizeof(buf), ",%ld", long(v));
+              break;
+            }
+            default: {
+              if (d.elem_size(q) == 8) {
+                double v;
+                std::memcpy(&v, p, 8);
+                if (zeroNaNs && std::isnan(v)) v = 0;
+                std::snprintf(buf, sizeof(buf), ",%f", v);
+              } else {
+                float v = 0;
+                std::memcpy(&v, p, std::min<int64_t>(4, d.elem_size(q)));
+                if (zeroNaNs && std::isnan(v)) v = 0;
+                std::snprintf(buf, sizeof(buf), ",%f", double(v));
+              }
+            }
+            }
+            line += buf;
+          }
+          line += "\n";
+          std::fputs(line.c_str(), f);
+        }
+    std::fclose(f);
+  }
+}
+
+} // namespace stencil

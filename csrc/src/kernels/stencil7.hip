@@ -1,0 +1,496 @@
+// 7-point stencil kernels (Jacobi3D / Astaroth proxy) for gfx950. See stencil/kernels/stencil_ops.hpp.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "stencil/kernels/stencil_ops.hpp"
+#include "stencil/rt/hip_check.hpp"
+
+namespace stencil {
+
+template <typename T> struct Vec16;
+typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef double nd2 __attribute__((ext_vector_type(2)));
+template <> struct Vec16<float> {
+  using type = float4;
+  using native = nf4;
+  static constexpr int N = 4;
+};
+template <> struct Vec16<double> {
+  using type = double2;
+  using native = nd2;
+  static constexpr int N = 2;
+};
+
+template <typename T> __device__ __forceinline__ T vget(const typename Vec16<T>::type &v, int i);
+template <> __device__ __forceinline__ float vget<float>(const float4 &v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+template <> __device__ __forceinline__ double vget<double>(const double2 &v, int i) { return i == 0 ? v.x : v.y; }
+
+template <typename T> __device__ __forceinline__ T shfl_up1(T v);
+template <typename T> __device__ __forceinline__ T shfl_down1(T v);
+template <> __device__ __forceinline__ float shfl_up1<float>(float v) { return __shfl_up(v, 1, 64); }
+template <> __device__ __forceinline__ float shfl_down1<float>(float v) { return __shfl_down(v, 1, 64); }
+template <> __device__ __forceinline__ double shfl_up1<double>(double v) { return __shfl_up(v, 1, 64); }
+template <> __device__ __forceinline__ double shfl_down1<double>(double v) { return __shfl_down(v, 1, 64); }
+
+template <typename T> struct StencilArgs {
+  const T *src; // raw [0,0,0] of curr
+  T *dst;       // raw [0,0,0] of next
+  int64_t px, pxy;
+  int lox, loy, loz, hix, hiy, hiz; // region, raw coordinates
+  int x0;                           // raw x of chunk 0 (16-B aligned in memory)
+  int nchunks;                      // chunks covering [x0, hix)
+  int rawYm1;                       // clamp for row loads
+  int zc;                           // planes per block
+  int gx, gy, gz;                   // logical grid
+  // spheres, raw coordinates
+  int hx, hy, hz, cx, cy, cz;
+  int r1sq; // (radius+1)^2, 0 = disabled
+};
+
+// bijective XCD-aware remap: consecutive logical ids land on the same XCD (blocks b, b+8, ... share one)
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t hw, uint32_t n) {
+  const uint32_t q = n / 8, r = n % 8, xcd = hw % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + hw / 8;
+}
+
+template <typename T, int TY, int KIND, bool NT, bool REMAP>
+__global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
+  using VT = typename Vec16<T>::type;
+  constexpr int V = Vec16<T>::N;
+  const uint32_t nb = uint32_t(a.gx) * a.gy * a.gz;
+  const uint32_t hw = blockIdx.x;
+  const uint32_t lb = REMAP ? xcd_remap(hw, nb) : hw;
+  // logical order: z-chunk fastest, then y group, then x wave-column, so neighbours in z/y are consecutive
+  const int bz = int(lb % uint32_t(a.gz));
+  const int by = int((lb / uint32_t(a.gz)) % uint32_t(a.gy));
+  const int bx = int(lb / (uint32_t(a.gz) * a.gy));
+  const int lane = threadIdx.x;
+  const int c = bx * 64 + lane;
+  const bool cvalid = c < a.nchunks;
+  const int cl = cvalid ? c : a.nchunks - 1;
+  const int xb = a.x0 + cl * V;
+  const int ybase = a.loy + TY * (by * 4 + int(threadIdx.y));
+  const int zs = a.loz + bz * a.zc;
+  const int ze = min(zs + a.zc, a.hiz);
+  if (ybase >= a.hiy || zs >= ze) return; // wave-uniform
+
+  auto rowp = [&](int y, int z) -> const T * {
+    y = min(y, a.rawYm1);
+    return a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+  };
+  auto ld = [&](const T *p) -> VT { return *reinterpret_cast<const VT *>(p); };
+
+  VT prev[TY], cur[TY + 2], nxt[TY + 2];
+#pragma unroll
+  for (int i = 0; i < TY; ++i) prev[i] = ld(rowp(ybase + i, zs - 1));
+#pragma unroll
+  for (int i = 0; i < TY + 2; ++i) cur[i] = ld(rowp(ybase - 1 + i, zs));
+
+  const bool edgeL = lane == 0;
+  const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
+  const int r1sq = a.r1sq;
+
+  for (int z = zs; z < ze; ++z) {
+#pragma unroll
+    for (int i = 0; i < TY + 2; ++i) nxt[i] = ld(rowp(ybase - 1 + i, z + 1));
+
+    const int dzh = z - a.hz, dzc = z - a.cz;
+#pragma unroll
+    for (int i = 1; i <= TY; ++i) {
+      const int y = ybase + i - 1;
+      // x neighbours across lanes; wave edges read memory directly
+      T left = shfl_up1<T>(vget<T>(cur[i], V - 1));
+      T right = shfl_down1<T>(vget<T>(cur[i], 0));
+      const T *rp = rowp(y, z);
+      if (edgeL) left = rp[-1];
+      if (edgeR) right = rp[V];
+
+      // spheres: a row can only touch a sphere if its (y,z) distance is inside the radius
+      bool rowHot = false, rowCold = false;
+      int dyzh = 0, dyzc = 0;
+      if (KIND == 0 && r1sq > 0) {
+        const int dyh = y - a.hy, dyc = y - a.cy;
+        dyzh = dyh * dyh + dzh * dzh;
+        dyzc = dyc * dyc + dzc * dzc;
+        rowHot = dyzh < r1sq;
+        rowCold = dyzc < r1sq;
+      }
+      T out[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const T vpx = e < V - 1 ? vget<T>(cur[i], e + 1) : right;
+        const T vmx = e > 0 ? vget<T>(cur[i], e - 1) : left;
+        const T vpy = vget<T>(cur[i + 1], e);
+        const T vmy = vget<T>(cur[i - 1], e);
+        const T vpz = vget<T>(nxt[i], e);
+        const T vmz = vget<T>(prev[i - 1], e);
+        T val = T(0);
+        if (KIND == 0) {
+          val += vpx;
+          val += vmx;
+          val += vpy;
+          val += vmy;
+          val += vpz;
+          val += vmz;
+        } else {
+          val += vmx;
+          val += vmy;
+          val += vmz;
+          val += vpx;
+          val += vpy;
+          val += vpz;
+        }
+        val /= T(6);
+        if (KIND == 0) {
+          const int x = xb + e;
+          bool inHot = false;
+          if (rowHot) {
+            const int dx = x - a.hx;
+            inHot = dx * dx + dyzh < r1sq;
+          }
+          if (inHot) {
+            val = T(1);
+          } else if (rowCold) {
+            const int dx = x - a.cx;
+            if (dx * dx + dyzc < r1sq) val = T(0);
+          }
+        }
+        out[e] = val;
+      }
+      // masked store
+      if (cvalid && y < a.hiy) {
+        T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+        if (xb >= a.lox && xb + V <= a.hix) {
+          using NV = typename Vec16<T>::native;
+          NV v;
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[e] = out[e];
+          if (NT)
+            __builtin_nontemporal_store(v, reinterpret_cast<NV *>(dp));
+          else
+            *reinterpret_cast<NV *>(dp) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (xb + e >= a.lox && xb + e < a.hix) dp[e] = out[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TY; ++i) prev[i] = cur[i + 1];
+#pragma unroll
+    for (int i = 0; i < TY + 2; ++i) cur[i] = nxt[i];
+  }
+}
+
+// generic scalar fallback (unaligned layouts); also the device reference used by tests
+template <typename T, int KIND>
+__global__ __launch_bounds__(256) void stencil7_generic_kernel(StencilArgs<T> a) {
+  const int64_t nx = a.hix - a.lox, ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  const int64_t total = nx * ny * nz;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int x = a.lox + int(i % nx), y = a.loy + int((i / nx) % ny), z = a.loz + int(i / (nx * ny));
+    const T *p = a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + x;
+    T val = T(0);
+    if (KIND == 0) {
+      val += p[1];
+      val += p[-1];
+      val += p[a.px];
+      val += p[-a.px];
+      val += p[a.pxy];
+      val += p[-a.pxy];
+    } else {
+      val += p[-1];
+      val += p[-a.px];
+      val += p[-a.pxy];
+      val += p[1];
+      val += p[a.px];
+      val += p[a.pxy];
+    }
+    val /= T(6);
+    if (KIND == 0 && a.r1sq > 0) {
+      const int dh = (x - a.hx) * (x - a.hx) + (y - a.hy) * (y - a.hy) + (z - a.hz) * (z - a.hz);
+      const int dc = (x - a.cx) * (x - a.cx) + (y - a.cy) * (y - a.cy) + (z - a.cz) * (z - a.cz);
+      if (dh < a.r1sq)
+        val = T(1);
+      else if (dc < a.r1sq)
+        val = T(0);
+    }
+    a.dst[int64_t(z) * a.pxy + int64_t(y) * a.px + x] = val;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------------------
+template <typename T>
+static StencilArgs<T> make_args(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind,
+                                const Spheres &sph) {
+  StencilArgs<T> a{};
+  const Dim3 org = dom.accessor_origin();
+  const Dim3 p = dom.pitch(qi);
+  a.src = static_cast<const T *>(dom.curr_data(qi));
+  a.dst = static_cast<T *>(dom.next_data(qi));
+  a.px = p.x;
+  a.pxy = p.x * p.y;
+  const Rect3 r(region.lo - org, region.hi - org);
+  a.lox = int(r.lo.x);
+  a.loy = int(r.lo.y);
+  a.loz = int(r.lo.z);
+  a.hix = int(r.hi.x);
+  a.hiy = int(r.hi.y);
+  a.hiz = int(r.hi.z);
+  a.rawYm1 = int(dom.raw_size().y - 1);
+  if (kind == StencilKind::Jacobi && sph.enabled) {
+    a.hx = int(sph.hot.x - org.x);
+    a.hy = int(sph.hot.y - org.y);
+    a.hz = int(sph.hot.z - org.z);
+    a.cx = int(sph.cold.x - org.x);
+    a.cy = int(sph.cold.y - org.y);
+    a.cz = int(sph.cold.z - org.z);
+    a.r1sq = int((sph.radius + 1) * (sph.radius + 1));
+  }
+  return a;
+}
+
+template <typename T, int KIND>
+static void host_apply(const LocalDomain &dom, const StencilArgs<T> &a) {
+  (void)dom;
+  for (int z = a.loz; z < a.hiz; ++z)
+    for (int y = a.loy; y < a.hiy; ++y)
+      for (int x = a.lox; x < a.hix; ++x) {
+        const T *p = a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + x;
+        T val = T(0);
+        if (KIND == 0) {
+          val += p[1];
+          val += p[-1];
+          val += p[a.px];
+          val += p[-a.px];
+          val += p[a.pxy];
+          val += p[-a.pxy];
+        } else {
+          val += p[-1];
+          val += p[-a.px];
+          val += p[-a.pxy];
+          val += p[1];
+          val += p[a.px];
+          val += p[a.pxy];
+        }
+        val /= T(6);
+        if (KIND == 0 && a.r1sq > 0) {
+          const int dh = (x - a.hx) * (x - a.hx) + (y - a.hy) * (y - a.hy) + (z - a.hz) * (z - a.hz);
+          const int dc = (x - a.cx) * (x - a.cx) + (y - a.cy) * (y - a.cy) + (z - a.cz) * (z - a.cz);
+          if (dh < a.r1sq)
+            val = T(1);
+          else if (dc < a.r1sq)
+            val = T(0);
+        }
+        a.dst[int64_t(z) * a.pxy + int64_t(y) * a.px + x] = val;
+      }
+}
+
+template <typename T, int TY, int KIND>
+static void launch_fast(StencilArgs<T> a, const StencilTune &tune, hipStream_t stream) {
+  constexpr int V = Vec16<T>::N;
+  const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  a.gx = (a.nchunks + 63) / 64;
+  a.gy = (ny + 4 * TY - 1) / (4 * TY);
+  int zc = tune.zchunk;
+  if (zc <= 0) {
+    // aim for ~8 waves per SIMD worth of waves over 256 CUs, but keep z-chunks >= 8 planes
+    const int64_t wavesPerPlaneSet = int64_t(a.gx) * a.gy * 4;
+    const int64_t target = 256 * 4 * 6;
+    int64_t nzc = std::max<int64_t>(1, target / std::max<int64_t>(1, wavesPerPlaneSet));
+    zc = int(std::max<int64_t>(8, (nz + nzc - 1) / nzc));
+  }
+  a.zc = zc;
+  a.gz = (nz + zc - 1) / zc;
+  (void)V;
+  const uint32_t blocks = uint32_t(a.gx) * a.gy * a.gz;
+  const dim3 block(64, 4);
+  if (tune.nontemporal) {
+    if (tune.xcdRemap)
+      hipLaunchKernelGGL((stencil7_kernel<T, TY, KIND, true, true>), dim3(blocks), block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((stencil7_kernel<T, TY, KIND, true, false>), dim3(blocks), block, 0, stream, a);
+  } else {
+    if (tune.xcdRemap)
+      hipLaunchKernelGGL((stencil7_kernel<T, TY, KIND, false, true>), dim3(blocks), block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((stencil7_kernel<T, TY, KIND, false, false>), dim3(blocks), block, 0, stream, a);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T, int KIND>
+static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
+                    const StencilTune &tune) {
+  if (region.empty()) return;
+  StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
+  if (dom.backend() == Backend::Host) {
+    host_apply<T, KIND>(dom, a);
+    return;
+  }
+  constexpr int V = Vec16<T>::N;
+  const int rxm = int(dom.radius().x(-1));
+  // chunk grid anchored at the (64-B aligned) interior start
+  const int off = ((a.lox - rxm) % V + V) % V;
+  a.x0 = a.lox - off;
+  a.nchunks = (a.hix - a.x0 + V - 1) / V;
+  const bool alignedLayout = (reinterpret_cast<uintptr_t>(a.src + a.x0) % 16 == 0) &&
+                             (reinterpret_cast<uintptr_t>(a.dst + a.x0) % 16 == 0) && ((a.px * int64_t(sizeof(T))) % 16 == 0);
+  // vector loads and the right-edge neighbour stay inside the padded row (LocalDomain keeps >= V+1 tail elements)
+  const bool fits = a.x0 + int64_t(a.nchunks) * V < a.px - dom.pad_x(qi);
+  dom.set_device();
+  if (alignedLayout && fits && std::getenv("STENCIL_GENERIC_KERNEL") == nullptr) {
+    if (tune.ty == 4)
+      launch_fast<T, 4, KIND>(a, tune, stream);
+    else
+      launch_fast<T, 8, KIND>(a, tune, stream);
+  } else {
+    const int64_t total = Rect3(Dim3(a.lox, a.loy, a.loz), Dim3(a.hix, a.hiy, a.hiz)).extent().flatten();
+    const int blocks = int(std::min<int64_t>((total + 255) / 256, 4096));
+    hipLaunchKernelGGL((stencil7_generic_kernel<T, KIND>), dim3(blocks), dim3(256), 0, stream, a);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
+void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
+                    hipStream_t stream, const StencilTune &tune) {
+  STENCIL_REQUIRE(dom.radius().x(-1) >= 1 && dom.radius().x(1) >= 1 && dom.radius().y(-1) >= 1 &&
+                      dom.radius().y(1) >= 1 && dom.radius().z(-1) >= 1 && dom.radius().z(1) >= 1,
+                  "7-point stencil needs face radii >= 1");
+  const Rect3 cr = dom.get_compute_region();
+  STENCIL_REQUIRE(region.empty() || (cr.contains(region.lo) && region.hi.all_ge(region.lo) &&
+                                     region.hi.x <= cr.hi.x && region.hi.y <= cr.hi.y && region.hi.z <= cr.hi.z),
+                  "stencil region " << region << " outside compute region " << cr);
+  const DType dt = dom.dtype(qi);
+  const bool f32 = dt == DType::F32 || (dt == DType::Bytes && dom.elem_size(qi) == 4);
+  const bool f64 = dt == DType::F64 || (dt == DType::Bytes && dom.elem_size(qi) == 8);
+  if (f32) {
+    if (kind == StencilKind::Jacobi)
+      apply_t<float, 0>(dom, qi, region, sph, stream, tune);
+    else
+      apply_t<float, 1>(dom, qi, region, sph, stream, tune);
+  } else if (f64) {
+    if (kind == StencilKind::Jacobi)
+      apply_t<double, 0>(dom, qi, region, sph, stream, tune);
+    else
+      apply_t<double, 1>(dom, qi, region, sph, stream, tune);
+  } else {
+    LOG_FATAL("stencil7 supports fp32/fp64 quantities only");
+  }
+}
+
+void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
+                            const Spheres &sph, hipStream_t stream, const StencilTune &tune) {
+  for (const auto &r : regions) stencil7_apply(dom, qi, r, kind, sph, stream, tune);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// init kernels
+// ---------------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void fill_region_kernel(T *raw, int64_t px, int64_t pxy, int lox, int loy, int loz, int nx, int ny, int nz,
+                                   T v) {
+  const int64_t total = int64_t(nx) * ny * nz;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int x = lox + int(i % nx), y = loy + int((i / nx) % ny), z = loz + int(i / (int64_t(nx) * ny));
+    raw[int64_t(z) * pxy + int64_t(y) * px + x] = v;
+  }
+}
+
+template <typename T>
+__global__ void astaroth_init_kernel(T *raw, int64_t px, int64_t pxy, int rx, int ry, int rz, int nx, int ny, int nz,
+                                     int ox, int oy, int oz, int rxl, int ryl, int rzl, int rxh, int ryh, int rzh,
+                                     double period) {
+  const int64_t total = int64_t(rx) * ry * rz;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    const int x = int(i % rx), y = int((i / rx) % ry), z = int(i / (int64_t(rx) * ry));
+    T v;
+    if (x >= rxl && y >= ryl && z >= rzl && x < rx - rxh && y < ry - ryh && z < rz - rzh) {
+      v = T(sin(2 * 3.14159 / period * (ox + x) + 2 * 3.14159 / period * (oy + y) + 2 * 3.14159 / period * (oz + z)));
+    } else {
+      v = T(-10);
+    }
+    raw[int64_t(z) * pxy + int64_t(y) * px + x] = v;
+    (void)nx;
+    (void)ny;
+    (void)nz;
+  }
+}
+
+template <typename T> static void fill_t(const LocalDomain &dom, int64_t qi, const Rect3 &rawRegion, T v, bool curr, hipStream_t s) {
+  T *raw = static_cast<T *>(curr ? dom.curr_data(qi) : dom.next_data(qi));
+  const Dim3 p = dom.pitch(qi);
+  const Dim3 e = rawRegion.extent();
+  if (e.flatten() <= 0) return;
+  if (dom.backend() == Backend::Host) {
+    for (int64_t z = rawRegion.lo.z; z < rawRegion.hi.z; ++z)
+      for (int64_t y = rawRegion.lo.y; y < rawRegion.hi.y; ++y)
+        for (int64_t x = rawRegion.lo.x; x < rawRegion.hi.x; ++x) raw[z * p.x * p.y + y * p.x + x] = v;
+    return;
+  }
+  dom.set_device();
+  const int blocks = int(std::min<int64_t>((e.flatten() + 255) / 256, 8192));
+  hipLaunchKernelGGL((fill_region_kernel<T>), dim3(blocks), dim3(256), 0, s, raw, p.x, p.x * p.y, int(rawRegion.lo.x),
+                     int(rawRegion.lo.y), int(rawRegion.lo.z), int(e.x), int(e.y), int(e.z), v);
+  HIP_CHECK(hipGetLastError());
+}
+
+void jacobi_init(const LocalDomain &dom, int64_t qi, const Rect3 &region, hipStream_t stream) {
+  const Dim3 org = dom.accessor_origin();
+  const Rect3 r(region.lo - org, region.hi - org);
+  if (dom.elem_size(qi) == 8)
+    fill_t<double>(dom, qi, r, 0.5, true, stream);
+  else
+    fill_t<float>(dom, qi, r, 0.5f, true, stream);
+}
+
+void fill_value(const LocalDomain &dom, int64_t qi, double value, bool curr, hipStream_t stream) {
+  const Rect3 r(Dim3(0, 0, 0), dom.raw_size());
+  if (dom.elem_size(qi) == 8)
+    fill_t<double>(dom, qi, r, value, curr, stream);
+  else
+    fill_t<float>(dom, qi, r, float(value), curr, stream);
+}
+
+template <typename T> static void astaroth_init_t(const LocalDomain &dom, int64_t qi, double period, hipStream_t s) {
+  T *raw = static_cast<T *>(dom.curr_data(qi));
+  const Dim3 p = dom.pitch(qi), rs = dom.raw_size(), o = dom.origin();
+  const Radius &R = dom.radius();
+  if (dom.backend() == Backend::Host) {
+    for (int64_t z = 0; z < rs.z; ++z)
+      for (int64_t y = 0; y < rs.y; ++y)
+        for (int64_t x = 0; x < rs.x; ++x) {
+          T v;
+          if (x >= R.x(-1) && y >= R.y(-1) && z >= R.z(-1) && x < rs.x - R.x(1) && y < rs.y - R.y(1) && z < rs.z - R.z(1))
+            v = T(std::sin(2 * 3.14159 / period * double(o.x + x) + 2 * 3.14159 / period * double(o.y + y) +
+                           2 * 3.14159 / period * double(o.z + z)));
+          else
+            v = T(-10);
+          raw[z * p.x * p.y + y * p.x + x] = v;
+        }
+    return;
+  }
+  dom.set_device();
+  const int blocks = int(std::min<int64_t>((rs.flatten() + 255) / 256, 8192));
+  hipLaunchKernelGGL((astaroth_init_kernel<T>), dim3(blocks), dim3(256), 0, s, raw, p.x, p.x * p.y, int(rs.x), int(rs.y),
+                     int(rs.z), 0, 0, 0, int(o.x), int(o.y), int(o.z), int(R.x(-1)), int(R.y(-1)), int(R.z(-1)),
+                     int(R.x(1)), int(R.y(1)), int(R.z(1)), period);
+  HIP_CHECK(hipGetLastError());
+}
+
+void astaroth_init(const LocalDomain &dom, int64_t qi, double period, hipStream_t stream) {
+  if (dom.elem_size(qi) == 8)
+    astaroth_init_t<double>(dom, qi, period, stream);
+  else
+    astaroth_init_t<float>(dom, qi, period, stream);
+}
+
+} // namespace stencil

@@ -1,0 +1,104 @@
+#include "stencil/models/stencil_model.hpp"
+
+#include "stencil/rt/hip_check.hpp"
+#include "stencil/rt/trace.hpp"
+
+namespace stencil {
+
+StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::ProcGroup> pg) : cfg_(cfg) {
+  dd_.reset(new DistributedDomain(cfg.size.x, cfg.size.y, cfg.size.z, pg));
+  if (cfg.allDirections) {
+    dd_->set_radius(cfg.radius);
+  } else {
+    Radius r = Radius::constant(0);
+    r.set_face(cfg.radius);
+    dd_->set_radius(r);
+  }
+  dd_->set_methods(cfg.methods);
+  dd_->set_placement(cfg.placement);
+  if (!cfg.gpus.empty()) dd_->set_gpus(cfg.gpus);
+  if (cfg.setBackend) dd_->set_backend(cfg.backend);
+  for (int q = 0; q < cfg.quantities; ++q) {
+    const std::string name = cfg.kind == StencilKind::Jacobi && cfg.quantities == 1 ? "d" : "d" + std::to_string(q);
+    if (cfg.fp64)
+      dd_->add_data<double>(name);
+    else
+      dd_->add_data<float>(name);
+  }
+}
+
+StencilModel::~StencilModel() {
+  try {
+    for (auto &s : compute_) s.sync();
+  } catch (...) {
+  }
+}
+
+int64_t StencilModel::local_cells() const {
+  int64_t n = 0;
+  for (const auto &d : dd_->domains()) n += d.size().flatten();
+  return n;
+}
+
+hipStream_t StencilModel::compute_stream(size_t di) const { return compute_.empty() ? nullptr : compute_.at(di).get(); }
+
+void StencilModel::init() {
+  TraceRange tr("StencilModel::init");
+  dd_->realize();
+  const Rect3 cReg = dd_->get_compute_region();
+  sph_ = cfg_.kind == StencilKind::Jacobi ? Spheres::jacobi(cReg) : Spheres();
+  interiors_ = dd_->get_interior();
+  exteriors_ = dd_->get_exterior();
+  auto &doms = dd_->domains();
+  for (size_t di = 0; di < doms.size(); ++di) {
+    auto &d = doms[di];
+    if (d.backend() == Backend::Device) compute_.emplace_back(d.gpu(), Priority::DEFAULT);
+    hipStream_t s = compute_.empty() ? nullptr : compute_.back().get();
+    for (int64_t q = 0; q < d.num_data(); ++q) {
+      if (cfg_.kind == StencilKind::Jacobi)
+        jacobi_init(d, q, d.get_compute_region(), s);
+      else
+        astaroth_init(d, q, cfg_.astarothPeriod, s);
+    }
+  }
+  synchronize();
+  for (size_t di = 0; di < doms.size(); ++di)
+    if (!compute_.empty()) dd_->record_ready(di, compute_[di]);
+}
+
+void StencilModel::step() {
+  TraceRange tr("StencilModel::step");
+  auto &doms = dd_->domains();
+  const bool device = !compute_.empty();
+  if (cfg_.overlap) {
+    for (size_t di = 0; di < doms.size(); ++di)
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7_apply(doms[di], q, interiors_[di], cfg_.kind, sph_, device ? compute_[di].get() : nullptr, cfg_.tune);
+    dd_->exchange_async();
+    for (size_t di = 0; di < doms.size(); ++di) {
+      hipStream_t s = device ? compute_[di].get() : nullptr;
+      dd_->wait_exchange(di, s);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7_apply_regions(doms[di], q, exteriors_[di], cfg_.kind, sph_, s, cfg_.tune);
+    }
+  } else {
+    dd_->exchange_async();
+    for (size_t di = 0; di < doms.size(); ++di) {
+      hipStream_t s = device ? compute_[di].get() : nullptr;
+      dd_->wait_exchange(di, s);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, cfg_.tune);
+    }
+  }
+  dd_->swap();
+  if (device)
+    for (size_t di = 0; di < doms.size(); ++di) dd_->record_ready(di, compute_[di]);
+  ++steps_;
+}
+
+void StencilModel::synchronize() {
+  for (auto &s : compute_) s.sync();
+  if (dd_->realized()) dd_->sync_exchange();
+}
+
+} // namespace stencil

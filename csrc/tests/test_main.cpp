@@ -1,0 +1,172 @@
+// Native unit tests (ctest). Parity: reference test/test_cpu_*.cpp expectations (radius, mat2d, partition, qap)
+// plus host-backend exchange checks. GPU cases run only with --gpu.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "stencil/domain/distributed_domain.hpp"
+#include "stencil/rt/statistics.hpp"
+#include "stencil/topo/partition.hpp"
+#include "stencil/topo/qap.hpp"
+
+using namespace stencil;
+
+struct TestCase {
+  const char *name;
+  bool gpu;
+  std::function<void()> fn;
+};
+static std::vector<TestCase> &registry() {
+  static std::vector<TestCase> r;
+  return r;
+}
+struct Reg {
+  Reg(const char *n, bool g, std::function<void()> f) { registry().push_back({n, g, f}); }
+};
+static int g_fail = 0;
+#define CHECK(c)                                                                                                   \
+  do {                                                                                                             \
+    if (!(c)) {                                                                                                    \
+      std::fprintf(stderr, "  CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c);                                   \
+      ++g_fail;                                                                                                    \
+    }                                                                                                              \
+  } while (0)
+#define TEST(name, gpu) static void name(); static Reg reg_##name(#name, gpu, name); static void name()
+
+TEST(radius_basics, false) {
+  Radius r = Radius::constant(0);
+  r.set_face(2);
+  CHECK(r.x(1) == 2 && r.y(-1) == 2 && r.dir(1, 1, 0) == 0);
+  Radius c = Radius::constant(3);
+  CHECK(c.dir(1, -1, 1) == 3);
+  Radius f = Radius::face_edge_corner(3, 2, 1);
+  CHECK(f.dir(0, 0, 0) == 0 && f.dir(1, 0, 0) == 3 && f.dir(1, 1, 0) == 2 && f.dir(1, 1, 1) == 1);
+}
+
+TEST(dim3_fixed_bugs, false) {
+  CHECK(Dim3(1, 5, 3).max() == 5);
+  CHECK(Dim3(1, 2, 3) != Dim3(1, 2, 4));
+  CHECK(Dim3(-1, 5, 10).wrap(Dim3(4, 4, 4)) == Dim3(3, 1, 2));
+}
+
+TEST(partition_reference_values, false) {
+  RankPartition p(Dim3(10, 3, 1), 4);
+  CHECK(p.subdomain_size(Dim3(0, 0, 0)) == Dim3(3, 3, 1));
+  CHECK(p.subdomain_size(Dim3(3, 0, 0)) == Dim3(2, 3, 1));
+  CHECK(p.subdomain_origin(Dim3(3, 0, 0)) == Dim3(8, 0, 0));
+  RankPartition q(Dim3(10, 14, 2), 9);
+  CHECK(q.subdomain_origin(Dim3(1, 1, 0)) == Dim3(4, 5, 0));
+  CHECK(q.subdomain_origin(Dim3(2, 2, 0)) == Dim3(7, 10, 0));
+}
+
+TEST(qap_reference_values, false) {
+  const double inf = INFINITY;
+  Mat2D<double> bw = {{inf, 1, 10}, {1, inf, 1}, {10, 1, inf}};
+  Mat2D<double> comm = {{0, 10, 1}, {10, 0, 1}, {1, 1, 0}};
+  auto f = qap::solve(comm, make_reciprocal(bw));
+  CHECK(f[0] == 0 && f[1] == 2 && f[2] == 1);
+  Mat2D<double> bw9 = {{900, 75, 64, 64}, {75, 900, 64, 64}, {64, 64, 900, 75}, {64, 64, 75, 900}};
+  Mat2D<double> c9 = {{7, 5, 10, 1}, {5, 7, 1, 10}, {10, 1, 7, 5}, {1, 10, 5, 7}};
+  auto g = qap::solve(c9, make_reciprocal(bw9));
+  CHECK(g[0] == 0 && g[1] == 2 && g[2] == 1 && g[3] == 3);
+  auto h = qap::solve_catch(c9, make_reciprocal(bw9));
+  CHECK(h[0] == 3 && h[1] == 1 && h[2] == 2 && h[3] == 0);
+}
+
+TEST(statistics_trimean, false) {
+  Statistics s;
+  for (int i = 0; i < 8; ++i) s.insert(i);
+  CHECK(s.trimean() == (2 + 2 * 4 + 6) / 4.0);
+  CHECK(s.med() == 3.5);
+}
+
+// encode the global coordinate in the value; after exchange every halo cell must hold its periodic image
+static void check_exchange(Backend b, const Radius &r, const Dim3 &sz, std::vector<int> gpus, MethodFlags m) {
+  DistributedDomain dd(sz.x, sz.y, sz.z, comm::make_single_group());
+  dd.set_backend(b);
+  dd.set_radius(r);
+  dd.set_gpus(gpus);
+  dd.set_methods(m);
+  dd.set_plan_file("");
+  auto h = dd.add_data<int32_t>("coord");
+  dd.realize();
+  for (auto &d : dd.domains()) {
+    const Dim3 raw = d.raw_size();
+    std::vector<int32_t> v(size_t(raw.flatten()), -1);
+    const Dim3 org = d.accessor_origin();
+    for (int64_t z = 0; z < raw.z; ++z)
+      for (int64_t y = 0; y < raw.y; ++y)
+        for (int64_t x = 0; x < raw.x; ++x) {
+          const Dim3 g = org + Dim3(x, y, z);
+          if (d.get_compute_region().contains(g)) v[size_t(x + raw.x * (y + raw.y * z))] = int32_t(g.x + 1000 * g.y + 1000000 * g.z);
+        }
+    d.region_from_host(Dim3(0, 0, 0), raw, h.id(), v.data());
+  }
+  dd.exchange();
+  for (auto &d : dd.domains()) {
+    const Dim3 raw = d.raw_size();
+    auto bytes = d.quantity_to_host(h.id());
+    const int32_t *v = reinterpret_cast<const int32_t *>(bytes.data());
+    const Dim3 org = d.accessor_origin();
+    int bad = 0;
+    for (int64_t z = 0; z < raw.z; ++z)
+      for (int64_t y = 0; y < raw.y; ++y)
+        for (int64_t x = 0; x < raw.x; ++x) {
+          const Dim3 g = org + Dim3(x, y, z);
+          // which halo direction is this cell in?
+          const Rect3 cr = d.get_compute_region();
+          Dim3 dir(g.x < cr.lo.x ? -1 : (g.x >= cr.hi.x ? 1 : 0), g.y < cr.lo.y ? -1 : (g.y >= cr.hi.y ? 1 : 0),
+                   g.z < cr.lo.z ? -1 : (g.z >= cr.hi.z ? 1 : 0));
+          if (dir == Dim3(0, 0, 0)) continue;
+          const int32_t got = v[size_t(x + raw.x * (y + raw.y * z))];
+          // a halo cell in direction dir is filled iff the neighbour on that side sends (radius(dir) != 0) and the
+          // cell lies within the face-radius extents
+          if (r.dir(dir) == 0) continue;
+          const Dim3 w = g.wrap(sz);
+          const int32_t want = int32_t(w.x + 1000 * w.y + 1000000 * w.z);
+          if (got != want) ++bad;
+        }
+    CHECK(bad == 0);
+  }
+}
+
+TEST(host_exchange_uniform, false) { check_exchange(Backend::Host, Radius::constant(2), Dim3(10, 9, 8), {0}, MethodFlags::All); }
+TEST(host_exchange_two_subdomains, false) {
+  check_exchange(Backend::Host, Radius::constant(1), Dim3(12, 10, 10), {0, 0}, MethodFlags::All);
+}
+TEST(host_exchange_asymmetric, false) {
+  Radius r = Radius::constant(0);
+  r.dir(1, 0, 0) = 2;
+  r.dir(-1, 0, 0) = 1;
+  check_exchange(Backend::Host, r, Dim3(10, 10, 10), {0, 0, 0}, MethodFlags::All);
+}
+TEST(gpu_exchange_uniform, true) { check_exchange(Backend::Device, Radius::constant(2), Dim3(10, 9, 8), {0}, MethodFlags::All); }
+TEST(gpu_exchange_two_subdomains_rccl, true) {
+  check_exchange(Backend::Device, Radius::constant(1), Dim3(12, 10, 10), {0, 0}, MethodFlags::Rccl);
+}
+
+int main(int argc, char **argv) {
+  bool cpu = true, gpu = false;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--gpu")) gpu = true, cpu = false;
+    if (!std::strcmp(argv[i], "--all")) gpu = true, cpu = true;
+  }
+  int ran = 0;
+  for (auto &t : registry()) {
+    if ((t.gpu && !gpu) || (!t.gpu && !cpu)) continue;
+    const int before = g_fail;
+    try {
+      t.fn();
+    } catch (std::exception &e) {
+      std::fprintf(stderr, "  exception: %s\n", e.what());
+      ++g_fail;
+    }
+    std::printf("%s %s\n", g_fail == before ? "PASS" : "FAIL", t.name);
+    ++ran;
+  }
+  std::printf("%d tests, %d failures\n", ran, g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,67 @@
+"""In-tree build of the native runtime (CMake + Ninja, hipcc for gfx950).
+
+Produces ``stencil2_amd/_C*.so`` (pybind11 module) and ``stencil2_amd/libstencil2.so`` (the C++/HIP runtime),
+plus the C++ apps in ``build/bin``. Everything stays in-tree so it travels with a gpurun snapshot.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "stencil2_amd")
+BUILD = os.path.join(REPO, "build")
+
+
+def _sources():
+    pats = ["csrc/**/*.hpp", "csrc/**/*.cpp", "csrc/**/*.hip", "CMakeLists.txt"]
+    out = []
+    for p in pats:
+        out += glob.glob(os.path.join(REPO, p), recursive=True)
+    return out
+
+
+def _artifacts():
+    return glob.glob(os.path.join(PKG, "_C*.so")) + glob.glob(os.path.join(PKG, "libstencil2.so"))
+
+
+def is_stale() -> bool:
+    arts = _artifacts()
+    if len(arts) < 2 or not os.path.exists(os.path.join(BUILD, "bin", "jacobi3d")):
+        return True
+    newest_src = max(os.path.getmtime(s) for s in _sources())
+    oldest_art = min(os.path.getmtime(a) for a in arts)
+    return newest_src > oldest_art
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> None:
+    """Configure (once) and build everything; copy the Python-facing .so files into the package."""
+    jobs = jobs or min(8, os.cpu_count() or 8)
+    env = dict(os.environ)
+    env.setdefault("CMAKE_PREFIX_PATH", "/opt/rocm")
+    if not os.path.exists(os.path.join(BUILD, "build.ninja")):
+        os.makedirs(BUILD, exist_ok=True)
+        cmd = ["cmake", "-S", REPO, "-B", BUILD, "-G", "Ninja", "-DCMAKE_HIP_ARCHITECTURES=gfx950",
+               "-DCMAKE_BUILD_TYPE=Release", f"-DPython3_EXECUTABLE={sys.executable}"]
+        subprocess.run(cmd, check=True, env=env, stdout=None if verbose else subprocess.DEVNULL)
+    r = subprocess.run(["ninja", "-C", BUILD, f"-j{jobs}"], env=env, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("native build failed:\n" + (r.stdout or "")[-8000:] + (r.stderr or "")[-4000:])
+    for so in glob.glob(os.path.join(BUILD, "_C*.so")) + [os.path.join(BUILD, "libstencil2.so")]:
+        dst = os.path.join(PKG, os.path.basename(so))
+        tmp = dst + ".tmp"
+        shutil.copy2(so, tmp)
+        os.replace(tmp, dst)
+
+
+def ensure_built() -> None:
+    if is_stale():
+        build()
+
+
+if __name__ == "__main__":
+    build(verbose="-v" in sys.argv)
+    print("built:", _artifacts())

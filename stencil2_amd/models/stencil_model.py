@@ -1,0 +1,88 @@
+"""Jacobi3D / Astaroth proxy models on the native StencilModel (csrc/src/stencil_model.cpp).
+
+Each ``step()`` enqueues interior compute, the halo exchange and the exterior compute on HIP streams without any
+host synchronisation (see csrc/include/stencil/models/stencil_model.hpp); ``synchronize()`` waits.
+Reference: bin/jacobi3d.cu (weak scaling, hot/cold spheres), bin/astaroth_sim.cu (radius 3, 26 directions).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _C
+from ..parallel.process_group import get_group
+
+
+def weak_scaled_size(per_gpu: int, n: int) -> int:
+    """Reference weak-scaling rule: each axis = per_gpu * n**0.33333, rounded (bin/jacobi3d.cu:167-169)."""
+    return int(per_gpu * float(n) ** 0.33333 + 0.5)
+
+
+class StencilModel:
+    def __init__(self, size, kind=_C.StencilKind.Jacobi, radius: int = 1, all_directions: bool = False,
+                 quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
+                 placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, backend=None,
+                 tune: _C.StencilTune | None = None, group=None):
+        cfg = _C.StencilModelConfig()
+        cfg.size = _C.Dim3(*size)
+        cfg.kind = kind
+        cfg.radius = radius
+        cfg.all_directions = all_directions
+        cfg.quantities = quantities
+        cfg.fp64 = fp64
+        cfg.methods = methods
+        cfg.placement = placement
+        if gpus is not None:
+            cfg.gpus = list(gpus)
+        cfg.overlap = overlap
+        if backend is not None:
+            cfg.backend = backend
+        if tune is not None:
+            cfg.tune = tune
+        self.config = cfg
+        self._m = _C.StencilModel(cfg, group if group is not None else get_group())
+        self._dd = None
+
+    def init(self):
+        self._m.init()
+        self._dd = self._m.domain()
+        return self
+
+    def step(self):
+        self._m.step()
+
+    def run(self, iters: int):
+        self._m.run(iters)
+
+    def synchronize(self):
+        self._m.synchronize()
+
+    @property
+    def domain(self):
+        return self._dd
+
+    def cells(self) -> int:
+        return self._m.cells()
+
+    def local_cells(self) -> int:
+        return self._m.local_cells()
+
+    def field(self, di: int = 0, q: int = 0, curr: bool = True) -> torch.Tensor:
+        """Full (z, y, x) view including halo."""
+        return torch.from_dlpack(self._dd.dlpack(di, q, curr))
+
+    def interior(self, di: int = 0, q: int = 0) -> torch.Tensor:
+        d = self._dd.domain(di)
+        r, sz = d.radius(), d.size()
+        t = self.field(di, q)
+        return t[r.z(-1): r.z(-1) + sz.z, r.y(-1): r.y(-1) + sz.y, r.x(-1): r.x(-1) + sz.x]
+
+
+class Jacobi3D(StencilModel):
+    def __init__(self, size=(512, 512, 512), **kw):
+        super().__init__(size, kind=_C.StencilKind.Jacobi, radius=1, all_directions=False, **kw)
+
+
+class AstarothSim(StencilModel):
+    def __init__(self, size=(512, 512, 512), quantities: int = 8, **kw):
+        super().__init__(size, kind=_C.StencilKind.Astaroth, radius=3, all_directions=True, quantities=quantities,
+                         **kw)
