@@ -52,8 +52,29 @@ uint64_t finalize_segs(std::vector<CopySeg> &segs);
 // Host execution (CPU backend and reference for tests).
 void copy_segs_host(const std::vector<CopySeg> &segs);
 
-// Device execution. `dsegs` is a device-resident copy of the finalized segment list.
-void copy_segs_device(const CopySeg *dsegs, int nsegs, uint64_t totalUnits, hipStream_t stream);
+// Device execution plan: the segment list plus a per-block work table built on the host, so every block reads
+// its (segment, first item, count) with scalar loads and never searches. Items are whole rows for narrow rows
+// (x-faces: <= 4 units per row) and single vector units otherwise.
+struct CopyWork {
+  uint32_t seg;
+  uint32_t first;
+  uint32_t count;
+  uint32_t rows; // 1: items are rows, 0: items are units
+};
+struct CopyPlan {
+  CopySeg *dsegs = nullptr;
+  CopyWork *dwork = nullptr;
+  int nsegs = 0;
+  int nwork = 0;
+  int device = -1;
+  uint64_t bytes = 0;
+};
+// build + upload (device must be current). Segments must be finalized.
+CopyPlan make_copy_plan(const std::vector<CopySeg> &segs, int device);
+void free_copy_plan(CopyPlan &p);
+void copy_plan_device(const CopyPlan &p, hipStream_t stream);
+// one-shot helper (allocates a temporary plan, synchronous)
+void copy_segs_device_sync(std::vector<CopySeg> segs, int device);
 
 // ---- cross-process signalling for the IPC transport (device flags, see DistributedDomain colocated path) ----
 // Lane i polls *flags[i] (relaxed, system scope, s_sleep back-off) until >= target, then one system-scope

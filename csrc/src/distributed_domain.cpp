@@ -64,30 +64,24 @@ static double now_s() {
 // internal state
 // ------------------------------------------------------------------------------------------------
 
-// segment list with up to 4 variants (domain parity x inbox slot), host and device copies
+// segment list with up to 4 variants (domain parity x inbox slot), host copies and device copy plans
 struct SegList {
   std::vector<CopySeg> host[4];
-  CopySeg *dev[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint64_t units[4] = {0, 0, 0, 0};
+  CopyPlan plan[4];
   bool empty() const { return host[0].empty() && host[1].empty() && host[2].empty() && host[3].empty(); }
   void upload(int device) {
     for (int v = 0; v < 4; ++v) {
-      units[v] = finalize_segs(host[v]);
+      finalize_segs(host[v]);
       if (device >= 0 && !host[v].empty()) {
         HIP_CHECK(hipSetDevice(device));
-        HIP_CHECK(hipMalloc(&dev[v], sizeof(CopySeg) * host[v].size()));
-        HIP_CHECK(hipMemcpy(dev[v], host[v].data(), sizeof(CopySeg) * host[v].size(), hipMemcpyHostToDevice));
+        plan[v] = make_copy_plan(host[v], device);
       }
     }
   }
-  void run_device(int v, hipStream_t s) const { copy_segs_device(dev[v], int(host[v].size()), units[v], s); }
+  void run_device(int v, hipStream_t s) const { copy_plan_device(plan[v], s); }
   void run_host(int v) const { copy_segs_host(host[v]); }
   void release() {
-    for (auto &d : dev)
-      if (d) {
-        (void)hipFree(d);
-        d = nullptr;
-      }
+    for (auto &p : plan) free_copy_plan(p);
   }
 };
 

@@ -71,58 +71,100 @@ template <uint32_t V> __device__ __forceinline__ void copy_unit(char *dst, const
   *reinterpret_cast<T *>(dst) = *reinterpret_cast<const T *>(src);
 }
 
-// One launch walks every segment. Units are assigned with a grid-stride loop over the flattened unit space;
-// the owning segment is found by binary search over unit_begin (segments are few and L1/L2 resident).
-// All index math past the segment base is 32-bit (a segment holds < 2^32 units) to keep VALU cost per 16-B unit
-// well under the HBM-bound budget.
-__global__ __launch_bounds__(256) void copy_segs_kernel(const CopySeg *__restrict__ segs, int nsegs, uint64_t total) {
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t u = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; u < total; u += stride) {
-    int lo = 0, hi = nsegs - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (segs[mid].unit_begin <= u)
-        lo = mid;
-      else
-        hi = mid - 1;
+template <uint32_t V> __device__ __forceinline__ void copy_row(char *dst, const char *src, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) copy_unit<V>(dst + k * V, src + k * V);
+}
+
+// One block per work-table entry; the entry and its segment are wave-uniform (scalar loads). Narrow-row segments
+// (x-faces) assign one row per thread, wide rows one 16-B unit per thread, so a y/z face moves 1 KiB per wave
+// instruction and the strided x-face rows are spread over every lane.
+__global__ __launch_bounds__(256) void copy_plan_kernel(const CopySeg *__restrict__ segs,
+                                                        const CopyWork *__restrict__ work) {
+  const CopyWork w = work[blockIdx.x];
+  const CopySeg &s = segs[w.seg];
+  const uint32_t vec = s.vec, ru = s.row_units, ny = s.ny;
+  const int64_t sys = s.src_ystride, szs = s.src_zstride, dys = s.dst_ystride, dzs = s.dst_zstride;
+  const char *src = s.src;
+  char *dst = s.dst;
+  for (uint32_t it = threadIdx.x; it < w.count; it += blockDim.x) {
+    const uint32_t item = w.first + it;
+    uint32_t r, c;
+    if (w.rows) {
+      r = item;
+      c = 0;
+    } else {
+      r = item / ru;
+      c = item - r * ru;
     }
-    const CopySeg &s = segs[lo];
-    const uint32_t lu = uint32_t(u - s.unit_begin);
-    const uint32_t c = lu % s.row_units;
-    const uint32_t r = lu / s.row_units;
-    const uint32_t y = r % s.ny;
-    const uint32_t z = r / s.ny;
-    const uint32_t vec = s.vec;
-    const char *sp = s.src + int64_t(z) * s.src_zstride + int64_t(y) * s.src_ystride + uint64_t(c) * vec;
-    char *dp = s.dst + int64_t(z) * s.dst_zstride + int64_t(y) * s.dst_ystride + uint64_t(c) * vec;
+    const uint32_t y = r % ny, z = r / ny;
+    const char *sp = src + int64_t(z) * szs + int64_t(y) * sys + uint64_t(c) * vec;
+    char *dp = dst + int64_t(z) * dzs + int64_t(y) * dys + uint64_t(c) * vec;
+    const uint32_t n = w.rows ? ru : 1;
     switch (vec) {
     case 16:
-      copy_unit<16>(dp, sp);
+      copy_row<16>(dp, sp, n);
       break;
     case 8:
-      copy_unit<8>(dp, sp);
+      copy_row<8>(dp, sp, n);
       break;
     case 4:
-      copy_unit<4>(dp, sp);
+      copy_row<4>(dp, sp, n);
       break;
     case 2:
-      copy_unit<2>(dp, sp);
+      copy_row<2>(dp, sp, n);
       break;
     default:
-      copy_unit<1>(dp, sp);
+      copy_row<1>(dp, sp, n);
       break;
     }
   }
 }
 
-void copy_segs_device(const CopySeg *dsegs, int nsegs, uint64_t totalUnits, hipStream_t stream) {
-  if (!nsegs || !totalUnits) return;
-  const int threads = 256;
-  // enough blocks to cover the units, capped at 8 blocks/CU over 256 CUs (grid-stride for the rest)
-  const uint64_t want = (totalUnits + threads - 1) / threads;
-  const int blocks = int(std::min<uint64_t>(want, 2048));
-  hipLaunchKernelGGL(copy_segs_kernel, dim3(blocks), dim3(threads), 0, stream, dsegs, nsegs, totalUnits);
+CopyPlan make_copy_plan(const std::vector<CopySeg> &segs, int device) {
+  CopyPlan p;
+  p.device = device;
+  std::vector<CopyWork> work;
+  const uint32_t perBlockUnits = 256 * 4; // items per block
+  for (uint32_t si = 0; si < segs.size(); ++si) {
+    const CopySeg &s = segs[si];
+    if (!s.units) continue;
+    p.bytes += s.units * s.vec;
+    const bool rows = s.row_units <= 4;
+    const uint64_t items = rows ? s.units / s.row_units : s.units;
+    STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
+    for (uint64_t f = 0; f < items; f += perBlockUnits)
+      work.push_back({si, uint32_t(f), uint32_t(std::min<uint64_t>(perBlockUnits, items - f)), rows ? 1u : 0u});
+  }
+  p.nsegs = int(segs.size());
+  p.nwork = int(work.size());
+  if (p.nwork == 0) return p;
+  HIP_CHECK(hipMalloc(&p.dsegs, sizeof(CopySeg) * segs.size()));
+  HIP_CHECK(hipMemcpy(p.dsegs, segs.data(), sizeof(CopySeg) * segs.size(), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMalloc(&p.dwork, sizeof(CopyWork) * work.size()));
+  HIP_CHECK(hipMemcpy(p.dwork, work.data(), sizeof(CopyWork) * work.size(), hipMemcpyHostToDevice));
+  return p;
+}
+
+void free_copy_plan(CopyPlan &p) {
+  if (p.dsegs) (void)hipFree(p.dsegs);
+  if (p.dwork) (void)hipFree(p.dwork);
+  p.dsegs = nullptr;
+  p.dwork = nullptr;
+  p.nwork = 0;
+}
+
+void copy_plan_device(const CopyPlan &p, hipStream_t stream) {
+  if (!p.nwork) return;
+  hipLaunchKernelGGL(copy_plan_kernel, dim3(p.nwork), dim3(256), 0, stream, p.dsegs, p.dwork);
   HIP_CHECK(hipGetLastError());
+}
+
+void copy_segs_device_sync(std::vector<CopySeg> segs, int device) {
+  finalize_segs(segs);
+  CopyPlan p = make_copy_plan(segs, device);
+  copy_plan_device(p, nullptr);
+  HIP_CHECK(hipDeviceSynchronize());
+  free_copy_plan(p);
 }
 
 // ------------------------------------------------------------------------------------------------

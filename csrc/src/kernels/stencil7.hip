@@ -58,6 +58,21 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t hw, uint32_t n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + hw / 8;
 }
 
+// x / 6 rounded to nearest-even, bit-identical to IEEE division. fp32: two FMAs around the reciprocal (verified
+// exhaustively over all 2^32 inputs for |x| >= 2^-100; the subnormal-result range takes the true division).
+template <typename T> __device__ __forceinline__ T div6(T x) { return x / T(6); }
+template <> __device__ __forceinline__ float div6<float>(float x) {
+  constexpr float c = 1.0f / 6.0f;
+  const float q0 = x * c;
+  const float r = __builtin_fmaf(-q0, 6.0f, x);
+  float q = __builtin_fmaf(r, c, q0);
+  if (__builtin_expect(__builtin_fabsf(x) < 0x1p-100f, 0)) q = x / 6.0f;
+  return q;
+}
+
+// 2.5D z-march. Lane = one 16-B x-chunk; wave = 64 chunks x TY rows; block = 4 waves stacked in y.
+// Per z step a lane issues TY+2 row loads of plane z+1 (plus the two wave-edge scalars), then emits TY rows of
+// plane z from registers: x-neighbours by ds_bpermute, y-neighbours from the adjacent rows, z from prev/next.
 template <typename T, int TY, int KIND, bool NT, bool REMAP>
 __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
   using VT = typename Vec16<T>::type;
@@ -65,7 +80,7 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
   const uint32_t nb = uint32_t(a.gx) * a.gy * a.gz;
   const uint32_t hw = blockIdx.x;
   const uint32_t lb = REMAP ? xcd_remap(hw, nb) : hw;
-  // logical order: z-chunk fastest, then y group, then x wave-column, so neighbours in z/y are consecutive
+  // logical order: z-chunk fastest, then y group, then x wave-column
   const int bz = int(lb % uint32_t(a.gz));
   const int by = int((lb / uint32_t(a.gz)) % uint32_t(a.gy));
   const int bx = int(lb / (uint32_t(a.gz) * a.gy));
@@ -79,6 +94,10 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
   const int ze = min(zs + a.zc, a.hiz);
   if (ybase >= a.hiy || zs >= ze) return; // wave-uniform
 
+  const bool edgeL = lane == 0;
+  const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
+  const bool fullX = xb >= a.lox && xb + V <= a.hix;
+
   auto rowp = [&](int y, int z) -> const T * {
     y = min(y, a.rawYm1);
     return a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
@@ -86,40 +105,39 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
   auto ld = [&](const T *p) -> VT { return *reinterpret_cast<const VT *>(p); };
 
   VT prev[TY], cur[TY + 2], nxt[TY + 2];
+  T curL[TY], curR[TY], nxtL[TY], nxtR[TY];
 #pragma unroll
   for (int i = 0; i < TY; ++i) prev[i] = ld(rowp(ybase + i, zs - 1));
 #pragma unroll
   for (int i = 0; i < TY + 2; ++i) cur[i] = ld(rowp(ybase - 1 + i, zs));
+#pragma unroll
+  for (int i = 0; i < TY; ++i) {
+    const T *p = rowp(ybase + i, zs);
+    curL[i] = edgeL ? p[-1] : T(0);
+    curR[i] = edgeR ? p[V] : T(0);
+  }
 
-  const bool edgeL = lane == 0;
-  const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
   const int r1sq = a.r1sq;
-
   for (int z = zs; z < ze; ++z) {
 #pragma unroll
     for (int i = 0; i < TY + 2; ++i) nxt[i] = ld(rowp(ybase - 1 + i, z + 1));
+    if (z + 1 < ze) {
+#pragma unroll
+      for (int i = 0; i < TY; ++i) {
+        const T *p = rowp(ybase + i, z + 1);
+        nxtL[i] = edgeL ? p[-1] : T(0);
+        nxtR[i] = edgeR ? p[V] : T(0);
+      }
+    }
 
     const int dzh = z - a.hz, dzc = z - a.cz;
 #pragma unroll
     for (int i = 1; i <= TY; ++i) {
       const int y = ybase + i - 1;
-      // x neighbours across lanes; wave edges read memory directly
-      T left = shfl_up1<T>(vget<T>(cur[i], V - 1));
-      T right = shfl_down1<T>(vget<T>(cur[i], 0));
-      const T *rp = rowp(y, z);
-      if (edgeL) left = rp[-1];
-      if (edgeR) right = rp[V];
-
-      // spheres: a row can only touch a sphere if its (y,z) distance is inside the radius
-      bool rowHot = false, rowCold = false;
-      int dyzh = 0, dyzc = 0;
-      if (KIND == 0 && r1sq > 0) {
-        const int dyh = y - a.hy, dyc = y - a.cy;
-        dyzh = dyh * dyh + dzh * dzh;
-        dyzc = dyc * dyc + dzc * dzc;
-        rowHot = dyzh < r1sq;
-        rowCold = dyzc < r1sq;
-      }
+      const T sl = shfl_up1<T>(vget<T>(cur[i], V - 1));
+      const T sr = shfl_down1<T>(vget<T>(cur[i], 0));
+      const T left = edgeL ? curL[i - 1] : sl;
+      const T right = edgeR ? curR[i - 1] : sr;
       T out[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) {
@@ -129,43 +147,43 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
         const T vmy = vget<T>(cur[i - 1], e);
         const T vpz = vget<T>(nxt[i], e);
         const T vmz = vget<T>(prev[i - 1], e);
-        T val = T(0);
+        T val;
+        // leading 0 + as in the reference (keeps the sign of zero identical)
         if (KIND == 0) {
-          val += vpx;
+          val = T(0) + vpx;
           val += vmx;
           val += vpy;
           val += vmy;
           val += vpz;
           val += vmz;
         } else {
-          val += vmx;
+          val = T(0) + vmx;
           val += vmy;
           val += vmz;
           val += vpx;
           val += vpy;
           val += vpz;
         }
-        val /= T(6);
-        if (KIND == 0) {
-          const int x = xb + e;
-          bool inHot = false;
-          if (rowHot) {
-            const int dx = x - a.hx;
-            inHot = dx * dx + dyzh < r1sq;
-          }
-          if (inHot) {
-            val = T(1);
-          } else if (rowCold) {
-            const int dx = x - a.cx;
-            if (dx * dx + dyzc < r1sq) val = T(0);
+        out[e] = div6<T>(val);
+      }
+      if (KIND == 0 && r1sq > 0) {
+        // spheres: only rows whose (y,z) distance is inside the radius can contain sphere cells (wave-uniform)
+        const int dyh = y - a.hy, dyc = y - a.cy;
+        const int dyzh = dyh * dyh + dzh * dzh;
+        const int dyzc = dyc * dyc + dzc * dzc;
+        if (dyzh < r1sq || dyzc < r1sq) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const int x = xb + e;
+            const bool hot = (x - a.hx) * (x - a.hx) + dyzh < r1sq;
+            const bool cold = (x - a.cx) * (x - a.cx) + dyzc < r1sq;
+            out[e] = hot ? T(1) : (cold ? T(0) : out[e]);
           }
         }
-        out[e] = val;
       }
-      // masked store
       if (cvalid && y < a.hiy) {
         T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
-        if (xb >= a.lox && xb + V <= a.hix) {
+        if (fullX) {
           using NV = typename Vec16<T>::native;
           NV v;
 #pragma unroll
@@ -185,6 +203,58 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
     for (int i = 0; i < TY; ++i) prev[i] = cur[i + 1];
 #pragma unroll
     for (int i = 0; i < TY + 2; ++i) cur[i] = nxt[i];
+#pragma unroll
+    for (int i = 0; i < TY; ++i) {
+      curL[i] = nxtL[i];
+      curR[i] = nxtR[i];
+    }
+  }
+}
+
+// Several thin regions (the exterior slabs) in one launch, one thread per cell.
+constexpr int kMaxRegions = 8;
+struct RegionTable {
+  int lo[kMaxRegions][3];
+  int ext[kMaxRegions][3];
+  int64_t begin[kMaxRegions + 1];
+  int n;
+};
+
+template <typename T, int KIND>
+__global__ __launch_bounds__(256) void stencil7_regions_kernel(StencilArgs<T> a, RegionTable rt) {
+  const int64_t total = rt.begin[rt.n];
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    int k = 0;
+    while (k + 1 < rt.n && rt.begin[k + 1] <= i) ++k;
+    const int64_t li = i - rt.begin[k];
+    const int nx = rt.ext[k][0], ny = rt.ext[k][1];
+    const int x = rt.lo[k][0] + int(li % nx);
+    const int y = rt.lo[k][1] + int((li / nx) % ny);
+    const int z = rt.lo[k][2] + int(li / (int64_t(nx) * ny));
+    const T *p = a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + x;
+    T val = T(0);
+    if (KIND == 0) {
+      val += p[1];
+      val += p[-1];
+      val += p[a.px];
+      val += p[-a.px];
+      val += p[a.pxy];
+      val += p[-a.pxy];
+    } else {
+      val += p[-1];
+      val += p[-a.px];
+      val += p[-a.pxy];
+      val += p[1];
+      val += p[a.px];
+      val += p[a.pxy];
+    }
+    val = div6<T>(val);
+    if (KIND == 0 && a.r1sq > 0) {
+      const int dh = (x - a.hx) * (x - a.hx) + (y - a.hy) * (y - a.hy) + (z - a.hz) * (z - a.hz);
+      const int dc = (x - a.cx) * (x - a.cx) + (y - a.cy) * (y - a.cy) + (z - a.cz) * (z - a.cz);
+      val = dh < a.r1sq ? T(1) : (dc < a.r1sq ? T(0) : val);
+    }
+    a.dst[int64_t(z) * a.pxy + int64_t(y) * a.px + x] = val;
   }
 }
 
@@ -302,10 +372,10 @@ static void launch_fast(StencilArgs<T> a, const StencilTune &tune, hipStream_t s
   a.gy = (ny + 4 * TY - 1) / (4 * TY);
   int zc = tune.zchunk;
   if (zc <= 0) {
-    // aim for ~8 waves per SIMD worth of waves over 256 CUs, but keep z-chunks >= 8 planes
-    const int64_t wavesPerPlaneSet = int64_t(a.gx) * a.gy * 4;
-    const int64_t target = 256 * 4 * 6;
-    int64_t nzc = std::max<int64_t>(1, target / std::max<int64_t>(1, wavesPerPlaneSet));
+    // ~2 rounds of resident blocks (4 blocks of 4 waves per CU at <=128 VGPRs) over 256 CUs, z-chunks >= 8 planes
+    const int64_t cols = int64_t(a.gx) * a.gy;
+    const int64_t targetBlocks = 2048;
+    const int64_t nzc = std::max<int64_t>(1, (targetBlocks + cols - 1) / cols);
     zc = int(std::max<int64_t>(8, (nz + nzc - 1) / nzc));
   }
   a.zc = zc;
@@ -387,9 +457,55 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
   }
 }
 
+template <typename T, int KIND>
+static void apply_regions_t(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, const Spheres &sph,
+                            hipStream_t stream) {
+  StencilArgs<T> a = make_args<T>(dom, qi, dom.get_compute_region(), KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth,
+                                  sph);
+  const Dim3 org = dom.accessor_origin();
+  for (size_t k0 = 0; k0 < regions.size(); k0 += kMaxRegions) {
+    RegionTable rt{};
+    rt.begin[0] = 0;
+    for (size_t k = k0; k < regions.size() && rt.n < kMaxRegions; ++k) {
+      if (regions[k].empty()) continue;
+      const Rect3 r(regions[k].lo - org, regions[k].hi - org);
+      const Dim3 e = r.extent();
+      rt.lo[rt.n][0] = int(r.lo.x);
+      rt.lo[rt.n][1] = int(r.lo.y);
+      rt.lo[rt.n][2] = int(r.lo.z);
+      rt.ext[rt.n][0] = int(e.x);
+      rt.ext[rt.n][1] = int(e.y);
+      rt.ext[rt.n][2] = int(e.z);
+      rt.begin[rt.n + 1] = rt.begin[rt.n] + e.flatten();
+      ++rt.n;
+    }
+    if (rt.n == 0) continue;
+    const int64_t total = rt.begin[rt.n];
+    const int blocks = int(std::min<int64_t>((total + 255) / 256, 8192));
+    hipLaunchKernelGGL((stencil7_regions_kernel<T, KIND>), dim3(blocks), dim3(256), 0, stream, a, rt);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
 void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
                             const Spheres &sph, hipStream_t stream, const StencilTune &tune) {
-  for (const auto &r : regions) stencil7_apply(dom, qi, r, kind, sph, stream, tune);
+  if (dom.backend() == Backend::Host || std::getenv("STENCIL_EXTERIOR_PER_REGION")) {
+    for (const auto &r : regions) stencil7_apply(dom, qi, r, kind, sph, stream, tune);
+    return;
+  }
+  for (const auto &r : regions) {
+    const Rect3 cr = dom.get_compute_region();
+    STENCIL_REQUIRE(r.empty() || (cr.contains(r.lo) && r.hi.x <= cr.hi.x && r.hi.y <= cr.hi.y && r.hi.z <= cr.hi.z),
+                    "stencil region " << r << " outside compute region " << cr);
+  }
+  dom.set_device();
+  const bool f64 = dom.elem_size(qi) == 8;
+  if (!f64)
+    kind == StencilKind::Jacobi ? apply_regions_t<float, 0>(dom, qi, regions, sph, stream)
+                                : apply_regions_t<float, 1>(dom, qi, regions, sph, stream);
+  else
+    kind == StencilKind::Jacobi ? apply_regions_t<double, 0>(dom, qi, regions, sph, stream)
+                                : apply_regions_t<double, 1>(dom, qi, regions, sph, stream);
 }
 
 // ---------------------------------------------------------------------------------------------------------

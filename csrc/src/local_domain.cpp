@@ -164,17 +164,10 @@ std::vector<unsigned char> LocalDomain::region_to_host(const Dim3 &pos, const Di
   }
   set_device();
   char *dbuf = nullptr;
-  CopySeg *dseg = nullptr;
   HIP_CHECK(hipMalloc(&dbuf, out.size()));
   dense.base = dbuf;
-  std::vector<CopySeg> segs{make_copy_seg(box(qi, curr, pos), dense, ext, es)};
-  const uint64_t units = finalize_segs(segs);
-  HIP_CHECK(hipMalloc(&dseg, sizeof(CopySeg) * segs.size()));
-  HIP_CHECK(hipMemcpy(dseg, segs.data(), sizeof(CopySeg) * segs.size(), hipMemcpyHostToDevice));
-  copy_segs_device(dseg, int(segs.size()), units, nullptr);
-  HIP_CHECK(hipDeviceSynchronize());
+  copy_segs_device_sync({make_copy_seg(box(qi, curr, pos), dense, ext, es)}, dev_);
   HIP_CHECK(hipMemcpy(out.data(), dbuf, out.size(), hipMemcpyDeviceToHost));
-  HIP_CHECK(hipFree(dseg));
   HIP_CHECK(hipFree(dbuf));
   return out;
 }
@@ -196,17 +189,10 @@ void LocalDomain::region_from_host(const Dim3 &pos, const Dim3 &ext, int64_t qi,
   }
   set_device();
   char *dbuf = nullptr;
-  CopySeg *dseg = nullptr;
   HIP_CHECK(hipMalloc(&dbuf, bytes));
   HIP_CHECK(hipMemcpy(dbuf, src, bytes, hipMemcpyHostToDevice));
   dense.base = dbuf;
-  std::vector<CopySeg> segs{make_copy_seg(dense, box(qi, curr, pos), ext, es)};
-  const uint64_t units = finalize_segs(segs);
-  HIP_CHECK(hipMalloc(&dseg, sizeof(CopySeg) * segs.size()));
-  HIP_CHECK(hipMemcpy(dseg, segs.data(), sizeof(CopySeg) * segs.size(), hipMemcpyHostToDevice));
-  copy_segs_device(dseg, int(segs.size()), units, nullptr);
-  HIP_CHECK(hipDeviceSynchronize());
-  HIP_CHECK(hipFree(dseg));
+  copy_segs_device_sync({make_copy_seg(dense, box(qi, curr, pos), ext, es)}, dev_);
   HIP_CHECK(hipFree(dbuf));
 }
 

@@ -52,7 +52,8 @@ def jacobi_step_reference(u: torch.Tensor) -> torch.Tensor:
     my = torch.roll(u, 1, 1)
     pz = torch.roll(u, -1, 0)
     mz = torch.roll(u, 1, 0)
-    val = px + mx
+    val = torch.zeros_like(u) + px  # leading 0 + as in the reference kernel (sign of zero)
+    val = val + mx
     val = val + py
     val = val + my
     val = val + pz
@@ -72,7 +73,8 @@ def astaroth_step_reference(u: torch.Tensor) -> torch.Tensor:
     px = torch.roll(u, -1, 2)
     py = torch.roll(u, -1, 1)
     pz = torch.roll(u, -1, 0)
-    val = mx + my
+    val = torch.zeros_like(u) + mx
+    val = val + my
     val = val + mz
     val = val + px
     val = val + py
