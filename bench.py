@@ -113,7 +113,7 @@ def main():
             "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": L,
                        "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
                        "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods),
-                       "overlap": not args.no_overlap},
+                       "overlap": model.overlapping()},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
                       "gcells_per_gpu": round(gcells / n, 3)},

@@ -36,7 +36,8 @@ struct Spheres {
 };
 
 struct StencilTune {
-  int ty = 8;     // rows per lane (4 or 8)
+  int variant = 0; // 0: LDS-shared y-halo kernel (default), 1: register-only kernel
+  int ty = 4;     // rows per lane (variant 0: 2/4/8, variant 1: 4/8)
   int zchunk = 0; // planes per block (0 = auto)
   bool xcdRemap = true;
   bool nontemporal = true;

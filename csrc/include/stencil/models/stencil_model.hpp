@@ -4,8 +4,8 @@
 //
 // One step() (overlap mode) is fully stream-ordered, no host synchronisation:
 //   compute[d]: interior(curr -> next)                               (overlaps the exchange)
-//   comm[dev] : exchange(curr halos)  after ready[d] of the previous step
-//   compute[d]: wait(exchange done) -> exterior slabs(curr -> next) -> record ready
+//   comm[dev] : exchange(curr halos) after ready[d] of the previous step -> exterior slabs(curr -> next)
+//   compute[d]: wait(exterior done) -> record ready
 //   host      : swap curr/next pointers
 // The reference instead host-synchronises every compute stream each iteration (jacobi3d.cu:331-337).
 #include <memory>
@@ -27,6 +27,10 @@ struct StencilModelConfig {
   PlacementStrategy placement = PlacementStrategy::NodeAware;
   std::vector<int> gpus;       // empty = automatic
   bool overlap = true;
+  // when every halo comes from this GPU (periodic self-wrap / co-resident sub-domains) the exchange is a local
+  // HBM copy: overlapping it only adds exterior-slab work that competes for the same bandwidth, so run
+  // exchange -> whole-region stencil instead. Off-GPU transports (xGMI/RCCL) keep the overlap.
+  bool autoOverlap = true;
   bool setBackend = false;
   Backend backend = Backend::Device;
   StencilTune tune;
@@ -51,14 +55,17 @@ public:
   hipStream_t compute_stream(size_t di) const;
   int64_t steps_done() const { return steps_; }
   const Spheres &spheres() const { return sph_; }
+  bool overlapping() const { return overlap_; }
 
 private:
   StencilModelConfig cfg_;
   std::unique_ptr<DistributedDomain> dd_;
   std::vector<Stream> compute_;
+  std::vector<Event> exteriorDone_;
   std::vector<Rect3> interiors_;
   std::vector<std::vector<Rect3>> exteriors_;
   Spheres sph_;
+  bool overlap_ = true;
   int64_t steps_ = 0;
 };
 

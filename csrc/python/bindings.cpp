@@ -500,6 +500,7 @@ PYBIND11_MODULE(_C, m) {
   // ---------------- models ----------------
   py::class_<StencilTune>(m, "StencilTune")
       .def(py::init<>())
+      .def_readwrite("variant", &StencilTune::variant)
       .def_readwrite("ty", &StencilTune::ty)
       .def_readwrite("zchunk", &StencilTune::zchunk)
       .def_readwrite("xcd_remap", &StencilTune::xcdRemap)
@@ -516,6 +517,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("placement", &StencilModelConfig::placement)
       .def_readwrite("gpus", &StencilModelConfig::gpus)
       .def_readwrite("overlap", &StencilModelConfig::overlap)
+      .def_readwrite("auto_overlap", &StencilModelConfig::autoOverlap)
       .def_property(
           "backend", [](const StencilModelConfig &c) { return c.backend; },
           [](StencilModelConfig &c, Backend b) {
@@ -537,6 +539,7 @@ PYBIND11_MODULE(_C, m) {
       .def("cells", &StencilModel::cells)
       .def("local_cells", &StencilModel::local_cells)
       .def("steps_done", &StencilModel::steps_done)
+      .def("overlapping", &StencilModel::overlapping)
       .def("compute_stream", [](StencilModel &mdl, size_t di) { return reinterpret_cast<uintptr_t>(mdl.compute_stream(di)); })
       .def("domain",
            [](std::shared_ptr<StencilModel> mdl) {

@@ -211,6 +211,167 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
   }
 }
 
+// v3: block = NW waves stacked in y, TY rows per wave, one shared 16-B x-chunk column of 64 lanes. The y-halo rows of
+// every wave come from its neighbours through LDS (double-buffered by z parity, one barrier per z step), so HBM
+// reads per output row drop from (TY+2)/TY to (NW*TY+2)/(NW*TY).
+template <typename T, int TY, int NW, int KIND, bool NT, bool REMAP>
+__global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a) {
+  using VT = typename Vec16<T>::type;
+  constexpr int V = Vec16<T>::N;
+  constexpr int SLOTS = 2 * NW + 2; // per wave: top row, bottom row; plus block halo above and below
+  __shared__ VT lds[2][SLOTS][64];
+  const uint32_t nb = uint32_t(a.gx) * a.gy * a.gz;
+  const uint32_t lb = REMAP ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
+  const int bz = int(lb % uint32_t(a.gz));
+  const int by = int((lb / uint32_t(a.gz)) % uint32_t(a.gy));
+  const int bx = int(lb / (uint32_t(a.gz) * a.gy));
+  const int lane = threadIdx.x;
+  const int w = int(threadIdx.y);
+  const int c = bx * 64 + lane;
+  const bool cvalid = c < a.nchunks;
+  const int cl = cvalid ? c : a.nchunks - 1;
+  const int xb = a.x0 + cl * V;
+  const int yblk = a.loy + NW * TY * by;
+  const int ybase = yblk + TY * w;
+  const int zs = a.loz + bz * a.zc;
+  const int ze = min(zs + a.zc, a.hiz);
+  if (yblk >= a.hiy || zs >= ze) return; // block-uniform: every wave of the block leaves together
+
+  const bool edgeL = lane == 0;
+  const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
+  const bool fullX = xb >= a.lox && xb + V <= a.hix;
+  const int slotTop = 2 * w, slotBot = 2 * w + 1;
+  const int slotAbove = w == 0 ? 2 * NW : 2 * (w - 1) + 1;
+  const int slotBelow = w == NW - 1 ? 2 * NW + 1 : 2 * (w + 1);
+
+  auto rowp = [&](int y, int z) -> const T * {
+    y = min(y, a.rawYm1);
+    return a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+  };
+  auto ld = [&](const T *p) -> VT { return *reinterpret_cast<const VT *>(p); };
+
+  VT prev[TY], cur[TY], nxt[TY];
+  T curL[TY], curR[TY], nxtL[TY], nxtR[TY];
+  VT haloN; // block halo row of the next plane (wave 0: above, wave NW-1: below)
+#pragma unroll
+  for (int i = 0; i < TY; ++i) prev[i] = ld(rowp(ybase + i, zs - 1));
+#pragma unroll
+  for (int i = 0; i < TY; ++i) {
+    const T *p = rowp(ybase + i, zs);
+    cur[i] = ld(p);
+    curL[i] = edgeL ? p[-1] : T(0);
+    curR[i] = edgeR ? p[V] : T(0);
+  }
+  if (w == 0) lds[0][2 * NW][lane] = ld(rowp(yblk - 1, zs));
+  if (w == NW - 1) lds[0][2 * NW + 1][lane] = ld(rowp(yblk + NW * TY, zs));
+  lds[0][slotTop][lane] = cur[0];
+  lds[0][slotBot][lane] = cur[TY - 1];
+  __syncthreads();
+
+  const int r1sq = a.r1sq;
+  int buf = 0;
+  for (int z = zs; z < ze; ++z) {
+#pragma unroll
+    for (int i = 0; i < TY; ++i) nxt[i] = ld(rowp(ybase + i, z + 1));
+    if (w == 0) haloN = ld(rowp(yblk - 1, z + 1));
+    if (w == NW - 1) haloN = ld(rowp(yblk + NW * TY, z + 1));
+    if (z + 1 < ze) {
+#pragma unroll
+      for (int i = 0; i < TY; ++i) {
+        const T *p = rowp(ybase + i, z + 1);
+        nxtL[i] = edgeL ? p[-1] : T(0);
+        nxtR[i] = edgeR ? p[V] : T(0);
+      }
+    }
+    const VT above = lds[buf][slotAbove][lane];
+    const VT below = lds[buf][slotBelow][lane];
+
+    const int dzh = z - a.hz, dzc = z - a.cz;
+#pragma unroll
+    for (int i = 0; i < TY; ++i) {
+      const int y = ybase + i;
+      const VT &up = i == 0 ? above : cur[i - 1];
+      const VT &dn = i == TY - 1 ? below : cur[i + 1];
+      const T sl = shfl_up1<T>(vget<T>(cur[i], V - 1));
+      const T sr = shfl_down1<T>(vget<T>(cur[i], 0));
+      const T left = edgeL ? curL[i] : sl;
+      const T right = edgeR ? curR[i] : sr;
+      T out[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const T vpx = e < V - 1 ? vget<T>(cur[i], e + 1) : right;
+        const T vmx = e > 0 ? vget<T>(cur[i], e - 1) : left;
+        const T vpy = vget<T>(dn, e);
+        const T vmy = vget<T>(up, e);
+        const T vpz = vget<T>(nxt[i], e);
+        const T vmz = vget<T>(prev[i], e);
+        T val;
+        if (KIND == 0) {
+          val = T(0) + vpx;
+          val += vmx;
+          val += vpy;
+          val += vmy;
+          val += vpz;
+          val += vmz;
+        } else {
+          val = T(0) + vmx;
+          val += vmy;
+          val += vmz;
+          val += vpx;
+          val += vpy;
+          val += vpz;
+        }
+        out[e] = div6<T>(val);
+      }
+      if (KIND == 0 && r1sq > 0) {
+        const int dyh = y - a.hy, dyc = y - a.cy;
+        const int dyzh = dyh * dyh + dzh * dzh;
+        const int dyzc = dyc * dyc + dzc * dzc;
+        if (dyzh < r1sq || dyzc < r1sq) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const int x = xb + e;
+            const bool hot = (x - a.hx) * (x - a.hx) + dyzh < r1sq;
+            const bool cold = (x - a.cx) * (x - a.cx) + dyzc < r1sq;
+            out[e] = hot ? T(1) : (cold ? T(0) : out[e]);
+          }
+        }
+      }
+      if (cvalid && y < a.hiy) {
+        T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+        if (fullX) {
+          using NV = typename Vec16<T>::native;
+          NV v;
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[e] = out[e];
+          if (NT)
+            __builtin_nontemporal_store(v, reinterpret_cast<NV *>(dp));
+          else
+            *reinterpret_cast<NV *>(dp) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (xb + e >= a.lox && xb + e < a.hix) dp[e] = out[e];
+        }
+      }
+    }
+    // publish plane z+1 boundary rows for the next step
+    buf ^= 1;
+    lds[buf][slotTop][lane] = nxt[0];
+    lds[buf][slotBot][lane] = nxt[TY - 1];
+    if (w == 0) lds[buf][2 * NW][lane] = haloN;
+    if (w == NW - 1) lds[buf][2 * NW + 1][lane] = haloN;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TY; ++i) {
+      prev[i] = cur[i];
+      cur[i] = nxt[i];
+      curL[i] = nxtL[i];
+      curR[i] = nxtR[i];
+    }
+  }
+}
+
 // Several thin regions (the exterior slabs) in one launch, one thread per cell.
 constexpr int kMaxRegions = 8;
 struct RegionTable {
@@ -397,6 +558,30 @@ static void launch_fast(StencilArgs<T> a, const StencilTune &tune, hipStream_t s
   HIP_CHECK(hipGetLastError());
 }
 
+template <typename T, int TY, int NW, int KIND>
+static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t stream) {
+  const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  a.gx = (a.nchunks + 63) / 64;
+  a.gy = (ny + NW * TY - 1) / (NW * TY);
+  int zc = tune.zchunk;
+  if (zc <= 0) {
+    // ~4 waves per SIMD over 256 CUs in one round, z-chunks >= 16 planes (warm-up planes cost 2/zc)
+    const int64_t cols = int64_t(a.gx) * a.gy;
+    const int64_t targetBlocks = 256 * 4 * 4 / NW;
+    const int64_t nzc = std::max<int64_t>(1, (targetBlocks + cols - 1) / cols);
+    zc = int(std::max<int64_t>(16, (nz + nzc - 1) / nzc));
+  }
+  a.zc = zc;
+  a.gz = (nz + zc - 1) / zc;
+  const uint32_t blocks = uint32_t(a.gx) * a.gy * a.gz;
+  const dim3 block(64, NW);
+  if (tune.xcdRemap)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true>), dim3(blocks), block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, false>), dim3(blocks), block, 0, stream, a);
+  HIP_CHECK(hipGetLastError());
+}
+
 template <typename T, int KIND>
 static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
                     const StencilTune &tune) {
@@ -418,10 +603,19 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
   const bool fits = a.x0 + int64_t(a.nchunks) * V < a.px - dom.pad_x(qi);
   dom.set_device();
   if (alignedLayout && fits && std::getenv("STENCIL_GENERIC_KERNEL") == nullptr) {
-    if (tune.ty == 4)
-      launch_fast<T, 4, KIND>(a, tune, stream);
-    else
-      launch_fast<T, 8, KIND>(a, tune, stream);
+    if (tune.variant == 1) {
+      if (tune.ty == 4)
+        launch_fast<T, 4, KIND>(a, tune, stream);
+      else
+        launch_fast<T, 8, KIND>(a, tune, stream);
+    } else {
+      if (tune.ty == 8)
+        launch_lds<T, 8, 4, KIND>(a, tune, stream);
+      else if (tune.ty == 2)
+        launch_lds<T, 2, 8, KIND>(a, tune, stream);
+      else
+        launch_lds<T, 4, 8, KIND>(a, tune, stream);
+    }
   } else {
     const int64_t total = Rect3(Dim3(a.lox, a.loy, a.loz), Dim3(a.hix, a.hiy, a.hiz)).extent().flatten();
     const int blocks = int(std::min<int64_t>((total + 255) / 256, 4096));

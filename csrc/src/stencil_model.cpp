@@ -47,12 +47,19 @@ void StencilModel::init() {
   dd_->realize();
   const Rect3 cReg = dd_->get_compute_region();
   sph_ = cfg_.kind == StencilKind::Jacobi ? Spheres::jacobi(cReg) : Spheres();
+  overlap_ = cfg_.overlap;
+  if (cfg_.overlap && cfg_.autoOverlap &&
+      dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All))
+    overlap_ = false;
   interiors_ = dd_->get_interior();
   exteriors_ = dd_->get_exterior();
   auto &doms = dd_->domains();
   for (size_t di = 0; di < doms.size(); ++di) {
     auto &d = doms[di];
-    if (d.backend() == Backend::Device) compute_.emplace_back(d.gpu(), Priority::DEFAULT);
+    if (d.backend() == Backend::Device) {
+      compute_.emplace_back(d.gpu(), Priority::DEFAULT);
+      exteriorDone_.emplace_back(d.gpu());
+    }
     hipStream_t s = compute_.empty() ? nullptr : compute_.back().get();
     for (int64_t q = 0; q < d.num_data(); ++q) {
       if (cfg_.kind == StencilKind::Jacobi)
@@ -70,16 +77,21 @@ void StencilModel::step() {
   TraceRange tr("StencilModel::step");
   auto &doms = dd_->domains();
   const bool device = !compute_.empty();
-  if (cfg_.overlap) {
+  if (overlap_) {
     for (size_t di = 0; di < doms.size(); ++di)
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
         stencil7_apply(doms[di], q, interiors_[di], cfg_.kind, sph_, device ? compute_[di].get() : nullptr, cfg_.tune);
     dd_->exchange_async();
+    // The exterior slabs only need the halos, not the interior result: run them on the comm stream right behind
+    // the exchange so they overlap the interior kernel too; the compute stream then joins the comm stream.
     for (size_t di = 0; di < doms.size(); ++di) {
-      hipStream_t s = device ? compute_[di].get() : nullptr;
-      dd_->wait_exchange(di, s);
+      hipStream_t s = device ? dd_->comm_stream(di) : nullptr;
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
         stencil7_apply_regions(doms[di], q, exteriors_[di], cfg_.kind, sph_, s, cfg_.tune);
+      if (device) {
+        exteriorDone_[di].record(s);
+        exteriorDone_[di].wait_on(compute_[di]);
+      }
     }
   } else {
     dd_->exchange_async();

@@ -20,7 +20,8 @@ def weak_scaled_size(per_gpu: int, n: int) -> int:
 class StencilModel:
     def __init__(self, size, kind=_C.StencilKind.Jacobi, radius: int = 1, all_directions: bool = False,
                  quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
-                 placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, backend=None,
+                 placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, auto_overlap: bool = True,
+                 backend=None,
                  tune: _C.StencilTune | None = None, group=None):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
@@ -34,6 +35,7 @@ class StencilModel:
         if gpus is not None:
             cfg.gpus = list(gpus)
         cfg.overlap = overlap
+        cfg.auto_overlap = auto_overlap
         if backend is not None:
             cfg.backend = backend
         if tune is not None:
@@ -59,6 +61,9 @@ class StencilModel:
     @property
     def domain(self):
         return self._dd
+
+    def overlapping(self) -> bool:
+        return self._m.overlapping()
 
     def cells(self) -> int:
         return self._m.cells()
