@@ -62,6 +62,10 @@ struct ExchangePlanEntry {
   int64_t bytes;
 };
 
+// bytes of the aggregated message for sending `dirs` from `dom` (reference wire layout: messages sorted by dir,
+// each quantity aligned to its element size; reference packer.cuh:136-160 — pinned by the 264-byte test)
+int64_t packed_message_bytes(const LocalDomain &dom, std::vector<Dim3> dirs);
+
 class DistributedDomain {
 public:
   DistributedDomain(int64_t x, int64_t y, int64_t z, std::shared_ptr<comm::ProcGroup> pg = nullptr);

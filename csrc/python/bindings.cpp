@@ -300,6 +300,7 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::keep_alive<1, 3>());
   m.def("halo_volume", &halo_volume);
+  m.def("packed_message_bytes", &packed_message_bytes);
   m.def("qap_solve", [](const std::vector<std::vector<double>> &w, const std::vector<std::vector<double>> &d) {
     Mat2D<double> W, D;
     for (auto &r : w) W.push_back(r);
@@ -358,6 +359,16 @@ PYBIND11_MODULE(_C, m) {
 
   // ---------------- LocalDomain (owned by DistributedDomain; exposed by reference) ----------------
   py::class_<LocalDomain>(m, "LocalDomain")
+      .def(py::init<const Dim3 &, const Dim3 &, int, Backend>(), py::arg("size"), py::arg("origin"), py::arg("device"),
+           py::arg("backend") = Backend::Device)
+      .def("add_data",
+           [](LocalDomain &d, int64_t es, const std::string &name, DType dt) { return d.add_data(es, name, dt); },
+           py::arg("elem_size"), py::arg("name") = "", py::arg("dtype") = DType::Bytes)
+      .def("set_radius", py::overload_cast<int64_t>(&LocalDomain::set_radius))
+      .def("set_radius", py::overload_cast<const Radius &>(&LocalDomain::set_radius))
+      .def("set_padding", &LocalDomain::set_padding)
+      .def("realize", &LocalDomain::realize)
+      .def("swap", &LocalDomain::swap)
       .def("size", &LocalDomain::size)
       .def("origin", &LocalDomain::origin)
       .def("radius", &LocalDomain::radius)

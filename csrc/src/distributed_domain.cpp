@@ -210,6 +210,13 @@ static int64_t packed_size(const LocalDomain &dom, const std::vector<Message> &m
   return off;
 }
 
+int64_t packed_message_bytes(const LocalDomain &dom, std::vector<Dim3> dirs) {
+  std::sort(dirs.begin(), dirs.end());
+  std::vector<Message> msgs;
+  for (auto &d : dirs) msgs.push_back(Message{d, 0, 0});
+  return packed_size(dom, msgs);
+}
+
 // pack: interior slab on the `dir` side -> dense buffer. `curr`: which physical buffer is "curr" in this variant.
 static void build_pack(const LocalDomain &dom, const std::vector<Message> &msgs, char *buf, bool curr,
                        std::vector<CopySeg> &out) {

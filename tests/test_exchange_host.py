@@ -1,0 +1,121 @@
+"""Halo exchange on the CPU backend (BASELINE config #1 path: no GPU, 1 rank) with the analytic coordinate oracle.
+Covers the reference's test_exchange.cu radius patterns plus its coverage gaps: asymmetric radii on the
+same-device path, edge/corner-only radii, uneven partitions, mixed element sizes, several sub-domains per process."""
+import pytest
+import torch
+
+from stencil2_amd.utils.testing import check_exchange, fill_coords
+
+
+def radius_patterns(st):
+    pats = {}
+    pats["r0"] = st.Radius.constant(0)
+    pats["r1"] = st.Radius.constant(1)
+    pats["r2"] = st.Radius.constant(2)
+    r = st.Radius.constant(0); r.set_dir(1, 0, 0, 2); pats["+x2"] = r
+    r = st.Radius.constant(0); r.set_dir(-1, 0, 0, 1); pats["-x1"] = r
+    r = st.Radius.constant(0); r.set_dir(1, 0, 0, 2); r.set_dir(-1, 0, 0, 1); pats["+x2-x1"] = r
+    r = st.Radius.constant(0); r.set_face(1); pats["faces"] = r
+    pats["fec"] = st.Radius.face_edge_corner(2, 1, 0)
+    pats["corners"] = st.Radius.face_edge_corner(1, 0, 1)
+    r = st.Radius.constant(0); r.set_face(2); r.set_dir(1, 1, 0, 2); pats["faces+1edge"] = r
+    r = st.Radius.constant(1); r.set_dir(0, 0, 1, 3); r.set_dir(0, -1, 0, 2); pats["mixed"] = r
+    return pats
+
+
+def make_dd(st, size, radius, gpus, methods=None, dtype=torch.int64, nq=1, backend=None):
+    dd = st.DistributedDomain(*size, group=st.make_single_group())
+    dd.set_backend(backend or st.Backend.Host)
+    dd.set_radius(radius)
+    dd.set_gpus(gpus)
+    if methods is not None:
+        dd.set_methods(methods)
+    qs = [dd.add_data(f"q{i}", dtype) for i in range(nq)]
+    dd.realize()
+    return dd, qs
+
+
+@pytest.mark.parametrize("name", ["r0", "r1", "r2", "+x2", "-x1", "+x2-x1", "faces", "fec", "corners",
+                                  "faces+1edge", "mixed"])
+@pytest.mark.parametrize("gpus", [[0], [0, 0], [0, 0, 0]])
+def test_exchange_patterns(st, name, gpus):
+    radius = radius_patterns(st)[name]
+    dd, (q,) = make_dd(st, (13, 11, 9), radius, gpus)
+    fill_coords(dd, q)
+    dd.exchange()
+    assert check_exchange(dd, q, radius) == 0
+
+
+@pytest.mark.parametrize("gpus", [[0, 0], [0, 0, 0, 0]])
+def test_exchange_staged_only_same_process(st, gpus):
+    """Staged transport between sub-domains of one process (loopback through the process group)."""
+    radius = st.Radius.constant(1)
+    dd, (q,) = make_dd(st, (12, 10, 8), radius, gpus, methods=st.MethodFlags.Staged)
+    fill_coords(dd, q)
+    dd.exchange()
+    assert check_exchange(dd, q, radius) == 0
+    assert dd.exchange_bytes_for_method(st.MethodFlags.Staged) > 0
+
+
+def test_exchange_mixed_dtypes_multi_quantity(st):
+    radius = st.Radius.constant(2)
+    dd = st.DistributedDomain(10, 9, 8, group=st.make_single_group())
+    dd.set_backend(st.Backend.Host)
+    dd.set_radius(radius)
+    dd.set_gpus([0, 0])
+    qa = dd.add_data("a", torch.int64)
+    qb = dd.add_data("b", torch.int32)
+    qc = dd.add_data("c", torch.float64)
+    dd.realize()
+    for q in (qa, qb, qc):
+        fill_coords(dd, q)
+    dd.exchange()
+    for q in (qa, qb, qc):
+        assert check_exchange(dd, q, radius) == 0
+
+
+def test_exchange_swap_parity(st):
+    """Exchanges act on the current buffer after any number of swaps."""
+    radius = st.Radius.constant(1)
+    dd, (q,) = make_dd(st, (8, 8, 8), radius, [0, 0])
+    for it in range(3):
+        fill_coords(dd, q)
+        dd.exchange()
+        assert check_exchange(dd, q, radius) == 0
+        dd.swap()
+
+
+def test_exchange_interior_untouched_and_bytes(st):
+    radius = st.Radius.constant(1)
+    dd, (q,) = make_dd(st, (64, 64, 64), radius, [0], dtype=torch.float32)
+    dd.fill_from_global(q, lambda z, y, x: (x + 3 * y + 7 * z).float())
+    before = dd.curr_interior(0, q).clone()
+    dd.exchange()
+    assert torch.equal(before, dd.curr_interior(0, q))
+    # BASELINE config #1: 64^3 radius-1, 26 directions: 101408 B per quantity
+    assert dd.exchange_bytes_for_method(st.MethodFlags.All) == 101408
+
+
+def test_interior_exterior_partition(st):
+    """get_interior/get_exterior tile the compute region without overlap (reference stencil.cu:567-666)."""
+    for radius in (st.Radius.constant(1), radius_patterns(st)["+x2-x1"], radius_patterns(st)["mixed"]):
+        dd, (q,) = make_dd(st, (12, 10, 9), radius, [0, 0])
+        ins, exts = dd.get_interior(), dd.get_exterior()
+        for di in range(dd.num_domains()):
+            cr = dd.domain(di).get_compute_region()
+            cover = torch.zeros(cr.extent().z, cr.extent().y, cr.extent().x, dtype=torch.int32)
+            for reg in [ins[di], *exts[di]]:
+                lo, hi = reg.lo - cr.lo, reg.hi - cr.lo
+                if hi.x > lo.x and hi.y > lo.y and hi.z > lo.z:
+                    cover[lo.z:hi.z, lo.y:hi.y, lo.x:hi.x] += 1
+            assert int(cover.min()) == 1 and int(cover.max()) == 1
+
+
+def test_plan_summary_and_methods(st):
+    radius = st.Radius.constant(1)
+    dd, _ = make_dd(st, (16, 8, 8), radius, [0, 0])
+    s = dd.plan_summary()
+    assert "== kernel ==" in s
+    assert all(e.method == st.MethodFlags.Kernel for e in dd.plan())
+    assert len(dd.plan()) == 2 * 26
+    assert st.methods_to_string(st.MethodFlags.All) == "staged/rccl/colo/peer/kernel"

@@ -1,0 +1,140 @@
+"""GPU (MI355X) tests: every transport on the device backend against the coordinate oracle, the HIP stencil kernels
+against the torch fp32/fp64 oracle (bitwise), multi-process HIP-IPC on one GPU (reference
+test_cuda_mpi_colocatedtx.cu runs both ranks on device 0 the same way)."""
+import os
+
+import pytest
+import torch
+
+from conftest import run_ranks
+from stencil2_amd.ops import astaroth_init_reference, astaroth_step_reference, jacobi_step_reference
+from stencil2_amd.utils.testing import check_exchange, fill_coords
+
+pytestmark = pytest.mark.gpu
+WORKER = os.path.join(os.path.dirname(__file__), "mp_worker.py")
+
+
+def _dd(st, size, radius, gpus, methods, dtype=torch.int64):
+    dd = st.DistributedDomain(*size, group=st.make_single_group())
+    dd.set_backend(st.Backend.Device)
+    dd.set_radius(radius)
+    dd.set_gpus(gpus)
+    dd.set_methods(methods)
+    q = dd.add_data("c", dtype)
+    dd.realize()
+    return dd, q
+
+
+def _radii(st):
+    a = st.Radius.constant(0)
+    a.set_dir(1, 0, 0, 2)
+    a.set_dir(-1, 0, 0, 1)
+    b = st.Radius.constant(1)
+    b.set_dir(0, 0, 1, 3)
+    return {"r1": st.Radius.constant(1), "r3": st.Radius.constant(3), "asym": a, "fec": st.Radius.face_edge_corner(2, 1, 1),
+            "mixed": b}
+
+
+@pytest.mark.parametrize("method,gpus", [("Kernel", [0]), ("Kernel", [0, 0]), ("PeerCopy", [0, 0]),
+                                         ("Rccl", [0, 0]), ("Staged", [0, 0]), ("All", [0, 0, 0])])
+@pytest.mark.parametrize("rname", ["r1", "r3", "asym", "fec", "mixed"])
+def test_device_exchange(st, method, gpus, rname):
+    radius = _radii(st)[rname]
+    dd, q = _dd(st, (19, 13, 11), radius, gpus, getattr(st.MethodFlags, method))
+    for it in range(2):
+        fill_coords(dd, q)
+        dd.exchange()
+        assert check_exchange(dd, q, radius) == 0
+        dd.swap()
+
+
+def test_device_exchange_float_views(st):
+    radius = st.Radius.constant(2)
+    dd, q = _dd(st, (64, 32, 16), radius, [0], st.MethodFlags.All, dtype=torch.float32)
+    t = dd.curr(0, q)
+    assert t.device.type == "cuda" and t.dtype == torch.float32
+    fill_coords(dd, q)
+    dd.exchange()
+    assert check_exchange(dd, q, radius) == 0
+
+
+def _gather(model):
+    dd = model.domain
+    L = dd.size()
+    g = None
+    for di in range(dd.num_domains()):
+        d = dd.domain(di)
+        o, s = d.origin(), d.size()
+        t = model.interior(di).cpu()
+        if g is None:
+            g = torch.zeros(L.z, L.y, L.x, dtype=t.dtype)
+        g[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x] = t
+    return g
+
+
+@pytest.mark.parametrize("size", [(32, 32, 32), (67, 45, 33), (130, 64, 40)])
+@pytest.mark.parametrize("gpus", [[0], [0, 0]])
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_jacobi_device_matches_oracle(st, size, gpus, overlap, variant):
+    t = st.StencilTune()
+    t.variant = variant
+    m = st.Jacobi3D(size, gpus=gpus, overlap=overlap, auto_overlap=False, tune=t)
+    m.init()
+    u = _gather(m)
+    for _ in range(3):
+        m.step()
+        u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
+def test_jacobi_fp64_device(st):
+    m = st.Jacobi3D((40, 36, 20), gpus=[0], fp64=True)
+    m.init()
+    u = _gather(m)
+    for _ in range(3):
+        m.step()
+        u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
+def test_astaroth_device_matches_oracle(st):
+    L = (40, 34, 28)
+    m = st.AstarothSim(L, quantities=2, gpus=[0, 0])
+    m.init()
+    u = _gather(m)
+    assert torch.allclose(u, astaroth_init_reference(L, 3, 10.0), atol=1e-6)
+    for _ in range(3):
+        m.step()
+        u = astaroth_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
+@pytest.mark.parametrize("radius", ["r1", "fec", "asym"])
+def test_colocated_ipc_two_ranks_one_gpu(radius):
+    outs = run_ranks(2, WORKER, ["exchange", radius, "20,12,10"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "Colocated", "STENCIL_WAIT_TIMEOUT": "20"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
+def test_colocated_ipc_jacobi_two_ranks():
+    outs = run_ranks(2, WORKER, ["jacobi", "40,24,20"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
+def test_staged_two_ranks_one_gpu():
+    outs = run_ranks(2, WORKER, ["exchange", "r1", "16,12,10"], env_extra={"MP_DEVICE": "1", "MP_METHODS": "Staged"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
+def test_smoke_entry():
+    import __graft_entry__ as g
+
+    g.smoke()

@@ -1,0 +1,31 @@
+"""Multi-rank runs over the native TCP process group on the CPU backend (host-staged transport), including fake
+multi-node layouts via STENCIL_HOSTNAME (the reference never tested multi-node placement)."""
+import os
+
+import pytest
+
+from conftest import run_ranks
+
+WORKER = os.path.join(os.path.dirname(__file__), "mp_worker.py")
+
+
+def _ok(outs):
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
+@pytest.mark.parametrize("n,radius,size", [(2, "r1", "12,10,8"), (2, "asym", "13,9,7"), (3, "fec", "15,9,8"),
+                                           (4, "r2", "16,12,10")])
+def test_staged_exchange_ranks(n, radius, size):
+    _ok(run_ranks(n, WORKER, ["exchange", radius, size]))
+
+
+def test_fake_two_nodes_nodeaware():
+    outs = run_ranks(4, WORKER, ["exchange", "r1", "16,12,10"],
+                     per_rank_env=lambda r: {"STENCIL_HOSTNAME": f"node{r // 2}"})
+    _ok(outs)
+    assert all("nodes 2" in out for _, out in outs)
+
+
+def test_jacobi_ranks_match_oracle():
+    _ok(run_ranks(3, WORKER, ["jacobi", "15,11,9"]))
