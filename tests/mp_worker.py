@@ -65,7 +65,9 @@ def scenario_jacobi(backend, methods, size):
 def main():
     sc = sys.argv[1]
     backend = st.Backend.Device if os.environ.get("MP_DEVICE") == "1" else st.Backend.Host
-    methods = getattr(st.MethodFlags, os.environ.get("MP_METHODS", "All"))
+    methods = st.MethodFlags.None_
+    for name in os.environ.get("MP_METHODS", "All").split("|"):
+        methods = methods | getattr(st.MethodFlags, name)
     if sc == "exchange":
         bad = scenario_exchange(backend, methods, sys.argv[2], tuple(int(v) for v in sys.argv[3].split(",")))
     elif sc == "jacobi":

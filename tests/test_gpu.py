@@ -116,7 +116,7 @@ def test_astaroth_device_matches_oracle(st):
 @pytest.mark.parametrize("radius", ["r1", "fec", "asym"])
 def test_colocated_ipc_two_ranks_one_gpu(radius):
     outs = run_ranks(2, WORKER, ["exchange", radius, "20,12,10"],
-                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "Colocated", "STENCIL_WAIT_TIMEOUT": "20"})
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "Colocated|Kernel", "STENCIL_WAIT_TIMEOUT": "20"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 
@@ -129,7 +129,7 @@ def test_colocated_ipc_jacobi_two_ranks():
 
 
 def test_staged_two_ranks_one_gpu():
-    outs = run_ranks(2, WORKER, ["exchange", "r1", "16,12,10"], env_extra={"MP_DEVICE": "1", "MP_METHODS": "Staged"})
+    outs = run_ranks(2, WORKER, ["exchange", "r1", "16,12,10"], env_extra={"MP_DEVICE": "1", "MP_METHODS": "Staged|Kernel"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 
