@@ -115,7 +115,9 @@ public:
 
   // ---- exchange ----
   void exchange();       // blocking: returns when every halo of every local domain is valid
-  void exchange_async(); // enqueue on the comm streams; only the staged (host) path blocks the caller
+  // enqueue on the comm streams; only the staged (host) path blocks the caller. With a single local device a
+  // caller stream may be given: the exchange is then enqueued on it (no cross-stream events).
+  void exchange_async(hipStream_t stream = nullptr);
   // make the next exchange wait for the work currently enqueued on `s` (which touches domain di)
   void record_ready(size_t di, hipStream_t s);
   // make `s` wait until the halos of domain di from the last exchange are written

@@ -465,7 +465,9 @@ PYBIND11_MODULE(_C, m) {
       .def("plan", &DistributedDomain::plan)
       .def("plan_summary", &DistributedDomain::plan_summary)
       .def("exchange", &DistributedDomain::exchange, py::call_guard<py::gil_scoped_release>())
-      .def("exchange_async", &DistributedDomain::exchange_async, py::call_guard<py::gil_scoped_release>())
+      .def("exchange_async",
+           [](DistributedDomain &d, uintptr_t s) { d.exchange_async(reinterpret_cast<hipStream_t>(s)); },
+           py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
       .def("sync_exchange", &DistributedDomain::sync_exchange, py::call_guard<py::gil_scoped_release>())
       .def("record_ready",
            [](DistributedDomain &d, size_t di, uintptr_t s) { d.record_ready(di, reinterpret_cast<hipStream_t>(s)); })

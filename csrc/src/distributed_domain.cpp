@@ -782,7 +782,7 @@ void DistributedDomain::exchange() {
   if (exchangeStats_) timeExchange_ += pg_->allreduce_max(now_s() - t0);
 }
 
-void DistributedDomain::exchange_async() {
+void DistributedDomain::exchange_async(hipStream_t stream) {
   STENCIL_REQUIRE(realized_, "exchange before realize");
   TraceRange tr("DD::exchange()");
   Impl &I = *impl_;
@@ -806,8 +806,13 @@ void DistributedDomain::exchange_async() {
     return;
   }
 
+  // a caller-provided stream replaces the comm stream (single device): the exchange is then ordered by that
+  // stream alone, with no cross-stream events
+  const bool over = stream != nullptr && I.devs.size() == 1;
+  auto S = [&](DevCtx &c) -> hipStream_t { return over ? stream : c.comm.get(); };
+
   // (0) dependencies: the comm streams start after every local domain's producer work
-  {
+  if (!over) {
     bool anyMissing = false;
     for (size_t di = 0; di < domains_.size(); ++di) anyMissing |= !I.readyPending[di];
     if (anyMissing) {
@@ -819,8 +824,10 @@ void DistributedDomain::exchange_async() {
     for (auto &ctx : I.devs) {
       HIP_CHECK(hipSetDevice(ctx.dev));
       for (size_t di = 0; di < domains_.size(); ++di)
-        if (I.readyPending[di]) I.ready[di].wait_on(ctx.comm);
+        if (I.readyPending[di]) I.ready[di].wait_on(S(ctx));
     }
+    for (size_t di = 0; di < domains_.size(); ++di) I.readyPending[di] = false;
+  } else {
     for (size_t di = 0; di < domains_.size(); ++di) I.readyPending[di] = false;
   }
 
@@ -831,8 +838,8 @@ void DistributedDomain::exchange_async() {
   for (auto &ctx : I.devs) {
     HIP_CHECK(hipSetDevice(ctx.dev));
     TraceRange t("kernel/peer translate");
-    if (!ctx.translate.host[parity].empty()) ctx.translate.run_device(parity, ctx.comm);
-    ctx.translated.record(ctx.comm);
+    if (!ctx.translate.host[parity].empty()) ctx.translate.run_device(parity, S(ctx));
+    ctx.translated.record(S(ctx));
   }
 
   // (2) colocated sends: wait for inbox credit (slot reuse distance 2), pack into the peer's inbox over xGMI,
@@ -844,12 +851,12 @@ void DistributedDomain::exchange_async() {
     if (I.epoch > 2) {
       std::vector<uint64_t *> credits;
       for (int ci : ctx.coloSend) credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownBlock));
-      wait_flags_device(credits, I.epoch - 2, I.errDev, 1, I.waitTimeout, ctx.comm);
+      wait_flags_device(credits, I.epoch - 2, I.errDev, 1, I.waitTimeout, S(ctx));
     }
-    ctx.coloPack.run_device(cv, ctx.comm);
+    ctx.coloPack.run_device(cv, S(ctx));
     std::vector<uint64_t *> arrived;
     for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
-    signal_flags_device(arrived, I.epoch, ctx.comm);
+    signal_flags_device(arrived, I.epoch, S(ctx));
   }
 
   // (3) RCCL: pack, one group of send/recv over every local device, unpack
@@ -858,22 +865,22 @@ void DistributedDomain::exchange_async() {
     for (auto &ctx : I.devs) {
       if (ctx.rcclSend.empty()) continue;
       HIP_CHECK(hipSetDevice(ctx.dev));
-      ctx.rcclPack.run_device(parity, ctx.comm);
+      ctx.rcclPack.run_device(parity, S(ctx));
     }
     NCCL_CHECK(ncclGroupStart());
     for (auto &ctx : I.devs) {
       for (int ci : ctx.rcclSend)
         NCCL_CHECK(ncclSend(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, int(I.chans[ci].tag), ctx.nccl,
-                            ctx.comm));
+                            S(ctx)));
       for (int ci : ctx.rcclRecv)
         NCCL_CHECK(ncclRecv(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, int(I.chans[ci].tag), ctx.nccl,
-                            ctx.comm));
+                            S(ctx)));
     }
     NCCL_CHECK(ncclGroupEnd());
     for (auto &ctx : I.devs) {
       if (ctx.rcclRecv.empty()) continue;
       HIP_CHECK(hipSetDevice(ctx.dev));
-      ctx.rcclUnpack.run_device(parity, ctx.comm);
+      ctx.rcclUnpack.run_device(parity, S(ctx));
     }
   }
 
@@ -886,15 +893,15 @@ void DistributedDomain::exchange_async() {
       for (auto &ctx : I.devs) {
         if (ctx.stagedSend.empty()) continue;
         HIP_CHECK(hipSetDevice(ctx.dev));
-        ctx.stagedPack.run_device(parity, ctx.comm);
+        ctx.stagedPack.run_device(parity, S(ctx));
         for (int ci : ctx.stagedSend)
           HIP_CHECK(hipMemcpyAsync(I.chans[ci].hbuf, I.chans[ci].dbuf, size_t(I.chans[ci].bytes), hipMemcpyDeviceToHost,
-                                   ctx.comm));
+                                   S(ctx)));
       }
       for (auto &ctx : I.devs) {
         if (ctx.stagedSend.empty()) continue;
         HIP_CHECK(hipSetDevice(ctx.dev));
-        HIP_CHECK(hipStreamSynchronize(ctx.comm));
+        HIP_CHECK(hipStreamSynchronize(S(ctx)));
         for (int ci : ctx.stagedSend) pg.send(I.chans[ci].remoteRank, I.chans[ci].tag, I.chans[ci].hbuf, size_t(I.chans[ci].bytes));
       }
       for (auto &ctx : I.devs) {
@@ -903,9 +910,9 @@ void DistributedDomain::exchange_async() {
         for (int ci : ctx.stagedRecv) {
           pg.recv(I.chans[ci].remoteRank, I.chans[ci].tag, I.chans[ci].hbuf, size_t(I.chans[ci].bytes));
           HIP_CHECK(hipMemcpyAsync(I.chans[ci].dbuf, I.chans[ci].hbuf, size_t(I.chans[ci].bytes), hipMemcpyHostToDevice,
-                                   ctx.comm));
+                                   S(ctx)));
         }
-        ctx.stagedUnpack.run_device(parity, ctx.comm);
+        ctx.stagedUnpack.run_device(parity, S(ctx));
       }
     }
   }
@@ -920,16 +927,16 @@ void DistributedDomain::exchange_async() {
       arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownBlock));
       credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
     }
-    wait_flags_device(arrived, I.epoch, I.errDev, 2, I.waitTimeout, ctx.comm);
-    ctx.coloUnpack.run_device(cv, ctx.comm);
-    signal_flags_device(credits, I.epoch, ctx.comm);
+    wait_flags_device(arrived, I.epoch, I.errDev, 2, I.waitTimeout, S(ctx));
+    ctx.coloUnpack.run_device(cv, S(ctx));
+    signal_flags_device(credits, I.epoch, S(ctx));
   }
 
   // (6) halos written by peer devices of this process
   for (auto &ctx : I.devs) {
     HIP_CHECK(hipSetDevice(ctx.dev));
-    for (int src : ctx.peerWriters) I.devs[I.devIndex[src]].translated.wait_on(ctx.comm);
-    ctx.done.record(ctx.comm);
+    for (int src : ctx.peerWriters) I.devs[I.devIndex[src]].translated.wait_on(S(ctx));
+    ctx.done.record(S(ctx));
   }
 }
 

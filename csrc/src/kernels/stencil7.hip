@@ -236,6 +236,12 @@ __global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a)
   const int zs = a.loz + bz * a.zc;
   const int ze = min(zs + a.zc, a.hiz);
   if (yblk >= a.hiy || zs >= ze) return; // block-uniform: every wave of the block leaves together
+  // odd z-chunks march downwards: a chunk boundary is then read by both neighbouring chunks at the same time
+  // (both start there, or both end there), so the warm-up planes are L2/MALL hits instead of HBM re-reads
+  const bool down = (bz & 1) != 0;
+  const int dz = down ? -1 : 1;
+  const int z0 = down ? ze - 1 : zs;
+  const int nzs = ze - zs;
 
   const bool edgeL = lane == 0;
   const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
@@ -254,31 +260,33 @@ __global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a)
   T curL[TY], curR[TY], nxtL[TY], nxtR[TY];
   VT haloN; // block halo row of the next plane (wave 0: above, wave NW-1: below)
 #pragma unroll
-  for (int i = 0; i < TY; ++i) prev[i] = ld(rowp(ybase + i, zs - 1));
+  for (int i = 0; i < TY; ++i) prev[i] = ld(rowp(ybase + i, z0 - dz));
 #pragma unroll
   for (int i = 0; i < TY; ++i) {
-    const T *p = rowp(ybase + i, zs);
+    const T *p = rowp(ybase + i, z0);
     cur[i] = ld(p);
     curL[i] = edgeL ? p[-1] : T(0);
     curR[i] = edgeR ? p[V] : T(0);
   }
-  if (w == 0) lds[0][2 * NW][lane] = ld(rowp(yblk - 1, zs));
-  if (w == NW - 1) lds[0][2 * NW + 1][lane] = ld(rowp(yblk + NW * TY, zs));
+  if (w == 0) lds[0][2 * NW][lane] = ld(rowp(yblk - 1, z0));
+  if (w == NW - 1) lds[0][2 * NW + 1][lane] = ld(rowp(yblk + NW * TY, z0));
   lds[0][slotTop][lane] = cur[0];
   lds[0][slotBot][lane] = cur[TY - 1];
   __syncthreads();
 
   const int r1sq = a.r1sq;
   int buf = 0;
-  for (int z = zs; z < ze; ++z) {
+  int z = z0;
+  for (int step = 0; step < nzs; ++step, z += dz) {
+    const int zn = z + dz;
 #pragma unroll
-    for (int i = 0; i < TY; ++i) nxt[i] = ld(rowp(ybase + i, z + 1));
-    if (w == 0) haloN = ld(rowp(yblk - 1, z + 1));
-    if (w == NW - 1) haloN = ld(rowp(yblk + NW * TY, z + 1));
-    if (z + 1 < ze) {
+    for (int i = 0; i < TY; ++i) nxt[i] = ld(rowp(ybase + i, zn));
+    if (w == 0) haloN = ld(rowp(yblk - 1, zn));
+    if (w == NW - 1) haloN = ld(rowp(yblk + NW * TY, zn));
+    if (step + 1 < nzs) {
 #pragma unroll
       for (int i = 0; i < TY; ++i) {
-        const T *p = rowp(ybase + i, z + 1);
+        const T *p = rowp(ybase + i, zn);
         nxtL[i] = edgeL ? p[-1] : T(0);
         nxtR[i] = edgeR ? p[V] : T(0);
       }
@@ -303,8 +311,8 @@ __global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a)
         const T vmx = e > 0 ? vget<T>(cur[i], e - 1) : left;
         const T vpy = vget<T>(dn, e);
         const T vmy = vget<T>(up, e);
-        const T vpz = vget<T>(nxt[i], e);
-        const T vmz = vget<T>(prev[i], e);
+        const T vpz = down ? vget<T>(prev[i], e) : vget<T>(nxt[i], e);
+        const T vmz = down ? vget<T>(nxt[i], e) : vget<T>(prev[i], e);
         T val;
         if (KIND == 0) {
           val = T(0) + vpx;
@@ -565,9 +573,9 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
   a.gy = (ny + NW * TY - 1) / (NW * TY);
   int zc = tune.zchunk;
   if (zc <= 0) {
-    // ~4 waves per SIMD over 256 CUs in one round, z-chunks >= 16 planes (warm-up planes cost 2/zc)
+    // ~8 waves per SIMD over 256 CUs in one round, z-chunks >= 16 planes (warm-up planes are shared, see kernel)
     const int64_t cols = int64_t(a.gx) * a.gy;
-    const int64_t targetBlocks = 256 * 4 * 4 / NW;
+    const int64_t targetBlocks = 256 * 4 * 8 / NW;
     const int64_t nzc = std::max<int64_t>(1, (targetBlocks + cols - 1) / cols);
     zc = int(std::max<int64_t>(16, (nz + nzc - 1) / nzc));
   }

@@ -94,10 +94,12 @@ void StencilModel::step() {
       }
     }
   } else {
-    dd_->exchange_async();
+    // one device: enqueue the exchange on the compute stream itself (no cross-stream hand-offs)
+    const bool single = device && doms.size() == 1;
+    dd_->exchange_async(single ? compute_[0].get() : nullptr);
     for (size_t di = 0; di < doms.size(); ++di) {
       hipStream_t s = device ? compute_[di].get() : nullptr;
-      dd_->wait_exchange(di, s);
+      if (!single) dd_->wait_exchange(di, s);
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
         stencil7_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, cfg_.tune);
     }
