@@ -37,9 +37,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    device = local_rank % max(1, ndev)
+    torch.cuda.set_device(device)
+    # one rank per GPU: RCCL for the harness barrier/max-reduce. More ranks than GPUs (a rehearsal on a 1-GPU box,
+    # ranks sharing the device through HIP IPC) cannot use RCCL, so the harness collectives go over gloo.
+    shared = world > ndev
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+    red_dev = "cpu" if shared else "cuda"
 
     import stencil2_amd as st
 
@@ -59,7 +68,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    model = st.Jacobi3D((L, L, L), gpus=[local_rank], methods=methods, overlap=not args.no_overlap, group=pg)
+    model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=not args.no_overlap, group=pg)
     model.init()
     for _ in range(args.warmup):
         model.step()
@@ -73,7 +82,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -90,7 +99,7 @@ def main():
         dd.swap()
     torch.cuda.synchronize()
     xel = time.perf_counter() - t1
-    tx = torch.tensor([xel], dtype=torch.float64, device="cuda")
+    tx = torch.tensor([xel], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tx, op=dist.ReduceOp.MAX)
     xel = float(tx.item())

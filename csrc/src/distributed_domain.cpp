@@ -330,6 +330,56 @@ void DistributedDomain::realize() {
   for (auto &d : domains_) d.realize();
   timeRealize_ = pg.allreduce_max(now_s() - t0);
 
+  // ---- HIP-IPC pre-flight: every rank maps a small uncached block of every co-located rank and reads it back.
+  // If any mapping fails anywhere, Colocated is disabled on all ranks (they then agree on RCCL/staged). ----
+  if (dev && any_methods(MethodFlags::Colocated) && pg.size() > 1 && pg.colocated_size() > 1 &&
+      std::getenv("STENCIL_SKIP_IPC_PROBE") == nullptr) {
+    TraceRange trp("ipc probe");
+    int ok = 1;
+    char *blk = nullptr;
+    HIP_CHECK(hipSetDevice(gpus_[0]));
+    if (hipExtMallocWithFlags((void **)&blk, 256, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      ok = 0;
+    }
+    hipIpcMemHandle_t mine{};
+    if (ok && hipIpcGetMemHandle(&mine, blk) != hipSuccess) {
+      (void)hipGetLastError();
+      ok = 0;
+    }
+    if (ok) {
+      const uint64_t tag = 0x57e9c11000000000ull + uint64_t(myRank);
+      HIP_CHECK(hipMemcpy(blk, &tag, sizeof(tag), hipMemcpyHostToDevice));
+    }
+    std::vector<hipIpcMemHandle_t> all(pg.size());
+    pg.allgather(&mine, sizeof(mine), all.data());
+    std::vector<int> oks(pg.size());
+    pg.allgather(&ok, sizeof(int), oks.data());
+    for (int r = 0; r < pg.size() && ok; ++r) {
+      if (r == myRank || !pg.colocated(r) || !oks[r]) continue;
+      char *peer = nullptr;
+      if (hipIpcOpenMemHandle((void **)&peer, all[r], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = 0;
+        break;
+      }
+      uint64_t got = 0;
+      if (hipMemcpy(&got, peer, sizeof(got), hipMemcpyDeviceToHost) != hipSuccess ||
+          got != 0x57e9c11000000000ull + uint64_t(r)) {
+        (void)hipGetLastError();
+        ok = 0;
+      }
+      (void)hipIpcCloseMemHandle(peer);
+    }
+    const bool allOk = pg.allreduce_min_i64(ok) == 1;
+    pg.barrier(); // peers are done with our block
+    if (blk) (void)hipFree(blk);
+    if (!allOk) {
+      if (myRank == 0) LOG_WARN("HIP IPC between co-located ranks is unavailable; Colocated transport disabled");
+      flags_ = MethodFlags(int(flags_) & ~int(MethodFlags::Colocated));
+    }
+  }
+
   // ---- plan messages (reference src/stencil.cu:132-239) ----
   t0 = now_s();
   const Dim3 gdim = placement_->dim();
