@@ -1,0 +1,41 @@
+#pragma once
+// Shared helpers for the C++ apps (method-flag CLI, wall clock, weak-scaling rule).
+#include <chrono>
+#include <cmath>
+#include <string>
+
+#include "stencil/domain/distributed_domain.hpp"
+#include "stencil/rt/argparse.hpp"
+
+namespace app {
+using namespace stencil;
+
+struct MethodArgs {
+  bool staged = false, rccl = false, colo = false, peer = false, kernel = false, trivial = false;
+  void add(ArgParser &p) {
+    p.flag(&staged, "--staged,--remote", "host-staged transport (reference CudaMpi)")
+        .flag(&rccl, "--rccl,--cuda-aware,--cuda-aware-mpi", "RCCL transport (reference CudaAwareMpi)")
+        .flag(&colo, "--colo,--colocated", "HIP-IPC colocated transport")
+        .flag(&peer, "--peer", "same-process peer (xGMI) transport")
+        .flag(&kernel, "--kernel", "same-GPU kernel transport")
+        .flag(&trivial, "--trivial,--naive", "trivial placement");
+  }
+  MethodFlags flags() const {
+    MethodFlags m = MethodFlags::None;
+    if (staged) m |= MethodFlags::Staged;
+    if (rccl) m |= MethodFlags::Rccl;
+    if (colo) m |= MethodFlags::Colocated;
+    if (peer) m |= MethodFlags::PeerCopy;
+    if (kernel) m |= MethodFlags::Kernel;
+    return any(m) ? m : MethodFlags::All;
+  }
+  PlacementStrategy placement() const { return trivial ? PlacementStrategy::Trivial : PlacementStrategy::NodeAware; }
+};
+
+inline double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// reference weak-scaling rule (bin/weak.cu:63-65): size * n^0.33333, rounded
+inline int64_t weak_scale(int64_t v, int n) { return int64_t(double(v) * std::pow(double(n), 0.33333) + 0.5); }
+} // namespace app

@@ -1,0 +1,56 @@
+// Astaroth-like proxy: radius 3 in all 26 directions, several fp32 quantities, 6-neighbour mean.
+// Parity: reference bin/astaroth_sim.cu (flags --remote --cuda-aware-mpi --colocated --peer --kernel --trivial
+// --x --y --z; sin-wave init, halo -10; interior overlapped with the exchange; 5 iterations). The reference keeps
+// one quantity (three commented out); --q defaults to 8 here (BASELINE.json config).
+#include <cstdio>
+
+#include "app_common.hpp"
+#include "stencil/models/stencil_model.hpp"
+#include "stencil/rt/statistics.hpp"
+
+using namespace stencil;
+
+int main(int argc, char **argv) {
+  int64_t x = 512, y = 512, z = 512;
+  int iters = 5, nq = 8;
+  bool noOverlap = false, weak = false;
+  app::MethodArgs ma;
+  ArgParser p("Astaroth proxy (reference bin/astaroth_sim.cu)");
+  p.option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z").option(&iters, "-n,--iters", "iterations")
+      .option(&nq, "--q", "quantities").flag(&noOverlap, "--no-overlap", "no overlap")
+      .flag(&weak, "--weak", "treat x,y,z as per-GPU sizes");
+  ma.add(p);
+  if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
+  auto pg = comm::default_group();
+  if (weak) {
+    x = app::weak_scale(x, pg->size());
+    y = app::weak_scale(y, pg->size());
+    z = app::weak_scale(z, pg->size());
+  }
+  StencilModelConfig cfg;
+  cfg.size = Dim3(x, y, z);
+  cfg.kind = StencilKind::Astaroth;
+  cfg.radius = 3;
+  cfg.allDirections = true;
+  cfg.quantities = nq;
+  cfg.methods = ma.flags();
+  cfg.placement = ma.placement();
+  cfg.overlap = !noOverlap;
+  StencilModel m(cfg, pg);
+  m.init();
+  m.step();
+  m.synchronize();
+  Statistics st;
+  for (int i = 0; i < iters; ++i) {
+    pg->barrier();
+    const double t0 = app::now();
+    m.step();
+    m.synchronize();
+    st.insert(pg->allreduce_max(app::now() - t0));
+  }
+  if (pg->rank() == 0)
+    std::printf("astaroth,%s,%d,%ld,%ld,%ld,%d,%e,%e,%.3f,%e\n", to_string(cfg.methods).c_str(), pg->size(), long(x),
+                long(y), long(z), nq, st.min(), st.trimean(), double(x * y * z) / st.trimean() / 1e9,
+                double(m.domain().exchange_bytes_for_method(MethodFlags::All)));
+  return 0;
+}

@@ -24,6 +24,7 @@
 
 #include "stencil/comm/proc_group.hpp"
 #include "stencil/domain/local_domain.hpp"
+#include "stencil/domain/packer.hpp"
 #include "stencil/rt/stream.hpp"
 #include "stencil/topo/placement.hpp"
 
@@ -45,13 +46,6 @@ inline bool operator&&(MethodFlags a, MethodFlags b) { return (int(a) & int(b)) 
 inline bool any(MethodFlags a) { return a != MethodFlags::None; }
 std::string to_string(MethodFlags m);
 
-// one halo message: sent along `dir` from sub-domain srcId (on the sending rank) to dstId (on the receiving rank)
-struct Message {
-  Dim3 dir;
-  int srcId, dstId;
-  bool operator<(const Message &o) const { return dir < o.dir; }
-  bool operator==(const Message &o) const { return dir == o.dir && srcId == o.srcId && dstId == o.dstId; }
-};
 
 struct ExchangePlanEntry {
   MethodFlags method;

@@ -46,7 +46,10 @@ inline std::vector<size_t> solve_catch(const Mat2D<double> &w, const Mat2D<doubl
   std::iota(best.begin(), best.end(), 0);
   double bestCost = detail::cost(w, d, best);
   bool improved = true;
-  while (improved) {
+  // incremental costs carry rounding error: demand a strict relative improvement and re-anchor on the exact cost,
+  // so two assignments whose costs differ only by rounding cannot swap back and forth forever
+  size_t rounds = 0;
+  while (improved && rounds++ < 100 * n * n + 100) {
     improved = false;
     std::vector<size_t> imprF = best;
     double imprCost = bestCost;
@@ -57,7 +60,7 @@ inline std::vector<size_t> solve_catch(const Mat2D<double> &w, const Mat2D<doubl
         detail::pair_terms(c, -1.0, w, d, f, i, j);
         std::swap(f[i], f[j]);
         detail::pair_terms(c, 1.0, w, d, f, i, j);
-        if (c < imprCost) {
+        if (c < imprCost - 1e-12 * std::fabs(imprCost)) {
           imprF = f;
           imprCost = c;
           improved = true;
@@ -66,7 +69,7 @@ inline std::vector<size_t> solve_catch(const Mat2D<double> &w, const Mat2D<doubl
     }
     if (improved) {
       best = imprF;
-      bestCost = imprCost;
+      bestCost = detail::cost(w, d, best);
     }
   }
   if (costp) *costp = bestCost;

@@ -192,68 +192,17 @@ int64_t DistributedDomain::add_data(int64_t elemSize, const std::string &name, D
 // segment builders (reference wire layout: messages sorted by dir, each quantity aligned to its element size,
 // reference packer.cuh:136-160)
 // ------------------------------------------------------------------------------------------------
-static StridedBox dense_box(char *base, const Dim3 &ext, int64_t es) {
-  StridedBox b;
-  b.base = base;
-  b.ystride = ext.x * es;
-  b.zstride = ext.x * ext.y * es;
-  return b;
-}
-
-static int64_t packed_size(const LocalDomain &dom, const std::vector<Message> &msgs) {
-  int64_t off = 0;
-  for (const auto &m : msgs)
-    for (int64_t q = 0; q < dom.num_data(); ++q) {
-      off = round_up(off, dom.elem_size(q));
-      off += dom.halo_bytes(-m.dir, q);
-    }
-  return off;
-}
-
-int64_t packed_message_bytes(const LocalDomain &dom, std::vector<Dim3> dirs) {
-  std::sort(dirs.begin(), dirs.end());
-  std::vector<Message> msgs;
-  for (auto &d : dirs) msgs.push_back(Message{d, 0, 0});
-  return packed_size(dom, msgs);
-}
-
-// pack: interior slab on the `dir` side -> dense buffer. `curr`: which physical buffer is "curr" in this variant.
 static void build_pack(const LocalDomain &dom, const std::vector<Message> &msgs, char *buf, bool curr,
                        std::vector<CopySeg> &out) {
-  int64_t off = 0;
-  for (const auto &m : msgs)
-    for (int64_t q = 0; q < dom.num_data(); ++q) {
-      const int64_t es = dom.elem_size(q);
-      off = round_up(off, es);
-      const Dim3 ext = dom.halo_extent(-m.dir);
-      out.push_back(make_copy_seg(dom.box(q, curr, dom.halo_pos(m.dir, false)), dense_box(buf + off, ext, es), ext, es));
-      off += es * ext.flatten();
-    }
+  build_pack_segs(dom, msgs, buf, curr, out);
 }
-
-// unpack: dense buffer -> the -dir halo (message sent along dir lands on our -dir side)
 static void build_unpack(const LocalDomain &dom, const std::vector<Message> &msgs, char *buf, bool curr,
                          std::vector<CopySeg> &out) {
-  int64_t off = 0;
-  for (const auto &m : msgs)
-    for (int64_t q = 0; q < dom.num_data(); ++q) {
-      const int64_t es = dom.elem_size(q);
-      off = round_up(off, es);
-      const Dim3 ext = dom.halo_extent(-m.dir);
-      out.push_back(make_copy_seg(dense_box(buf + off, ext, es), dom.box(q, curr, dom.halo_pos(-m.dir, true)), ext, es));
-      off += es * ext.flatten();
-    }
+  build_unpack_segs(dom, msgs, buf, curr, out);
 }
-
-// direct translate src interior slab -> dst halo (same process)
 static void build_translate(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
                             std::vector<CopySeg> &out) {
-  for (int64_t q = 0; q < src.num_data(); ++q) {
-    const int64_t es = src.elem_size(q);
-    const Dim3 ext = src.halo_extent(-dir);
-    out.push_back(make_copy_seg(src.box(q, curr, src.halo_pos(dir, false)), dst.box(q, curr, dst.halo_pos(-dir, true)),
-                                ext, es));
-  }
+  build_translate_segs(src, dst, dir, curr, out);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,0 +1,124 @@
+// Message packing (see stencil/domain/packer.hpp).
+#include "stencil/domain/packer.hpp"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+
+#include "stencil/rt/hip_check.hpp"
+
+namespace stencil {
+
+static StridedBox dense_box(char *base, const Dim3 &ext, int64_t es) {
+  StridedBox b;
+  b.base = base;
+  b.ystride = ext.x * es;
+  b.zstride = ext.x * ext.y * es;
+  return b;
+}
+
+int64_t packed_size(const LocalDomain &dom, const std::vector<Message> &msgs) {
+  int64_t off = 0;
+  for (const auto &m : msgs)
+    for (int64_t q = 0; q < dom.num_data(); ++q) {
+      off = round_up(off, dom.elem_size(q));
+      off += dom.halo_bytes(-m.dir, q);
+    }
+  return off;
+}
+
+int64_t packed_message_bytes(const LocalDomain &dom, std::vector<Dim3> dirs) {
+  std::sort(dirs.begin(), dirs.end());
+  std::vector<Message> msgs;
+  for (auto &d : dirs) msgs.push_back(Message{d, 0, 0});
+  return packed_size(dom, msgs);
+}
+
+// pack: interior slab on the `dir` side -> dense buffer. `curr`: which physical buffer is "curr" in this variant.
+void build_pack_segs(const LocalDomain &dom, const std::vector<Message> &msgs, char *buf, bool curr,
+                       std::vector<CopySeg> &out) {
+  int64_t off = 0;
+  for (const auto &m : msgs)
+    for (int64_t q = 0; q < dom.num_data(); ++q) {
+      const int64_t es = dom.elem_size(q);
+      off = round_up(off, es);
+      const Dim3 ext = dom.halo_extent(-m.dir);
+      out.push_back(make_copy_seg(dom.box(q, curr, dom.halo_pos(m.dir, false)), dense_box(buf + off, ext, es), ext, es));
+      off += es * ext.flatten();
+    }
+}
+
+// unpack: dense buffer -> the -dir halo (message sent along dir lands on our -dir side)
+void build_unpack_segs(const LocalDomain &dom, const std::vector<Message> &msgs, char *buf, bool curr,
+                         std::vector<CopySeg> &out) {
+  int64_t off = 0;
+  for (const auto &m : msgs)
+    for (int64_t q = 0; q < dom.num_data(); ++q) {
+      const int64_t es = dom.elem_size(q);
+      off = round_up(off, es);
+      const Dim3 ext = dom.halo_extent(-m.dir);
+      out.push_back(make_copy_seg(dense_box(buf + off, ext, es), dom.box(q, curr, dom.halo_pos(-m.dir, true)), ext, es));
+      off += es * ext.flatten();
+    }
+}
+
+// direct translate src interior slab -> dst halo (same process)
+void build_translate_segs(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
+                            std::vector<CopySeg> &out) {
+  for (int64_t q = 0; q < src.num_data(); ++q) {
+    const int64_t es = src.elem_size(q);
+    const Dim3 ext = src.halo_extent(-dir);
+    out.push_back(make_copy_seg(src.box(q, curr, src.halo_pos(dir, false)), dst.box(q, curr, dst.halo_pos(-dir, true)),
+                                ext, es));
+  }
+}
+
+
+PackerBase::~PackerBase() {
+  for (auto &p : plan_) free_copy_plan(p);
+  if (buf_) {
+    if (device_)
+      (void)hipFree(buf_);
+    else
+      std::free(buf_);
+  }
+}
+
+void PackerBase::prepare_impl(LocalDomain *dom, std::vector<Message> msgs, bool pack) {
+  STENCIL_REQUIRE(dom && dom->realized(), "Packer::prepare needs a realized LocalDomain");
+  dom_ = dom;
+  std::sort(msgs.begin(), msgs.end());
+  msgs_ = msgs;
+  size_ = packed_size(*dom, msgs_);
+  STENCIL_REQUIRE(size_ > 0, "zero-size packer was prepared");
+  device_ = dom->backend() == Backend::Device;
+  if (device_) {
+    dom->set_device();
+    HIP_CHECK(hipMalloc(&buf_, size_t(size_)));
+  } else {
+    buf_ = static_cast<char *>(std::aligned_alloc(256, size_t(round_up(size_, 256))));
+  }
+  // variant p: "curr" is the buffer that is current after p swaps from the domain's present parity
+  for (int p = 0; p < 2; ++p) {
+    const bool currIsCurr = (p == dom->parity());
+    segs_[p].clear();
+    if (pack)
+      build_pack_segs(*dom, msgs_, buf_, currIsCurr, segs_[p]);
+    else
+      build_unpack_segs(*dom, msgs_, buf_, currIsCurr, segs_[p]);
+    finalize_segs(segs_[p]);
+    if (device_) plan_[p] = make_copy_plan(segs_[p], dom->gpu());
+  }
+}
+
+void PackerBase::run() {
+  const int p = dom_->parity();
+  if (device_) {
+    dom_->set_device();
+    copy_plan_device(plan_[p], stream_);
+  } else {
+    copy_segs_host(segs_[p]);
+  }
+}
+
+} // namespace stencil
