@@ -31,6 +31,9 @@ struct StencilModelConfig {
   // HBM copy: overlapping it only adds exterior-slab work that competes for the same bandwidth, so run
   // exchange -> whole-region stencil instead. Off-GPU transports (xGMI/RCCL) keep the overlap.
   bool autoOverlap = true;
+  // single stream + kernel-only exchange: capture the step (exchange + stencil) once per buffer parity into a
+  // hipGraph and replay it (removes per-kernel launch gaps)
+  bool useGraph = true;
   bool setBackend = false;
   Backend backend = Backend::Device;
   StencilTune tune;
@@ -66,6 +69,9 @@ private:
   std::vector<std::vector<Rect3>> exteriors_;
   Spheres sph_;
   bool overlap_ = true;
+  bool graphs_ = false;
+  hipGraphExec_t graphExec_[2] = {nullptr, nullptr};
+  void enqueue_step();
   int64_t steps_ = 0;
 };
 

@@ -99,15 +99,18 @@ class NodePartition : public GridPartition {
     const int64_t xIface = size_.y * size_.z * (radius.dir(1, 0, 0) + radius.dir(-1, 0, 0));
     const int64_t yIface = size_.x * size_.z * (radius.dir(0, 1, 0) + radius.dir(0, -1, 0));
     const int64_t zIface = size_.x * size_.y * (radius.dir(0, 0, 1) + radius.dir(0, 0, -1));
-    if (xIface <= yIface && xIface <= zIface) {
-      size_.x = div_ceil(size_.x, amt);
-      d.x *= amt;
-    } else if (yIface <= zIface) {
+    // minimum radius-weighted interface; ties go to z, then y, then x (the reference prefers x,
+    // partition.hpp:224-237). On MI355X a z-face is one contiguous plane (full-rate 16-B copies) while an x-face is a
+    // strided column touching one 128-B line per 4-B element, so remote faces are cheapest along z.
+    if (zIface <= yIface && zIface <= xIface) {
+      size_.z = div_ceil(size_.z, amt);
+      d.z *= amt;
+    } else if (yIface <= xIface) {
       size_.y = div_ceil(size_.y, amt);
       d.y *= amt;
     } else {
-      size_.z = div_ceil(size_.z, amt);
-      d.z *= amt;
+      size_.x = div_ceil(size_.x, amt);
+      d.x *= amt;
     }
   }
 

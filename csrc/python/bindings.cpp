@@ -531,6 +531,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("gpus", &StencilModelConfig::gpus)
       .def_readwrite("overlap", &StencilModelConfig::overlap)
       .def_readwrite("auto_overlap", &StencilModelConfig::autoOverlap)
+      .def_readwrite("use_graph", &StencilModelConfig::useGraph)
       .def_property(
           "backend", [](const StencilModelConfig &c) { return c.backend; },
           [](StencilModelConfig &c, Backend b) {

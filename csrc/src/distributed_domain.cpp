@@ -838,7 +838,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
     HIP_CHECK(hipSetDevice(ctx.dev));
     TraceRange t("kernel/peer translate");
     if (!ctx.translate.host[parity].empty()) ctx.translate.run_device(parity, S(ctx));
-    ctx.translated.record(S(ctx));
+    if (!over) ctx.translated.record(S(ctx)); // events only matter across streams
   }
 
   // (2) colocated sends: wait for inbox credit (slot reuse distance 2), pack into the peer's inbox over xGMI,
@@ -935,7 +935,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
   for (auto &ctx : I.devs) {
     HIP_CHECK(hipSetDevice(ctx.dev));
     for (int src : ctx.peerWriters) I.devs[I.devIndex[src]].translated.wait_on(S(ctx));
-    ctx.done.record(S(ctx));
+    if (!over) ctx.done.record(S(ctx));
   }
 }
 

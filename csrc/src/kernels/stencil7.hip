@@ -464,6 +464,117 @@ __global__ __launch_bounds__(256) void stencil7_generic_kernel(StencilArgs<T> a)
   }
 }
 
+// Exterior shell: thin slabs after the exchange. Wave-granular work table:
+//   ROW slabs (x-extent >= 8, i.e. y/z faces): one wave = 64 x-chunks of one (y, z) row; 5 coalesced 16-B row loads
+//     (centre, y+-1, z+-1) + 2 edge scalars per lane.
+//   COL slabs (thin in x, i.e. x faces): one wave = 64 consecutive y of one (x, z); lanes along y, so y-neighbours
+//     come from adjacent lanes and each lane touches its own row line once (x+-1 share it).
+constexpr int kMaxShell = 8;
+struct ShellTable {
+  int lo[kMaxShell][3];
+  int ext[kMaxShell][3];
+  int x0[kMaxShell];      // ROW: raw x of chunk 0
+  int nch[kMaxShell];     // ROW: chunks per row
+  int col[kMaxShell];     // 1 = COL slab
+  int64_t wbegin[kMaxShell + 1];
+  int n;
+};
+
+template <typename T, int KIND>
+__device__ __forceinline__ T finish_cell(const StencilArgs<T> &a, T px, T mx, T py, T my, T pz, T mz, int x, int y,
+                                         int z) {
+  T val;
+  if (KIND == 0) {
+    val = T(0) + px;
+    val += mx;
+    val += py;
+    val += my;
+    val += pz;
+    val += mz;
+  } else {
+    val = T(0) + mx;
+    val += my;
+    val += mz;
+    val += px;
+    val += py;
+    val += pz;
+  }
+  val = div6<T>(val);
+  if (KIND == 0 && a.r1sq > 0) {
+    const int dh = (x - a.hx) * (x - a.hx) + (y - a.hy) * (y - a.hy) + (z - a.hz) * (z - a.hz);
+    const int dc = (x - a.cx) * (x - a.cx) + (y - a.cy) * (y - a.cy) + (z - a.cz) * (z - a.cz);
+    val = dh < a.r1sq ? T(1) : (dc < a.r1sq ? T(0) : val);
+  }
+  return val;
+}
+
+template <typename T, int KIND>
+__global__ __launch_bounds__(256) void stencil7_shell_kernel(StencilArgs<T> a, ShellTable st) {
+  using VT = typename Vec16<T>::type;
+  constexpr int V = Vec16<T>::N;
+  const int64_t wave = int64_t(blockIdx.x) * 4 + threadIdx.y;
+  if (wave >= st.wbegin[st.n]) return; // wave-uniform
+  int k = 0;
+  while (k + 1 < st.n && st.wbegin[k + 1] <= wave) ++k;
+  const int64_t wl = wave - st.wbegin[k];
+  const int lane = threadIdx.x;
+  const int lx = st.lo[k][0], ly = st.lo[k][1], lz = st.lo[k][2];
+  const int ex = st.ext[k][0], ey = st.ext[k][1];
+  if (!st.col[k]) {
+    // ROW: wl -> (chunk wave cw, y, z)
+    const int cws = (st.nch[k] + 63) / 64;
+    const int cw = int(wl % cws);
+    const int64_t r = wl / cws;
+    const int y = ly + int(r % ey);
+    const int z = lz + int(r / ey);
+    const int c = cw * 64 + lane;
+    const bool valid = c < st.nch[k];
+    const int xb = st.x0[k] + (valid ? c : st.nch[k] - 1) * V;
+    const T *p = a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+    const VT cc = *reinterpret_cast<const VT *>(p);
+    const VT yp = *reinterpret_cast<const VT *>(p + a.px);
+    const VT ym = *reinterpret_cast<const VT *>(p - a.px);
+    const VT zp = *reinterpret_cast<const VT *>(p + a.pxy);
+    const VT zm = *reinterpret_cast<const VT *>(p - a.pxy);
+    const bool eL = lane == 0, eR = lane == 63 || c + 1 >= st.nch[k];
+    const T le = eL ? p[-1] : T(0);
+    const T re = eR ? p[V] : T(0);
+    const T sl = shfl_up1<T>(vget<T>(cc, V - 1));
+    const T sr = shfl_down1<T>(vget<T>(cc, 0));
+    const T left = eL ? le : sl, right = eR ? re : sr;
+    if (!valid) return;
+    T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int x = xb + e;
+      if (x < lx || x >= lx + ex) continue;
+      const T vpx = e < V - 1 ? vget<T>(cc, e + 1) : right;
+      const T vmx = e > 0 ? vget<T>(cc, e - 1) : left;
+      dp[e] = finish_cell<T, KIND>(a, vpx, vmx, vget<T>(yp, e), vget<T>(ym, e), vget<T>(zp, e), vget<T>(zm, e), x, y, z);
+    }
+  } else {
+    // COL: wl -> (x, y block, z); lanes along y
+    const int ybs = (ey + 63) / 64;
+    const int x = lx + int(wl % ex);
+    const int64_t r = wl / ex;
+    const int yb = int(r % ybs);
+    const int z = lz + int(r / ybs);
+    const int y = ly + yb * 64 + lane;
+    const bool valid = y < ly + ey;
+    const int yl = valid ? y : ly + ey - 1;
+    const T *p = a.src + int64_t(z) * a.pxy + int64_t(yl) * a.px + x;
+    const T c0 = p[0], vpx = p[1], vmx = p[-1], vpz = p[a.pxy], vmz = p[-a.pxy];
+    const bool eL = lane == 0, eR = lane == 63 || !(y + 1 < ly + ey);
+    const T ue = eL ? p[-a.px] : T(0);
+    const T de = eR ? p[a.px] : T(0);
+    const T su = shfl_up1<T>(c0);   // value of y-1
+    const T sd = shfl_down1<T>(c0); // value of y+1
+    const T vmy = eL ? ue : su, vpy = eR ? de : sd;
+    if (!valid) return;
+    a.dst[int64_t(z) * a.pxy + int64_t(y) * a.px + x] = finish_cell<T, KIND>(a, vpx, vmx, vpy, vmy, vpz, vmz, x, y, z);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------------------
@@ -662,15 +773,54 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
 template <typename T, int KIND>
 static void apply_regions_t(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, const Spheres &sph,
                             hipStream_t stream) {
+  constexpr int V = Vec16<T>::N;
   StencilArgs<T> a = make_args<T>(dom, qi, dom.get_compute_region(), KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth,
                                   sph);
   const Dim3 org = dom.accessor_origin();
-  for (size_t k0 = 0; k0 < regions.size(); k0 += kMaxRegions) {
+  const int rxm = int(dom.radius().x(-1));
+  const bool aligned = (reinterpret_cast<uintptr_t>(a.src + rxm) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(a.dst + rxm) % 16 == 0) && ((a.px * int64_t(sizeof(T))) % 16 == 0);
+  std::vector<Rect3> rs;
+  for (const auto &r : regions)
+    if (!r.empty()) rs.push_back(Rect3(r.lo - org, r.hi - org));
+  if (aligned && std::getenv("STENCIL_GENERIC_EXTERIOR") == nullptr) {
+    for (size_t k0 = 0; k0 < rs.size(); k0 += kMaxShell) {
+      ShellTable st{};
+      for (size_t k = k0; k < rs.size() && st.n < kMaxShell; ++k) {
+        const Rect3 &r = rs[k];
+        const Dim3 e = r.extent();
+        const int i = st.n;
+        st.lo[i][0] = int(r.lo.x);
+        st.lo[i][1] = int(r.lo.y);
+        st.lo[i][2] = int(r.lo.z);
+        st.ext[i][0] = int(e.x);
+        st.ext[i][1] = int(e.y);
+        st.ext[i][2] = int(e.z);
+        int64_t waves;
+        if (e.x >= 8) {
+          const int off = ((int(r.lo.x) - rxm) % V + V) % V;
+          st.x0[i] = int(r.lo.x) - off;
+          st.nch[i] = (int(r.hi.x) - st.x0[i] + V - 1) / V;
+          st.col[i] = 0;
+          waves = int64_t((st.nch[i] + 63) / 64) * e.y * e.z;
+        } else {
+          st.col[i] = 1;
+          waves = int64_t(e.x) * ((e.y + 63) / 64) * e.z;
+        }
+        st.wbegin[i + 1] = st.wbegin[i] + waves;
+        ++st.n;
+      }
+      const int64_t blocks = (st.wbegin[st.n] + 3) / 4;
+      hipLaunchKernelGGL((stencil7_shell_kernel<T, KIND>), dim3(uint32_t(blocks)), dim3(64, 4), 0, stream, a, st);
+      HIP_CHECK(hipGetLastError());
+    }
+    return;
+  }
+  for (size_t k0 = 0; k0 < rs.size(); k0 += kMaxRegions) {
     RegionTable rt{};
     rt.begin[0] = 0;
-    for (size_t k = k0; k < regions.size() && rt.n < kMaxRegions; ++k) {
-      if (regions[k].empty()) continue;
-      const Rect3 r(regions[k].lo - org, regions[k].hi - org);
+    for (size_t k = k0; k < rs.size() && rt.n < kMaxRegions; ++k) {
+      const Rect3 &r = rs[k];
       const Dim3 e = r.extent();
       rt.lo[rt.n][0] = int(r.lo.x);
       rt.lo[rt.n][1] = int(r.lo.y);

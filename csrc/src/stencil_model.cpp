@@ -1,5 +1,7 @@
 #include "stencil/models/stencil_model.hpp"
 
+#include <cstdlib>
+
 #include "stencil/rt/hip_check.hpp"
 #include "stencil/rt/trace.hpp"
 
@@ -32,6 +34,8 @@ StencilModel::~StencilModel() {
     for (auto &s : compute_) s.sync();
   } catch (...) {
   }
+  for (auto &g : graphExec_)
+    if (g) (void)hipGraphExecDestroy(g);
 }
 
 int64_t StencilModel::local_cells() const {
@@ -51,6 +55,10 @@ void StencilModel::init() {
   if (cfg_.overlap && cfg_.autoOverlap &&
       dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All))
     overlap_ = false;
+  graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
+            dd_->domains()[0].backend() == Backend::Device &&
+            dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
+            dd_->world_size() == 1 && std::getenv("STENCIL_NO_GRAPH") == nullptr;
   interiors_ = dd_->get_interior();
   exteriors_ = dd_->get_exterior();
   auto &doms = dd_->domains();
@@ -76,14 +84,43 @@ void StencilModel::init() {
 void StencilModel::step() {
   TraceRange tr("StencilModel::step");
   auto &doms = dd_->domains();
+  if (graphs_) {
+    const int p = doms[0].parity();
+    hipStream_t s = compute_[0].get();
+    if (!graphExec_[p]) {
+      hipGraph_t g = nullptr;
+      HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      enqueue_step();
+      HIP_CHECK(hipStreamEndCapture(s, &g));
+      HIP_CHECK(hipGraphInstantiate(&graphExec_[p], g, nullptr, nullptr, 0));
+      HIP_CHECK(hipGraphDestroy(g));
+    }
+    HIP_CHECK(hipGraphLaunch(graphExec_[p], s));
+    dd_->swap();
+    ++steps_;
+    return;
+  }
+  enqueue_step();
+  dd_->swap();
+  // the next exchange must follow this step's compute; in single-stream mode stream order already guarantees it
+  const bool device = !compute_.empty();
+  const bool singleStream = device && !overlap_ && doms.size() == 1;
+  if (device && !singleStream)
+    for (size_t di = 0; di < doms.size(); ++di) dd_->record_ready(di, compute_[di]);
+  ++steps_;
+}
+
+void StencilModel::enqueue_step() {
+  auto &doms = dd_->domains();
   const bool device = !compute_.empty();
   if (overlap_) {
+    // exchange first: its pack/send kernels (high-priority comm stream) get CUs before the interior sweep fills them
+    dd_->exchange_async();
     for (size_t di = 0; di < doms.size(); ++di)
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
         stencil7_apply(doms[di], q, interiors_[di], cfg_.kind, sph_, device ? compute_[di].get() : nullptr, cfg_.tune);
-    dd_->exchange_async();
     // The exterior slabs only need the halos, not the interior result: run them on the comm stream right behind
-    // the exchange so they overlap the interior kernel too; the compute stream then joins the comm stream.
+    // the exchange; the compute stream then joins the comm stream.
     for (size_t di = 0; di < doms.size(); ++di) {
       hipStream_t s = device ? dd_->comm_stream(di) : nullptr;
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
@@ -104,10 +141,6 @@ void StencilModel::step() {
         stencil7_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, cfg_.tune);
     }
   }
-  dd_->swap();
-  if (device)
-    for (size_t di = 0; di < doms.size(); ++di) dd_->record_ready(di, compute_[di]);
-  ++steps_;
 }
 
 void StencilModel::synchronize() {

@@ -10,7 +10,7 @@ overlap = (sys.argv[3] != "0") if len(sys.argv) > 3 else True
 t = st.StencilTune()
 if len(sys.argv) > 4:
     t.variant, t.ty, t.zchunk = (int(v) for v in sys.argv[4].split(","))
-m = st.Jacobi3D((L, L, L), gpus=[0], overlap=overlap, tune=t)
+m = st.Jacobi3D((L, L, L), gpus=[0], overlap=overlap, auto_overlap=False, tune=t)
 m.init()
 m.run(n)
 m.synchronize()

@@ -43,8 +43,7 @@ def timeit(t, L, steps, overlap=True):
 
 def main():
     L = int(sys.argv[1]) if len(sys.argv) > 1 else 512
-    variants = [(0, 4, 0), (0, 4, 16), (0, 4, 32), (0, 4, 64), (0, 2, 0), (0, 2, 32), (0, 8, 0), (0, 8, 32),
-                (1, 4, 16)]
+    variants = [(0, 4, 0), (0, 4, 24), (0, 2, 0), (0, 8, 0), (1, 4, 16)]
     ok = True
     for v in variants:
         for size in [(67, 45, 33), (64, 64, 64)]:

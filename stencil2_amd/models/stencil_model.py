@@ -21,7 +21,7 @@ class StencilModel:
     def __init__(self, size, kind=_C.StencilKind.Jacobi, radius: int = 1, all_directions: bool = False,
                  quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
                  placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, auto_overlap: bool = True,
-                 backend=None,
+                 use_graph: bool = True, backend=None,
                  tune: _C.StencilTune | None = None, group=None):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
@@ -36,6 +36,7 @@ class StencilModel:
             cfg.gpus = list(gpus)
         cfg.overlap = overlap
         cfg.auto_overlap = auto_overlap
+        cfg.use_graph = use_graph
         if backend is not None:
             cfg.backend = backend
         if tune is not None:

@@ -32,10 +32,12 @@ def test_node_partition_min_interface(st):
     p = st.NodePartition(D(1024, 1024, 1024), r, 1, 8)
     assert p.dim() == D(2, 2, 2)
     assert p.subdomain_size(D(1, 1, 1)) == D(512, 512, 512)
-    # weak-scaling sizes of the reference: 645 split in x -> 323 + 322
+    # weak-scaling sizes of the reference: 645 -> 323 + 322; ties cut z first (contiguous faces)
     p = st.NodePartition(D(645, 645, 645), r, 1, 2)
-    assert p.dim() == D(2, 1, 1)
-    assert p.subdomain_size(D(0, 0, 0)) == D(323, 645, 645) and p.subdomain_size(D(1, 0, 0)) == D(322, 645, 645)
+    assert p.dim() == D(1, 1, 2)
+    assert p.subdomain_size(D(0, 0, 0)) == D(645, 645, 323) and p.subdomain_size(D(0, 0, 1)) == D(645, 645, 322)
+    p = st.NodePartition(D(813, 813, 813), r, 1, 4)
+    assert p.dim() == D(1, 2, 2)
     # x-only radius: cuts avoid the x interface (x-interface weight large)
     rx = st.Radius.constant(0)
     rx.set_dir(1, 0, 0, 4)
