@@ -123,6 +123,12 @@ public:
 
   // ---- output ----
   void write_paraview(const std::string &prefix, bool zeroNaNs = false);
+  // binary checkpoint of every local sub-domain's interior (curr buffers): `prefix_<rank>_<di>.ckpt`, one file per
+  // sub-domain with a header (magic, global size, sub-domain index/origin/size, quantity sizes). load_checkpoint
+  // validates the header against this domain's decomposition and restores the interiors (halos are re-exchanged).
+  // Superset of the reference, which only writes ParaView dumps.
+  void save_checkpoint(const std::string &prefix) const;
+  void load_checkpoint(const std::string &prefix);
 
   // ---- setup / exchange timers (max over ranks, seconds), reference stencil.hpp:106-131 ----
   double timeMpiTopo_ = 0, timeNodeGpus_ = 0, timePeerEn_ = 0, timePlacement_ = 0, timePlan_ = 0, timeRealize_ = 0,

@@ -477,6 +477,8 @@ PYBIND11_MODULE(_C, m) {
       .def("swap", &DistributedDomain::swap)
       .def("write_paraview", &DistributedDomain::write_paraview, py::arg("prefix"), py::arg("zero_nans") = false,
            py::call_guard<py::gil_scoped_release>())
+      .def("save_checkpoint", &DistributedDomain::save_checkpoint, py::call_guard<py::gil_scoped_release>())
+      .def("load_checkpoint", &DistributedDomain::load_checkpoint, py::call_guard<py::gil_scoped_release>())
       .def("dlpack",
            [](std::shared_ptr<DistributedDomain> self, size_t di, int64_t q, bool curr) {
              return make_capsule(self, self->domains().at(di), q, curr);

@@ -13,6 +13,7 @@
 #include <fstream>
 #include <set>
 #include <sstream>
+#include <thread>
 
 #include "stencil/rt/hip_check.hpp"
 #include "stencil/rt/trace.hpp"
@@ -832,6 +833,15 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
 
   const int slot = int(I.epoch & 1);
   const int cv = parity * 2 + slot;
+  // STENCIL_JITTER_US=N: sleep a random 0..N us between transport phases (reference's unused rand_sleep(),
+  // packer.cuh:17-20) to shake out ordering assumptions between ranks and streams
+  static const int jitterUs = [] {
+    const char *e = std::getenv("STENCIL_JITTER_US");
+    return e ? std::atoi(e) : 0;
+  }();
+  auto jitter = [&] {
+    if (jitterUs > 0) std::this_thread::sleep_for(std::chrono::microseconds(std::rand() % (jitterUs + 1)));
+  };
 
   // (1) same-process direct stores (Kernel + PeerCopy)
   for (auto &ctx : I.devs) {
@@ -841,6 +851,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
     if (!over) ctx.translated.record(S(ctx)); // events only matter across streams
   }
 
+  jitter();
   // (2) colocated sends: wait for inbox credit (slot reuse distance 2), pack into the peer's inbox over xGMI,
   //     then raise the peer's arrival flag
   for (auto &ctx : I.devs) {
@@ -858,6 +869,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
     signal_flags_device(arrived, I.epoch, S(ctx));
   }
 
+  jitter();
   // (3) RCCL: pack, one group of send/recv over every local device, unpack
   if (I.rccl) {
     TraceRange t("rccl");
@@ -916,6 +928,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
     }
   }
 
+  jitter();
   // (5) colocated receives: wait for arrival, unpack from our inbox, return the credit to the sender
   for (auto &ctx : I.devs) {
     if (ctx.coloRecv.empty()) continue;
@@ -1024,6 +1037,76 @@ void DistributedDomain::write_paraview(const std::string &prefix, bool zeroNaNs)
         }
     std::fclose(f);
   }
+}
+
+} // namespace stencil
+
+namespace stencil {
+
+namespace {
+struct CkptHeader {
+  uint64_t magic;
+  int64_t global[3];
+  int64_t idx[3];
+  int64_t origin[3];
+  int64_t size[3];
+  int64_t nq;
+};
+constexpr uint64_t kCkptMagic = 0x53544e434b505432ull; // "STNCKPT2"
+} // namespace
+
+void DistributedDomain::save_checkpoint(const std::string &prefix) const {
+  STENCIL_REQUIRE(realized_, "save_checkpoint before realize");
+  const_cast<DistributedDomain *>(this)->sync_exchange();
+  for (size_t di = 0; di < domains_.size(); ++di) {
+    const LocalDomain &d = domains_[di];
+    const std::string path = prefix + "_" + std::to_string(rank()) + "_" + std::to_string(di) + ".ckpt";
+    FILE *f = std::fopen(path.c_str(), "wb");
+    STENCIL_REQUIRE(f, "cannot open " << path);
+    const Dim3 idx = placement_->get_idx(rank(), int(di));
+    CkptHeader h{kCkptMagic, {size_.x, size_.y, size_.z}, {idx.x, idx.y, idx.z}, {d.origin().x, d.origin().y, d.origin().z},
+                 {d.size().x, d.size().y, d.size().z}, d.num_data()};
+    std::fwrite(&h, sizeof(h), 1, f);
+    for (int64_t q = 0; q < d.num_data(); ++q) {
+      const int64_t es = d.elem_size(q);
+      std::fwrite(&es, sizeof(es), 1, f);
+    }
+    for (int64_t q = 0; q < d.num_data(); ++q) {
+      auto v = d.interior_to_host(q);
+      std::fwrite(v.data(), 1, v.size(), f);
+    }
+    std::fclose(f);
+  }
+  pg_->barrier();
+}
+
+void DistributedDomain::load_checkpoint(const std::string &prefix) {
+  STENCIL_REQUIRE(realized_, "load_checkpoint before realize");
+  sync_exchange();
+  for (size_t di = 0; di < domains_.size(); ++di) {
+    LocalDomain &d = domains_[di];
+    const std::string path = prefix + "_" + std::to_string(rank()) + "_" + std::to_string(di) + ".ckpt";
+    FILE *f = std::fopen(path.c_str(), "rb");
+    STENCIL_REQUIRE(f, "cannot open " << path);
+    CkptHeader h{};
+    STENCIL_REQUIRE(std::fread(&h, sizeof(h), 1, f) == 1 && h.magic == kCkptMagic, "bad checkpoint " << path);
+    const Dim3 idx = placement_->get_idx(rank(), int(di));
+    STENCIL_REQUIRE(h.global[0] == size_.x && h.global[1] == size_.y && h.global[2] == size_.z && h.idx[0] == idx.x &&
+                        h.idx[1] == idx.y && h.idx[2] == idx.z && h.size[0] == d.size().x && h.size[1] == d.size().y &&
+                        h.size[2] == d.size().z && h.nq == d.num_data(),
+                    "checkpoint " << path << " does not match this decomposition");
+    for (int64_t q = 0; q < d.num_data(); ++q) {
+      int64_t es = 0;
+      STENCIL_REQUIRE(std::fread(&es, sizeof(es), 1, f) == 1 && es == d.elem_size(q), "element size mismatch in " << path);
+    }
+    for (int64_t q = 0; q < d.num_data(); ++q) {
+      std::vector<unsigned char> v(size_t(d.size().flatten() * d.elem_size(q)));
+      STENCIL_REQUIRE(std::fread(v.data(), 1, v.size(), f) == v.size(), "truncated checkpoint " << path);
+      d.region_from_host(d.halo_pos(Dim3(0, 0, 0), true), d.size(), q, v.data());
+    }
+    std::fclose(f);
+  }
+  pg_->barrier();
 }
 
 } // namespace stencil
