@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "stencil/comm/proc_group.hpp"
+#include "stencil/core/boundary.hpp"
 #include "stencil/domain/local_domain.hpp"
 #include "stencil/domain/packer.hpp"
 #include "stencil/rt/stream.hpp"
@@ -71,6 +72,9 @@ public:
   void set_radius(int64_t r) { radius_ = Radius::constant(r); }
   void set_radius(const Radius &r) { radius_ = r; }
   const Radius &radius() const { return radius_; }
+  // global boundary condition (default periodic everywhere). No message crosses a non-periodic face.
+  void set_boundary(const Boundary &b) { boundary_ = b; }
+  const Boundary &boundary() const { return boundary_; }
   template <typename T> DataHandle<T> add_data(const std::string &name = "") {
     return DataHandle<T>(add_data(int64_t(sizeof(T)), name, dtype_of<T>()), name);
   }
@@ -142,6 +146,7 @@ private:
   Dim3 size_;
   std::shared_ptr<comm::ProcGroup> pg_;
   Radius radius_;
+  Boundary boundary_;
   std::vector<int> gpus_;
   std::vector<int64_t> elemSize_;
   std::vector<std::string> names_;

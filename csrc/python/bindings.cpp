@@ -187,6 +187,17 @@ PYBIND11_MODULE(_C, m) {
       .def("max", &Radius::max)
       .def("__eq__", [](const Radius &a, const Radius &b) { return a == b; })
       .def("__copy__", [](const Radius &r) { return Radius(r); });
+  py::class_<Boundary>(m, "Boundary")
+      .def(py::init<>())
+      .def_static("periodic", &Boundary::periodic)
+      .def_static("axes", &Boundary::axes, py::arg("x"), py::arg("y"), py::arg("z"))
+      .def_static("none", &Boundary::none)
+      .def("set_face", &Boundary::set_face)
+      .def("set_axis", &Boundary::set_axis)
+      .def("face_periodic", &Boundary::face_periodic)
+      .def("wraps", [](const Boundary &b, int x, int y, int z) { return b.wraps(Dim3(x, y, z)); })
+      .def("all_periodic", &Boundary::all_periodic)
+      .def("__eq__", [](const Boundary &a, const Boundary &b) { return a == b; });
 
   py::enum_<MethodFlags>(m, "MethodFlags", py::arithmetic())
       .value("None_", MethodFlags::None)
@@ -434,6 +445,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("x"), py::arg("y"), py::arg("z"), py::arg("group") = nullptr)
       .def("set_radius", py::overload_cast<int64_t>(&DistributedDomain::set_radius))
       .def("set_radius", py::overload_cast<const Radius &>(&DistributedDomain::set_radius))
+      .def("set_boundary", &DistributedDomain::set_boundary)
+      .def("boundary", &DistributedDomain::boundary)
       .def("radius", &DistributedDomain::radius)
       .def("add_data",
            [](DistributedDomain &d, int64_t es, const std::string &name, DType dt) { return d.add_data(es, name, dt); },

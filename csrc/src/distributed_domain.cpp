@@ -15,6 +15,7 @@
 #include <sstream>
 #include <thread>
 
+#include "stencil/comm/tags.hpp"
 #include "stencil/rt/hip_check.hpp"
 #include "stencil/rt/trace.hpp"
 #include "stencil/topo/gpu_topology.hpp"
@@ -86,6 +87,11 @@ struct SegList {
   }
 };
 
+// same (src, dst) pair key, different kind
+static uint32_t retag(uint32_t tag, comm::MsgKind kind) {
+  return comm::make_tag(kind, comm::tag_payload(tag));
+}
+
 struct Channel {
   MethodFlags method = MethodFlags::None;
   bool send = true;
@@ -95,7 +101,8 @@ struct Channel {
   int localDev = -1;
   std::vector<Message> msgs; // sorted by dir
   int64_t bytes = 0;         // packed bytes (reference wire layout)
-  uint32_t tag = 0;
+  uint32_t tag = 0;     // host-plane tag (comm::make_tag(Data, src, dst))
+  int ncclPeer = -1;    // RCCL rank of the remote (rank, device)
   int64_t orderKey = 0; // canonical (src, dst) order for RCCL matching
   char *dbuf = nullptr; // device staging buffer (Rccl, Staged)
   char *hbuf = nullptr; // pinned host (Staged, device backend)
@@ -371,8 +378,8 @@ void DistributedDomain::realize() {
     for (int i = 0; i < 27; ++i) {
       const Dim3 dir = dir_from_index(i);
       if (dir == Dim3(0, 0, 0) || radius_.dir(-dir) == 0) continue;
-      // send
-      {
+      // send (nothing crosses a non-periodic face of the global grid)
+      if (boundary_.reachable(myIdx, dir, gdim)) {
         const Dim3 dstIdx = (myIdx + dir).wrap(gdim);
         const int dstRank = placement_->get_rank(dstIdx), dstId = placement_->get_subdomain_id(dstIdx),
                   dstDev = placement_->get_device(dstIdx);
@@ -403,7 +410,7 @@ void DistributedDomain::realize() {
             c.localDev = myDev;
             const int64_t sl = linearize(myIdx, gdim), dl = linearize(dstIdx, gdim);
             c.orderKey = sl * numSub + dl;
-            c.tag = uint32_t(c.orderKey & 0x0fffffff);
+            c.tag = comm::make_tag(comm::MsgKind::Data, sl, dl, numSub);
             I.chans.push_back(c);
           } else {
             ci = it->second;
@@ -412,7 +419,7 @@ void DistributedDomain::realize() {
         }
       }
       // recv
-      {
+      if (boundary_.reachable(myIdx, -dir, gdim)) {
         const Dim3 srcIdx = (myIdx - dir).wrap(gdim);
         const int srcRank = placement_->get_rank(srcIdx), srcId = placement_->get_subdomain_id(srcIdx),
                   srcDev = placement_->get_device(srcIdx);
@@ -437,7 +444,7 @@ void DistributedDomain::realize() {
           c.localDev = myDev;
           const int64_t sl = linearize(srcIdx, gdim), dl = linearize(myIdx, gdim);
           c.orderKey = sl * numSub + dl;
-          c.tag = uint32_t(c.orderKey & 0x0fffffff);
+          c.tag = comm::make_tag(comm::MsgKind::Data, sl, dl, numSub);
           I.chans.push_back(c);
         } else {
           ci = it->second;
@@ -546,13 +553,13 @@ void DistributedDomain::realize() {
         hipIpcMemHandle_t h;
         HIP_CHECK(hipSetDevice(c.localDev));
         HIP_CHECK(hipIpcGetMemHandle(&h, c.ownBlock));
-        pg.send(c.remoteRank, c.tag | (c.send ? 0x20000000u : 0x10000000u), &h, sizeof(h));
+        pg.send(c.remoteRank, retag(c.tag, c.send ? comm::MsgKind::IpcCredit : comm::MsgKind::IpcInbox), &h, sizeof(h));
       }
       for (auto &c : I.chans) {
         if (c.method != MethodFlags::Colocated) continue;
         hipIpcMemHandle_t h;
-        // a sender needs the receiver's inbox (tagged 0x1...), a receiver the sender's credit block (0x2...)
-        pg.recv(c.remoteRank, c.tag | (c.send ? 0x10000000u : 0x20000000u), &h, sizeof(h));
+        // a sender needs the receiver's inbox, a receiver the sender's credit block
+        pg.recv(c.remoteRank, retag(c.tag, c.send ? comm::MsgKind::IpcInbox : comm::MsgKind::IpcCredit), &h, sizeof(h));
         HIP_CHECK(hipSetDevice(c.localDev));
         HIP_CHECK(hipIpcOpenMemHandle((void **)&c.remoteBlock, h, hipIpcMemLazyEnablePeerAccess));
       }
@@ -631,7 +638,7 @@ void DistributedDomain::realize() {
         NCCL_CHECK(ncclCommInitRank(&I.devs[k].nccl, total, id, first + k));
       }
       NCCL_CHECK(ncclGroupEnd());
-      // translate remote (rank, device) into RCCL ranks: stash in remoteId's high bits is confusing; keep a map
+      // translate remote (rank, device) into RCCL ranks
       std::vector<int> firstOf(pg.size(), 0);
       for (int r = 1; r < pg.size(); ++r) firstOf[r] = firstOf[r - 1] + counts[r - 1];
       for (auto &c : I.chans) {
@@ -640,7 +647,7 @@ void DistributedDomain::realize() {
         for (int k = 0; k < counts[c.remoteRank]; ++k)
           if (allDevs[size_t(c.remoteRank) * maxN + k] == c.remoteDev) slot = k;
         STENCIL_REQUIRE(slot >= 0, "RCCL peer device not found");
-        c.tag = uint32_t(firstOf[c.remoteRank] + slot); // reuse tag as the RCCL peer rank
+        c.ncclPeer = firstOf[c.remoteRank] + slot;
       }
       I.rccl = true;
     }
@@ -881,10 +888,10 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
     NCCL_CHECK(ncclGroupStart());
     for (auto &ctx : I.devs) {
       for (int ci : ctx.rcclSend)
-        NCCL_CHECK(ncclSend(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, int(I.chans[ci].tag), ctx.nccl,
+        NCCL_CHECK(ncclSend(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, I.chans[ci].ncclPeer, ctx.nccl,
                             S(ctx)));
       for (int ci : ctx.rcclRecv)
-        NCCL_CHECK(ncclRecv(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, int(I.chans[ci].tag), ctx.nccl,
+        NCCL_CHECK(ncclRecv(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, I.chans[ci].ncclPeer, ctx.nccl,
                             S(ctx)));
     }
     NCCL_CHECK(ncclGroupEnd());

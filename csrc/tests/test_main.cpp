@@ -1,5 +1,6 @@
 // Native unit tests (ctest). Parity: reference test/test_cpu_*.cpp expectations (radius, mat2d, partition, qap)
 // plus host-backend exchange checks. GPU cases run only with --gpu.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -7,7 +8,11 @@
 #include <string>
 #include <vector>
 
+#include "stencil/comm/tags.hpp"
+#include "stencil/core/array.hpp"
+#include "stencil/core/boundary.hpp"
 #include "stencil/domain/distributed_domain.hpp"
+#include "stencil/rt/allocator.hpp"
 #include "stencil/rt/statistics.hpp"
 #include "stencil/topo/partition.hpp"
 #include "stencil/topo/qap.hpp"
@@ -146,6 +151,135 @@ TEST(host_exchange_asymmetric, false) {
 TEST(gpu_exchange_uniform, true) { check_exchange(Backend::Device, Radius::constant(2), Dim3(10, 9, 8), {0}, MethodFlags::All); }
 TEST(gpu_exchange_two_subdomains_rccl, true) {
   check_exchange(Backend::Device, Radius::constant(1), Dim3(12, 10, 10), {0, 0}, MethodFlags::Rccl);
+}
+
+// reference test/test_cpu_array.cpp / test_cuda_array.cu
+TEST(array_host, false) {
+  Array<int> a(4, 7);
+  CHECK(a.size() == 4 && a[3] == 7);
+  Array<int> b = a;
+  CHECK(a == b);
+  b[0] = 1;
+  CHECK(a != b);
+  b.resize(6);
+  CHECK(b.size() == 6 && b[0] == 1 && b[3] == 7 && b[5] == 0);
+  Array<int> c{1, 2, 3};
+  Array<int> d(std::move(c));
+  CHECK(d.size() == 3 && c.size() == 0 && d[2] == 3);
+}
+
+// reference test/test_cpu_tx.cpp:5-9 (tags are distinct); here distinct across kinds and pairs, and overflow-checked
+TEST(tags_distinct, false) {
+  std::vector<uint32_t> seen;
+  const int64_t n = 9;
+  for (int k = 0; k < 5; ++k)
+    for (int64_t s = 0; s < n; ++s)
+      for (int64_t d = 0; d < n; ++d) seen.push_back(comm::make_tag(comm::MsgKind(k), s, d, n));
+  std::sort(seen.begin(), seen.end());
+  CHECK(std::adjacent_find(seen.begin(), seen.end()) == seen.end());
+  for (uint32_t t : seen) CHECK((t & comm::kTagReserved) == 0);
+  const uint32_t t = comm::make_tag(comm::MsgKind::IpcCredit, 3, 5, n);
+  CHECK(comm::tag_kind(t) == comm::MsgKind::IpcCredit && comm::tag_payload(t) == 3 * 9 + 5);
+  bool threw = false;
+  try {
+    comm::make_tag(comm::MsgKind::Data, 16383, 16383, int64_t(1) << 14);
+  } catch (stencil::Error &) {
+    threw = true;
+  }
+  CHECK(!threw);
+  threw = false;
+  try {
+    comm::make_tag(comm::MsgKind::Data, 0, 0, (int64_t(1) << 14) + 1);
+  } catch (stencil::Error &) {
+    threw = true;
+  }
+  CHECK(threw);
+}
+
+TEST(boundary_flags, false) {
+  Boundary b;
+  CHECK(b.all_periodic() && b.wraps(Dim3(1, -1, 1)));
+  Boundary nx = Boundary::axes(false, true, true);
+  CHECK(!nx.all_periodic() && !nx.wraps(Dim3(1, 0, 0)) && nx.wraps(Dim3(0, 1, -1)) && !nx.wraps(Dim3(-1, 1, 0)));
+  // 2 sub-domains in x: from idx 1, +x leaves the grid
+  CHECK(!nx.reachable(Dim3(1, 0, 0), Dim3(1, 0, 0), Dim3(2, 1, 1)));
+  CHECK(nx.reachable(Dim3(0, 0, 0), Dim3(1, 0, 0), Dim3(2, 1, 1)));
+  CHECK(nx.reachable(Dim3(1, 0, 0), Dim3(0, 1, 0), Dim3(2, 1, 1)));
+  Boundary one;
+  one.set_face(0, 0, -1, false);
+  CHECK(one.face_periodic(0, 0, 1) && !one.face_periodic(0, 0, -1));
+  CHECK(!one.reachable(Dim3(0, 0, 0), Dim3(0, 0, -1), Dim3(1, 1, 3)) && one.reachable(Dim3(0, 0, 2), Dim3(0, 0, 1), Dim3(1, 1, 3)));
+}
+
+// non-periodic x: halos across the global x faces are not written (keep the sentinel); everything else wraps
+static void check_nonperiodic(Backend b, std::vector<int> gpus) {
+  const Dim3 sz(12, 6, 5);
+  DistributedDomain dd(sz.x, sz.y, sz.z, comm::make_single_group());
+  dd.set_backend(b);
+  dd.set_radius(1);
+  dd.set_boundary(Boundary::axes(false, true, true));
+  dd.set_gpus(gpus);
+  dd.set_plan_file("");
+  auto h = dd.add_data<int32_t>("coord");
+  dd.realize();
+  for (auto &d : dd.domains()) {
+    const Dim3 raw = d.raw_size();
+    std::vector<int32_t> v(size_t(raw.flatten()), -1);
+    const Dim3 org = d.accessor_origin();
+    for (int64_t z = 0; z < raw.z; ++z)
+      for (int64_t y = 0; y < raw.y; ++y)
+        for (int64_t x = 0; x < raw.x; ++x) {
+          const Dim3 g = org + Dim3(x, y, z);
+          if (d.get_compute_region().contains(g)) v[size_t(x + raw.x * (y + raw.y * z))] = int32_t(g.x + 1000 * g.y + 1000000 * g.z);
+        }
+    d.region_from_host(Dim3(0, 0, 0), raw, h.id(), v.data());
+  }
+  dd.exchange();
+  int bad = 0, untouched = 0;
+  for (auto &d : dd.domains()) {
+    const Dim3 raw = d.raw_size();
+    auto bytes = d.quantity_to_host(h.id());
+    const int32_t *v = reinterpret_cast<const int32_t *>(bytes.data());
+    const Dim3 org = d.accessor_origin();
+    const Rect3 cr = d.get_compute_region();
+    for (int64_t z = 1; z < raw.z - 1; ++z)
+      for (int64_t y = 1; y < raw.y - 1; ++y)
+        for (int64_t x = 0; x < raw.x; ++x) {
+          const Dim3 g = org + Dim3(x, y, z);
+          if (g.x < cr.lo.x - 1 || g.x > cr.hi.x) continue; // x padding
+          if (cr.contains(g)) continue;
+          const int32_t got = v[size_t(x + raw.x * (y + raw.y * z))];
+          if (g.x < 0 || g.x >= sz.x) {
+            untouched += got == -1;
+            bad += got != -1;
+            continue;
+          }
+          const Dim3 w = g.wrap(sz);
+          bad += got != int32_t(w.x + 1000 * w.y + 1000000 * w.z);
+        }
+  }
+  CHECK(bad == 0);
+  CHECK(untouched > 0);
+}
+TEST(host_exchange_nonperiodic_x, false) { check_nonperiodic(Backend::Host, {0, 0}); }
+TEST(gpu_exchange_nonperiodic_x, true) { check_nonperiodic(Backend::Device, {0, 0}); }
+
+TEST(gpu_allocators_array, true) {
+  std::vector<float, DeviceAllocator<float>> dv(DeviceAllocator<float>(0));
+  dv.reserve(1024);
+  CHECK(dv.capacity() >= 1024);
+  std::vector<int, ManagedAllocator<int>> mv(16, 3, ManagedAllocator<int>(0));
+  int s = 0;
+  for (int x : mv) s += x;
+  CHECK(s == 48);
+  std::vector<char, PinnedAllocator<char>> pv(4096, 1);
+  CHECK(pv[4095] == 1);
+  Array<double, Mem::Device> a(std::vector<double>{1.0, 2.0, 3.0}, 0);
+  auto back = a.to_host();
+  CHECK(back.size() == 3 && back[2] == 3.0);
+  a.memset(0);
+  back = a.to_host();
+  CHECK(back[0] == 0.0 && back[2] == 0.0);
 }
 
 int main(int argc, char **argv) {

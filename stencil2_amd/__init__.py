@@ -27,6 +27,7 @@ if _os.environ.get("STENCIL_SKIP_BUILD") != "1":
 from . import _C  # noqa: E402
 from ._C import (  # noqa: E402,F401
     Backend,
+    Boundary,
     Dim3,
     DType,
     MethodFlags,
@@ -62,7 +63,7 @@ from .parallel.domain import DistributedDomain  # noqa: E402,F401
 from .models.stencil_model import Jacobi3D, AstarothSim, StencilModel  # noqa: E402,F401
 
 __all__ = [
-    "Backend", "Dim3", "DType", "MethodFlags", "PlacementStrategy", "Radius", "Rect3", "Statistics", "StencilKind",
+    "Backend", "Boundary", "Dim3", "DType", "MethodFlags", "PlacementStrategy", "Radius", "Rect3", "Statistics", "StencilKind",
     "DistributedDomain", "Jacobi3D", "AstarothSim", "StencilModel", "init_process_group", "get_group",
     "RankPartition", "NodePartition", "TrivialPlacement", "NodeAwarePlacement", "qap_solve", "qap_solve_catch",
 ]

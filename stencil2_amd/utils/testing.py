@@ -24,7 +24,7 @@ def fill_coords(dd, q: int, poison: int = POISON):
     dd.fill_from_global(q, lambda z, y, x: encode(z, y, x))
 
 
-def expected_full(dd, di: int, radius, poison: int = POISON) -> torch.Tensor:
+def expected_full(dd, di: int, radius, poison: int = POISON, boundary=None) -> torch.Tensor:
     d = dd.domain(di)
     org, raw, sz = d.accessor_origin(), d.raw_size(), d.size()
     cr = d.get_compute_region()
@@ -44,15 +44,24 @@ def expected_full(dd, di: int, radius, poison: int = POISON) -> torch.Tensor:
                 sel = (dz == zz) & (dy == yy) & (dx == xx)
                 if (xx, yy, zz) == (0, 0, 0) or radius.dir(xx, yy, zz) != 0:
                     filled |= sel
+    if boundary is not None:
+        # nothing crosses a non-periodic face of the global grid: cells outside it keep their poison
+        for axis, (g, n) in enumerate(((gx, X), (gy, Y), (gz, Z))):
+            for side in (-1, 1):
+                face = [0, 0, 0]
+                face[axis] = side
+                if not boundary.face_periodic(*face):
+                    out = (g < 0) if side < 0 else (g >= n)
+                    filled &= ~out.expand_as(filled)
     want[~filled] = poison
     return want
 
 
-def check_exchange(dd, q: int, radius, poison: int = POISON):
+def check_exchange(dd, q: int, radius, poison: int = POISON, boundary=None):
     """Return the number of wrong cells over every local sub-domain."""
     bad = 0
     for di in range(dd.num_domains()):
         got = dd.curr(di, q).cpu().long()
-        want = expected_full(dd, di, radius, poison)
+        want = expected_full(dd, di, radius, poison, boundary)
         bad += int((got != want).sum())
     return bad

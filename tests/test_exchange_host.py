@@ -119,3 +119,32 @@ def test_plan_summary_and_methods(st):
     assert all(e.method == st.MethodFlags.Kernel for e in dd.plan())
     assert len(dd.plan()) == 2 * 26
     assert st.methods_to_string(st.MethodFlags.All) == "staged/rccl/colo/peer/kernel"
+
+
+@pytest.mark.parametrize("axes", [(False, True, True), (True, False, True), (False, False, False), (True, True, False)])
+@pytest.mark.parametrize("gpus", [[0], [0, 0, 0, 0]])
+def test_exchange_nonperiodic(st, axes, gpus):
+    """Boundary (reference include/stencil/boundary.hpp, unused there): no halo crosses a non-periodic face."""
+    radius = st.Radius.face_edge_corner(2, 1, 1)
+    b = st.Boundary.axes(*axes)
+    dd = st.DistributedDomain(13, 11, 9, group=st.make_single_group())
+    dd.set_backend(st.Backend.Host)
+    dd.set_radius(radius)
+    dd.set_boundary(b)
+    dd.set_gpus(gpus)
+    q = dd.add_data("q", torch.int64)
+    dd.realize()
+    fill_coords(dd, q)
+    dd.exchange()
+    assert check_exchange(dd, q, radius, boundary=b) == 0
+
+
+def test_native_ctest_cpu():
+    """The native C++ unit tests (stencil_ctest, CPU cases: geometry, partition, QAP, tags, Array, host exchange)."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "bin", "stencil_ctest")
+    if not os.path.exists(exe):
+        pytest.skip("native tests not built")
+    r = subprocess.run([exe, "--cpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
