@@ -29,6 +29,11 @@ def main():
     ap.add_argument("--exchange-iters", type=int, default=20)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--methods", default="all")
+    ap.add_argument("--nt", type=int, default=1, help="non-temporal stencil stores")
+    ap.add_argument("--altz", type=int, default=1, help="alternate the z-march direction every step")
+    ap.add_argument("--ty", type=int, default=2, help="rows per lane of the stencil kernel (2/4/8)")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU)")
     args = ap.parse_args()
 
     import torch
@@ -68,15 +73,19 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=not args.no_overlap, group=pg)
+    tune = st.StencilTune()
+    tune.nontemporal = bool(args.nt)
+    tune.alternate_z = bool(args.altz)
+    tune.ty = args.ty
+    overlap = not args.no_overlap and args.overlap != "off"
+    model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=overlap,
+                        auto_overlap=args.overlap == "auto", tune=tune, group=pg)
     model.init()
-    for _ in range(args.warmup):
-        model.step()
+    model.run(args.warmup)
     model.synchronize()
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        model.step()
+    model.run(args.steps)  # every step is enqueued; whole blocks of steps replay as one hipGraph where possible
     model.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -122,7 +131,8 @@ def main():
             "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": L,
                        "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
                        "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods),
-                       "overlap": model.overlapping()},
+                       "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
+                       "ty": args.ty},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
                       "gcells_per_gpu": round(gcells / n, 3)},

@@ -1,0 +1,179 @@
+// Compute-kernel micro-benchmark: the 7-point Jacobi update on one MI355X against the HBM streaming roofline.
+// No reference counterpart as an app (the reference only cites kernel times, bin/astaroth_sim.cu:130-152); this is
+// the tuning harness behind the Jacobi3D numbers in BASELINE.md.
+// Prints CSV `kernel,variant,ty,zc,us,gcells,eff_TBps` where eff_TBps counts the 8 B/cell minimum traffic.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "stencil/domain/local_domain.hpp"
+#include "stencil/domain/packer.hpp"
+#include "stencil/kernels/stencil_ops.hpp"
+#include "stencil/rt/argparse.hpp"
+#include "stencil/rt/stream.hpp"
+
+using namespace stencil;
+
+// streaming roofline: dst = src over n float4, non-temporal stores, grid-stride
+typedef float f4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void stream_copy(const f4 *__restrict__ src, f4 *__restrict__ dst, int64_t n) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    f4 v = src[i];
+    __builtin_nontemporal_store(v, dst + i);
+  }
+}
+// U independent 16-B loads in flight per lane, contiguous block-sized tiles (each block owns a chunk)
+template <int U>
+__global__ __launch_bounds__(256) void stream_copy_tiles(const f4 *__restrict__ src, f4 *__restrict__ dst, int64_t n) {
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t beg = int64_t(blockIdx.x) * per, end = beg + per < n ? beg + per : n;
+  for (int64_t i = beg + threadIdx.x; i < end; i += 256 * U) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u * 256 < end) v[u] = src[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u * 256 < end) __builtin_nontemporal_store(v[u], dst + i + u * 256);
+  }
+}
+// read-only and write-only streams (the two halves of the roofline)
+__global__ __launch_bounds__(256) void stream_read(const f4 *__restrict__ src, float *__restrict__ sink, int64_t n) {
+  f4 acc = {0, 0, 0, 0};
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) acc += src[i];
+  if (acc.x == 1234.5f) sink[0] = acc.y + acc.z + acc.w;
+}
+__global__ __launch_bounds__(256) void stream_write(f4 *__restrict__ dst, int64_t n) {
+  const f4 v = {1, 2, 3, 4};
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+    __builtin_nontemporal_store(v, dst + i);
+}
+
+int main(int argc, char **argv) {
+  int64_t n = 512;
+  int iters = 20, reps = 1;
+  std::string only;
+  ArgParser p("7-point stencil kernel sweep on one GPU");
+  p.option(&n, "--n", "cube edge").option(&iters, "--iters", "timed launches per config")
+      .option(&reps, "--reps", "repetitions of the whole sweep (interleaved)")
+      .option(&only, "--only", "run only 'lds', 'reg' or 'copy'");
+  if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
+  LocalDomain ld(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
+  ld.set_radius(1);
+  ld.add_data<float>("d");
+  ld.realize();
+  Stream s(0);
+  const Rect3 reg = ld.get_compute_region();
+  const Spheres sph = Spheres::jacobi(reg);
+  jacobi_init(ld, 0, ld.get_full_region(), s);
+  s.sync();
+  const double cells = double(n) * n * n;
+
+  auto timeit = [&](auto &&fn) {
+    for (int i = 0; i < 3; ++i) fn();
+    Event a(0, true), b(0, true);
+    a.record(s);
+    for (int i = 0; i < iters; ++i) fn();
+    b.record(s);
+    b.sync();
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    return double(ms) * 1e3 / iters; // us
+  };
+  std::printf("kernel,variant,ty,zc,us,gcells,eff_TBps\n");
+  if (only.empty() || only == "copy") {
+    const int64_t nv = int64_t(n) * n * n / 4;
+    for (int blocks : {1024, 2048, 4096, 8192}) {
+      const double us = timeit([&] {
+        hipLaunchKernelGGL(stream_copy, dim3(blocks), dim3(256), 0, s, (const f4 *)ld.curr_data(0),
+                           (f4 *)ld.next_data(0), nv);
+      });
+      std::printf("copy,%d,0,0,%.2f,%.1f,%.3f\n", blocks, us, cells / us / 1e3, cells * 8 / us / 1e6);
+    }
+    for (int blocks : {512, 1024, 2048}) {
+      const double us4 = timeit([&] {
+        hipLaunchKernelGGL(stream_copy_tiles<4>, dim3(blocks), dim3(256), 0, s, (const f4 *)ld.curr_data(0),
+                           (f4 *)ld.next_data(0), nv);
+      });
+      std::printf("copy_tiles4,%d,0,0,%.2f,%.1f,%.3f\n", blocks, us4, cells / us4 / 1e3, cells * 8 / us4 / 1e6);
+      const double usr = timeit([&] {
+        hipLaunchKernelGGL(stream_read, dim3(blocks), dim3(256), 0, s, (const f4 *)ld.curr_data(0),
+                           (float *)ld.next_data(0), nv);
+      });
+      std::printf("read_only,%d,0,0,%.2f,%.1f,%.3f\n", blocks, usr, cells / usr / 1e3, cells * 4 / usr / 1e6);
+      const double usw = timeit([&] {
+        hipLaunchKernelGGL(stream_write, dim3(blocks), dim3(256), 0, s, (f4 *)ld.next_data(0), nv);
+      });
+      std::printf("write_only,%d,0,0,%.2f,%.1f,%.3f\n", blocks, usw, cells / usw / 1e3, cells * 4 / usw / 1e6);
+    }
+  }
+  struct Cfg {
+    int variant, ty, zc;
+  };
+  std::vector<Cfg> cfgs;
+  if (only.empty() || only == "lds")
+    for (int ty : {2, 4, 8})
+      for (int zc : {0, 8, 16, 32, 64}) cfgs.push_back({0, ty, zc});
+  if (only.empty() || only == "reg")
+    for (int ty : {4, 8})
+      for (int zc : {0, 16, 32}) cfgs.push_back({1, ty, zc});
+  for (int rep = 0; rep < reps; ++rep)
+  if (only.empty() || only == "xchg") {
+    // the Kernel-transport exchange of a single self-wrapping sub-domain (one copy-plan launch), all faces and per axis
+    const char *names[] = {"xchg_all", "xchg_x", "xchg_y", "xchg_z"};
+    for (int mode = 0; mode < 4; ++mode) {
+      std::vector<CopySeg> segs;
+      for (int ax = 0; ax < 3; ++ax) {
+        if (mode != 0 && mode != ax + 1) continue;
+        for (int sgn = -1; sgn <= 1; sgn += 2) {
+          Dim3 d(0, 0, 0);
+          (ax == 0 ? d.x : ax == 1 ? d.y : d.z) = sgn;
+          build_translate_segs(ld, ld, d, true, segs);
+        }
+      }
+      finalize_segs(segs);
+      CopyPlan cp = make_copy_plan(segs, 0);
+      const double us = timeit([&] { copy_plan_device(cp, s); });
+      std::printf("%s,0,0,0,%.2f,%.1f,%.3f\n", names[mode], us, double(cp.bytes) / us / 1e3, 2.0 * cp.bytes / us / 1e6);
+      free_copy_plan(cp);
+    }
+  }
+  for (int rep = 0; rep < reps; ++rep)
+  if (only.empty() || only == "fwd") {
+    // halo forwarding onto itself (periodic self-wrap of a single sub-domain): all faces, then each axis alone
+    // fwd_xself: x messages stored onto the sender's own output cells (same lines as the main store): separates
+    // the instruction cost of the x path from the cost of its scattered halo lines
+    const char *names[] = {"fwd_all", "fwd_x", "fwd_y", "fwd_z", "fwd_xself"};
+    for (int mode = 0; mode < 5; ++mode)
+    for (int zc : {0, 16, 32, 64}) {
+      std::vector<ForwardTarget> tg;
+      for (int ax = 0; ax < 3; ++ax) {
+        if (mode != 0 && mode != ax + 1 && !(mode == 4 && ax == 0)) continue;
+        for (int sgn = -1; sgn <= 1; sgn += 2) {
+          Dim3 d(0, 0, 0), off(0, 0, 0);
+          (ax == 0 ? d.x : ax == 1 ? d.y : d.z) = sgn;
+          (ax == 0 ? off.x : ax == 1 ? off.y : off.z) = mode == 4 ? 0 : -sgn * n;
+          tg.push_back(ForwardTarget{d, &ld, off});
+        }
+      }
+      HaloForwarder hf(ld, 0, tg);
+      StencilTune t;
+      t.zchunk = zc;
+      const double us = timeit([&] { stencil7_apply(ld, 0, reg, StencilKind::Jacobi, sph, s, t, &hf); });
+      std::printf("%s,0,2,%d,%.2f,%.1f,%.3f\n", names[mode], zc, us, cells / us / 1e3, cells * 8 / us / 1e6);
+    }
+  }
+  for (int rep = 0; rep < reps; ++rep)
+  for (const Cfg &c : cfgs) {
+    StencilTune t;
+    t.variant = c.variant;
+    t.ty = c.ty;
+    t.zchunk = c.zc;
+    const double us = timeit([&] { stencil7_apply(ld, 0, reg, StencilKind::Jacobi, sph, s, t); });
+    std::printf("stencil7,%d,%d,%d,%.2f,%.1f,%.3f\n", c.variant, c.ty, c.zc, us, cells / us / 1e3,
+                cells * 8 / us / 1e6);
+  }
+  return 0;
+}

@@ -26,6 +26,7 @@
 #include "stencil/core/boundary.hpp"
 #include "stencil/domain/local_domain.hpp"
 #include "stencil/domain/packer.hpp"
+#include "stencil/kernels/stencil_ops.hpp"
 #include "stencil/rt/stream.hpp"
 #include "stencil/topo/placement.hpp"
 
@@ -110,6 +111,15 @@ public:
   uint64_t exchange_bytes_for_method(MethodFlags m) const; // summed over all ranks, per exchange
   const std::vector<ExchangePlanEntry> &plan() const { return plan_; }
   std::string plan_summary() const;
+  // Direct-store targets of local domain di: every planned message of di whose receiver this process can write
+  // (Kernel: same GPU, PeerCopy: P2P-mapped peer GPU), with the raw-coordinate offset into the receiver.
+  // Used by the halo-forwarding compute kernels (stencil_ops.hpp HaloForwarder).
+  std::vector<ForwardTarget> forward_targets(size_t di) const;
+  // true when every message of every rank is Kernel or PeerCopy (a pure in-process exchange)
+  bool all_direct() const {
+    return exchange_bytes_for_method(MethodFlags::Kernel | MethodFlags::PeerCopy) ==
+           exchange_bytes_for_method(MethodFlags::All);
+  }
 
   // ---- exchange ----
   void exchange();       // blocking: returns when every halo of every local domain is valid

@@ -31,6 +31,9 @@ void build_unpack_segs(const LocalDomain &dom, const std::vector<Message> &sorte
 // direct same-process translate: src interior slab -> dst -dir halo
 void build_translate_segs(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
                           std::vector<CopySeg> &out);
+// same for one quantity
+void build_translate_segs_q(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr, int64_t q,
+                            std::vector<CopySeg> &out);
 
 class PackerBase {
 public:

@@ -9,6 +9,7 @@
 // ds_bpermute). Blocks are remapped XCD-aware so y/z-adjacent tiles share an XCD's L2. Summation order and the
 // division by 6 are the reference's, so results are bitwise identical to a sequential fp32 evaluation.
 #include <cstdint>
+#include <vector>
 
 #include "stencil/core/geometry.hpp"
 #include "stencil/domain/local_domain.hpp"
@@ -37,16 +38,64 @@ struct Spheres {
 
 struct StencilTune {
   int variant = 0; // 0: LDS-shared y-halo kernel (default), 1: register-only kernel
-  int ty = 4;     // rows per lane (variant 0: 2/4/8, variant 1: 4/8)
-  int zchunk = 0; // planes per block (0 = auto)
+  int ty = 2;     // rows per lane (variant 0: 2/4/8, variant 1: 4/8)
+  int zchunk = 0; // planes per block (0 = auto: exactly one round of resident blocks)
   bool xcdRemap = true;
   bool nontemporal = true;
+  // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous
+  // step wrote last, which are still in the MALL / L2
+  bool alternateZ = true;
+};
+
+// Halo forwarding: the producer writes its neighbours' halos. For every direction whose receiving halo lives in a
+// sub-domain this process can store into directly (same GPU, or a P2P-mapped peer GPU over xGMI), the stencil
+// kernel also stores each boundary output cell into the receiver's *next* buffer (the one that becomes curr after
+// swap). A step is then one kernel per sub-domain (plus a small copy for receivers with a different layout): no
+// pack, no separate exchange, and the halos of the new curr are valid when the step retires. Replaces the reference's separate exchange() for the Kernel/PeerCopy methods
+// (reference tx_cuda.cuh:68-95 multi_translate, :141-162 peer copy).
+struct ForwardTarget {
+  Dim3 dir;                   // send direction
+  const LocalDomain *dst;     // receiving sub-domain (same process)
+  Dim3 offset;                // dst raw coordinate = src raw coordinate + offset
+};
+
+class HaloForwarder {
+public:
+  // per buffer parity (the receivers' next buffers alternate with swap()): an in-kernel store offset for every
+  // receiver that shares this sub-domain's pitches, and a copy plan (run right after the kernel) for the others
+  // (e.g. x neighbours of a different x size in an uneven partition). `targets` come from
+  // DistributedDomain::forward_targets.
+  HaloForwarder(const LocalDomain &src, int64_t qi, const std::vector<ForwardTarget> &targets);
+  ~HaloForwarder();
+  HaloForwarder(const HaloForwarder &) = delete;
+  HaloForwarder &operator=(const HaloForwarder &) = delete;
+  // cells within wm[a] of the low face send along -a, within wp[a] of the high face along +a
+  const int *wm() const { return wm_; }
+  const int *wp() const { return wp_; }
+  int num_targets() const { return n_; }
+  uint32_t mask(int parity) const { return mask_[parity]; }              // directions stored by the kernel
+  int64_t delta(int parity, int k) const { return delta_[parity][k]; }   // element offset from the output cell
+  bool has_rest() const { return hasRest_; }
+  // copy the messages the kernel does not store (after the kernel, same stream)
+  void forward_rest(int parity, hipStream_t stream) const;
+  // can the forwarding kernel handle this sub-domain (aligned vector layout, fp32/fp64, sizes >= slab widths)?
+  static bool supported(const LocalDomain &dom, int64_t qi);
+
+private:
+  int wm_[3] = {0, 0, 0}, wp_[3] = {0, 0, 0};
+  int n_ = 0;
+  int dev_ = -1;
+  uint32_t mask_[2] = {0, 0};
+  int64_t delta_[2][27] = {};
+  CopyPlan rest_[2];
+  bool hasRest_ = false;
 };
 
 // dst(region) = stencil(src) for one quantity of one LocalDomain. `region` is in global coordinates and must lie in
 // the domain's compute region; face radii must be >= 1. `currIsSrc` selects curr->next (true) or next->curr.
+// With `fwd`, region must be the whole compute region and the output is also forwarded into the receivers' halos.
 void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
-                    hipStream_t stream, const StencilTune &tune = StencilTune());
+                    hipStream_t stream, const StencilTune &tune = StencilTune(), const HaloForwarder *fwd = nullptr);
 // same for several regions in one call (e.g. the exterior slabs)
 void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
                             const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());

@@ -34,6 +34,11 @@ struct StencilModelConfig {
   // single stream + kernel-only exchange: capture the step (exchange + stencil) once per buffer parity into a
   // hipGraph and replay it (removes per-kernel launch gaps)
   bool useGraph = true;
+  // in-process exchanges only (Kernel/PeerCopy): the stencil kernel stores its boundary outputs straight into the
+  // receivers' halos (HaloForwarder), so a step is one kernel per sub-domain and no separate exchange runs.
+  // Off by default: on one MI355X the scattered x-face stores cost the kernel more (~+23 us at 512^3) than the
+  // separate copy-plan exchange does (~19 us), see BASELINE.md / bench_stencil.
+  bool forward = false;
   bool setBackend = false;
   Backend backend = Backend::Device;
   StencilTune tune;
@@ -47,9 +52,10 @@ public:
 
   void init();                  // realize + initial condition; blocks until done
   void step();                  // one iteration, asynchronous
-  void run(int iters) {
-    for (int i = 0; i < iters; ++i) step();
-  }
+  // `iters` iterations, asynchronous. In hipGraph mode whole blocks of kGraphSteps steps are replayed as one
+  // graph (one launch instead of kGraphSteps: the GPU-side gap between graph launches is ~9 us on MI355X).
+  void run(int iters);
+  static constexpr int kGraphSteps = 16; // even: the block starts and ends on the same buffer parity
   void synchronize();           // wait for all enqueued work (and check exchange errors)
   DistributedDomain &domain() { return *dd_; }
   const StencilModelConfig &config() const { return cfg_; }
@@ -59,6 +65,7 @@ public:
   int64_t steps_done() const { return steps_; }
   const Spheres &spheres() const { return sph_; }
   bool overlapping() const { return overlap_; }
+  bool forwarding() const { return forward_; }
 
 private:
   StencilModelConfig cfg_;
@@ -70,7 +77,11 @@ private:
   Spheres sph_;
   bool overlap_ = true;
   bool graphs_ = false;
+  bool forward_ = false;
+  std::vector<std::vector<std::unique_ptr<HaloForwarder>>> fwd_; // [domain][quantity]
+  std::vector<Event> stepDone_;                                    // forwarding with several sub-domains
   hipGraphExec_t graphExec_[2] = {nullptr, nullptr};
+  hipGraphExec_t graphBlock_[2] = {nullptr, nullptr}; // kGraphSteps steps starting at parity p
   void enqueue_step();
   int64_t steps_ = 0;
 };

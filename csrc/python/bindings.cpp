@@ -532,7 +532,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ty", &StencilTune::ty)
       .def_readwrite("zchunk", &StencilTune::zchunk)
       .def_readwrite("xcd_remap", &StencilTune::xcdRemap)
-      .def_readwrite("nontemporal", &StencilTune::nontemporal);
+      .def_readwrite("nontemporal", &StencilTune::nontemporal)
+      .def_readwrite("alternate_z", &StencilTune::alternateZ);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())
       .def_readwrite("size", &StencilModelConfig::size)
@@ -547,6 +548,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("overlap", &StencilModelConfig::overlap)
       .def_readwrite("auto_overlap", &StencilModelConfig::autoOverlap)
       .def_readwrite("use_graph", &StencilModelConfig::useGraph)
+      .def_readwrite("forward", &StencilModelConfig::forward)
       .def_property(
           "backend", [](const StencilModelConfig &c) { return c.backend; },
           [](StencilModelConfig &c, Backend b) {
@@ -569,6 +571,7 @@ PYBIND11_MODULE(_C, m) {
       .def("local_cells", &StencilModel::local_cells)
       .def("steps_done", &StencilModel::steps_done)
       .def("overlapping", &StencilModel::overlapping)
+      .def("forwarding", &StencilModel::forwarding)
       .def("compute_stream", [](StencilModel &mdl, size_t di) { return reinterpret_cast<uintptr_t>(mdl.compute_stream(di)); })
       .def("domain",
            [](std::shared_ptr<StencilModel> mdl) {

@@ -677,6 +677,27 @@ std::string DistributedDomain::plan_summary() const {
   return ss.str();
 }
 
+std::vector<ForwardTarget> DistributedDomain::forward_targets(size_t di) const {
+  STENCIL_REQUIRE(realized_, "forward_targets before realize()");
+  const Dim3 myIdx = placement_->get_idx(rank(), int(di));
+  const Dim3 gdim = placement_->dim();
+  const LocalDomain &src = domains_.at(di);
+  std::vector<ForwardTarget> out;
+  for (const auto &e : plan_) {
+    if (e.srcIdx != myIdx || (e.method != MethodFlags::Kernel && e.method != MethodFlags::PeerCopy)) continue;
+    const LocalDomain &dst = domains_.at(size_t(placement_->get_subdomain_id(e.dstIdx)));
+    // global coordinate of the receiving halo cell = sender's cell - wrap, where wrap = +-global size when the
+    // step crosses the periodic boundary
+    const Dim3 step = myIdx + e.dir;
+    Dim3 wrap(0, 0, 0);
+    wrap.x = step.x >= gdim.x ? size_.x : (step.x < 0 ? -size_.x : 0);
+    wrap.y = step.y >= gdim.y ? size_.y : (step.y < 0 ? -size_.y : 0);
+    wrap.z = step.z >= gdim.z ? size_.z : (step.z < 0 ? -size_.z : 0);
+    out.push_back(ForwardTarget{e.dir, &dst, src.accessor_origin() - dst.accessor_origin() - wrap});
+  }
+  return out;
+}
+
 uint64_t DistributedDomain::exchange_bytes_for_method(MethodFlags m) const {
   uint64_t r = 0;
   const MethodFlags all[] = {MethodFlags::Staged, MethodFlags::Rccl, MethodFlags::Colocated, MethodFlags::PeerCopy,

@@ -66,57 +66,75 @@ template <> struct VecOf<4> { using T = uint32_t; };
 template <> struct VecOf<2> { using T = uint16_t; };
 template <> struct VecOf<1> { using T = uint8_t; };
 
-template <uint32_t V> __device__ __forceinline__ void copy_unit(char *dst, const char *src) {
-  using T = typename VecOf<V>::T;
-  *reinterpret_cast<T *>(dst) = *reinterpret_cast<const T *>(src);
-}
-
-template <uint32_t V> __device__ __forceinline__ void copy_row(char *dst, const char *src, uint32_t n) {
-  for (uint32_t k = 0; k < n; ++k) copy_unit<V>(dst + k * V, src + k * V);
-}
-
 // One block per work-table entry; the entry and its segment are wave-uniform (scalar loads). Narrow-row segments
-// (x-faces) assign one row per thread, wide rows one 16-B unit per thread, so a y/z face moves 1 KiB per wave
-// instruction and the strided x-face rows are spread over every lane.
+// (x-faces) assign one row per item, wide rows one 16-B unit per item, so a y/z face moves 1 KiB per wave
+// instruction and the strided x-face rows are spread over every lane. Each thread owns up to kItems items
+// (stride 256) and issues all their loads before any store, so the scattered x-face accesses of a thread are in
+// flight together instead of one round trip per item.
+constexpr uint32_t kItems = 4;
+
+template <uint32_t V, uint32_t MAXN>
+__device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w) {
+  using T = typename VecOf<V>::T;
+  const uint32_t ru = s.row_units, ny = s.ny;
+  const int64_t sys = s.src_ystride, szs = s.src_zstride, dys = s.dst_ystride, dzs = s.dst_zstride;
+  const uint32_t n = w.rows ? ru : 1;
+  for (uint32_t base = threadIdx.x; base < w.count; base += 256 * kItems) {
+    T v[kItems][MAXN];
+    char *dps[kItems];
+#pragma unroll
+    for (uint32_t k = 0; k < kItems; ++k) {
+      const uint32_t it = base + k * 256;
+      dps[k] = nullptr;
+      if (it < w.count) {
+        const uint32_t item = w.first + it;
+        uint32_t r, c;
+        if (w.rows) {
+          r = item;
+          c = 0;
+        } else {
+          r = item / ru;
+          c = item - r * ru;
+        }
+        const uint32_t y = r % ny, z = r / ny;
+        const T *sp = reinterpret_cast<const T *>(s.src + int64_t(z) * szs + int64_t(y) * sys + uint64_t(c) * V);
+        dps[k] = s.dst + int64_t(z) * dzs + int64_t(y) * dys + uint64_t(c) * V;
+#pragma unroll
+        for (uint32_t u = 0; u < MAXN; ++u)
+          if (u < n) v[k][u] = sp[u];
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kItems; ++k)
+      if (dps[k]) {
+        T *dp = reinterpret_cast<T *>(dps[k]);
+#pragma unroll
+        for (uint32_t u = 0; u < MAXN; ++u)
+          if (u < n) dp[u] = v[k][u];
+      }
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_plan_kernel(const CopySeg *__restrict__ segs,
                                                         const CopyWork *__restrict__ work) {
   const CopyWork w = work[blockIdx.x];
-  const CopySeg &s = segs[w.seg];
-  const uint32_t vec = s.vec, ru = s.row_units, ny = s.ny;
-  const int64_t sys = s.src_ystride, szs = s.src_zstride, dys = s.dst_ystride, dzs = s.dst_zstride;
-  const char *src = s.src;
-  char *dst = s.dst;
-  for (uint32_t it = threadIdx.x; it < w.count; it += blockDim.x) {
-    const uint32_t item = w.first + it;
-    uint32_t r, c;
-    if (w.rows) {
-      r = item;
-      c = 0;
-    } else {
-      r = item / ru;
-      c = item - r * ru;
-    }
-    const uint32_t y = r % ny, z = r / ny;
-    const char *sp = src + int64_t(z) * szs + int64_t(y) * sys + uint64_t(c) * vec;
-    char *dp = dst + int64_t(z) * dzs + int64_t(y) * dys + uint64_t(c) * vec;
-    const uint32_t n = w.rows ? ru : 1;
-    switch (vec) {
-    case 16:
-      copy_row<16>(dp, sp, n);
-      break;
-    case 8:
-      copy_row<8>(dp, sp, n);
-      break;
-    case 4:
-      copy_row<4>(dp, sp, n);
-      break;
-    case 2:
-      copy_row<2>(dp, sp, n);
-      break;
-    default:
-      copy_row<1>(dp, sp, n);
-      break;
-    }
+  const CopySeg s = segs[w.seg];
+  switch (s.vec) {
+  case 16:
+    copy_items<16, 4>(s, w);
+    break;
+  case 8:
+    copy_items<8, 4>(s, w);
+    break;
+  case 4:
+    copy_items<4, 4>(s, w);
+    break;
+  case 2:
+    copy_items<2, 4>(s, w);
+    break;
+  default:
+    copy_items<1, 4>(s, w);
+    break;
   }
 }
 

@@ -4,7 +4,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <mutex>
 
+#include "stencil/domain/packer.hpp"
 #include "stencil/kernels/stencil_ops.hpp"
 #include "stencil/rt/hip_check.hpp"
 
@@ -50,7 +53,15 @@ template <typename T> struct StencilArgs {
   // spheres, raw coordinates
   int hx, hy, hz, cx, cy, cz;
   int r1sq; // (radius+1)^2, 0 = disabled
+  // halo forwarding (FWD kernels): cells within fwm[a] of the low face send along -a, within fwp[a] of the high
+  // face along +a; the receiving halo cell of direction k = (dx+1) + 3(dy+1) + 9(dz+1) is at (own output address +
+  // fd[k]) for every k set in fmask (receivers with our pitches; the rest is copied after the kernel)
+  int flip; // reverse every block's z-march direction (alternated per step, see StencilTune::alternateZ)
+  int fwm[3], fwp[3];
+  uint32_t fmask;
+  int64_t fd[27];
 };
+
 
 // bijective XCD-aware remap: consecutive logical ids land on the same XCD (blocks b, b+8, ... share one)
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t hw, uint32_t n) {
@@ -211,11 +222,48 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
   }
 }
 
+// Forward one output row chunk into the edge/corner halos it feeds (messages with two or three non-zero
+// direction components; faces are stored inline by the kernel). sy/sz: wave-uniform y/z slab sides of the row,
+// xside/xm: this lane's x slab side and element mask. Store address = own output address + fd[k].
+template <typename T, int V>
+__device__ __forceinline__ void forward_edges(const StencilArgs<T> &a, T *dp, const T (&out)[V], int xb, bool fullX,
+                                              int sy, int sz, int xside, uint32_t xm) {
+  using NV = typename Vec16<T>::native;
+  for (int kz = 0; kz < 2; ++kz) {
+    if (kz && !sz) break;
+    const int dz = kz ? sz : 0;
+    for (int ky = 0; ky < 2; ++ky) {
+      if (ky && !sy) break;
+      const int dy = ky ? sy : 0;
+      const int k = 13 + 3 * dy + 9 * dz;
+      if (dy != 0 && dz != 0 && (a.fmask >> k & 1u)) { // y-z edge: whole row chunk
+        T *q = dp + a.fd[k];
+        if (fullX) {
+          NV v;
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[e] = out[e];
+          *reinterpret_cast<NV *>(q) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (xb + e >= a.lox && xb + e < a.hix) q[e] = out[e];
+        }
+      }
+      if ((dy | dz) != 0 && xside != 0 && (a.fmask >> (k + xside) & 1u)) { // x-y, x-z edges and corners
+        T *q = dp + a.fd[k + xside];
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (xm >> e & 1u) q[e] = out[e];
+      }
+    }
+  }
+}
+
 // v3: block = NW waves stacked in y, TY rows per wave, one shared 16-B x-chunk column of 64 lanes. The y-halo rows of
 // every wave come from its neighbours through LDS (double-buffered by z parity, one barrier per z step), so HBM
 // reads per output row drop from (TY+2)/TY to (NW*TY+2)/(NW*TY).
-template <typename T, int TY, int NW, int KIND, bool NT, bool REMAP>
-__global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a) {
+template <typename T, int TY, int NW, int KIND, bool NT, bool REMAP, bool FWD>
+__global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void stencil7_lds_kernel(StencilArgs<T> a) {
   using VT = typename Vec16<T>::type;
   constexpr int V = Vec16<T>::N;
   constexpr int SLOTS = 2 * NW + 2; // per wave: top row, bottom row; plus block halo above and below
@@ -238,7 +286,7 @@ __global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a)
   if (yblk >= a.hiy || zs >= ze) return; // block-uniform: every wave of the block leaves together
   // odd z-chunks march downwards: a chunk boundary is then read by both neighbouring chunks at the same time
   // (both start there, or both end there), so the warm-up planes are L2/MALL hits instead of HBM re-reads
-  const bool down = (bz & 1) != 0;
+  const bool down = ((bz & 1) != 0) != (a.flip != 0);
   const int dz = down ? -1 : 1;
   const int z0 = down ? ze - 1 : zs;
   const int nzs = ze - zs;
@@ -246,6 +294,47 @@ __global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a)
   const bool edgeL = lane == 0;
   const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
   const bool fullX = xb >= a.lox && xb + V <= a.hix;
+  // forwarding state, all fixed for the whole z-march except the z slab:
+  //   x: this lane's slab side, element mask and (for single-cell slabs) the element index; pure-x store offset
+  //   y: per row i of the wave, the slab side (wave-uniform) and the pure-y store offset (SGPRs)
+  //   edges/corners (several non-zero components) take the general path, only if such messages exist
+  int fxside = 0, fxe = -1;
+  uint32_t fxm = 0, fxmPure = 0;
+  int64_t fxd = 0;
+  int fsy[TY];
+  int64_t fdy[TY];
+  T fxv[TY];
+  bool fedges = false;
+  if (FWD) {
+    if (cvalid) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int x = xb + e;
+        if (x >= a.lox && x < a.lox + a.fwm[0]) {
+          fxm |= 1u << e;
+          fxside = -1;
+        }
+        if (x >= a.hix - a.fwp[0] && x < a.hix) {
+          fxm |= 1u << e;
+          fxside = 1;
+        }
+      }
+      if (fxside != 0 && (a.fmask >> (13 + fxside) & 1u)) {
+        fxmPure = fxm;
+        fxd = a.fd[13 + fxside];
+        if (__builtin_popcount(fxm) == 1) fxe = __builtin_ctz(fxm); // only edge lanes get fxe >= 0
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TY; ++i) {
+      const int y = ybase + i;
+      fsy[i] = y < a.loy + a.fwm[1] ? -1 : (y >= a.hiy - a.fwp[1] ? 1 : 0);
+      fdy[i] = (fsy[i] != 0 && (a.fmask >> (13 + 3 * fsy[i]) & 1u)) ? a.fd[13 + 3 * fsy[i]] : int64_t(-1) << 62;
+    }
+    // any message with two or more non-zero components?
+    constexpr uint32_t kFaces = (1u << 4) | (1u << 10) | (1u << 12) | (1u << 14) | (1u << 16) | (1u << 22);
+    fedges = (a.fmask & ~kFaces) != 0;
+  }
   const int slotTop = 2 * w, slotBot = 2 * w + 1;
   const int slotAbove = w == 0 ? 2 * NW : 2 * (w - 1) + 1;
   const int slotBelow = w == NW - 1 ? 2 * NW + 1 : 2 * (w + 1);
@@ -295,6 +384,12 @@ __global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a)
     const VT below = lds[buf][slotBelow][lane];
 
     const int dzh = z - a.hz, dzc = z - a.cz;
+    int fsz = 0;
+    int64_t fdz = int64_t(-1) << 62;
+    if constexpr (FWD) {
+      fsz = z < a.loz + a.fwm[2] ? -1 : (z >= a.hiz - a.fwp[2] ? 1 : 0);
+      if (fsz != 0 && (a.fmask >> (13 + 9 * fsz) & 1u)) fdz = a.fd[13 + 9 * fsz];
+    }
 #pragma unroll
     for (int i = 0; i < TY; ++i) {
       const int y = ybase + i;
@@ -361,6 +456,50 @@ __global__ __launch_bounds__(64 * NW) void stencil7_lds_kernel(StencilArgs<T> a)
           for (int e = 0; e < V; ++e)
             if (xb + e >= a.lox && xb + e < a.hix) dp[e] = out[e];
         }
+        if constexpr (FWD) {
+          using NV = typename Vec16<T>::native;
+          // pure x: single-cell slabs are stashed (one select, no branch) and stored once per plane below;
+          // wider slabs are stored here by the edge lane
+          if (fxe >= 0) {
+            T v = out[0];
+#pragma unroll
+            for (int e = 1; e < V; ++e) v = fxe == e ? out[e] : v;
+            fxv[i] = v;
+          } else if (fxmPure) {
+            T *q = dp + fxd;
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              if (fxmPure >> e & 1u) q[e] = out[e];
+          }
+          // pure y / pure z: wave-uniform, offsets already in SGPRs
+          const bool yrow = fdy[i] != (int64_t(-1) << 62), zrow = fdz != (int64_t(-1) << 62);
+          if (yrow || zrow) {
+            NV v;
+#pragma unroll
+            for (int e = 0; e < V; ++e) v[e] = out[e];
+            if (fullX) {
+              if (yrow) *reinterpret_cast<NV *>(dp + fdy[i]) = v;
+              if (zrow) *reinterpret_cast<NV *>(dp + fdz) = v;
+            } else {
+#pragma unroll
+              for (int e = 0; e < V; ++e)
+                if (xb + e >= a.lox && xb + e < a.hix) {
+                  if (yrow) dp[fdy[i] + e] = out[e];
+                  if (zrow) dp[fdz + e] = out[e];
+                }
+            }
+          }
+          if (fedges && ((fsy[i] != 0) + (fsz != 0) + (fxside != 0) >= 2))
+            forward_edges<T, V>(a, dp, out, xb, fullX, fsy[i], fsz, fxside, fxm);
+        }
+      }
+    }
+    if constexpr (FWD) {
+      if (fxe >= 0) { // edge lanes only: the plane's stashed single-cell x messages
+        T *q = a.dst + int64_t(z) * a.pxy + int64_t(ybase) * a.px + (xb + fxe) + fxd;
+#pragma unroll
+        for (int i = 0; i < TY; ++i)
+          if (ybase + i < a.hiy) q[int64_t(i) * a.px] = fxv[i];
       }
     }
     // publish plane z+1 boundary rows for the next step
@@ -677,6 +816,23 @@ static void launch_fast(StencilArgs<T> a, const StencilTune &tune, hipStream_t s
   HIP_CHECK(hipGetLastError());
 }
 
+// resident blocks of `kernel` over the whole device (cached per kernel)
+static int64_t resident_blocks(const void *kernel, int threads) {
+  static std::map<const void *, int64_t> cache;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  int dev = 0, perCU = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, threads, 0) != hipSuccess || perCU <= 0) perCU = 2;
+  (void)hipGetLastError();
+  const int64_t r = int64_t(perCU) * cus;
+  cache[kernel] = r;
+  return r;
+}
+
 template <typename T, int TY, int NW, int KIND>
 static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t stream) {
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
@@ -684,28 +840,48 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
   a.gy = (ny + NW * TY - 1) / (NW * TY);
   int zc = tune.zchunk;
   if (zc <= 0) {
-    // ~8 waves per SIMD over 256 CUs in one round, z-chunks >= 16 planes (warm-up planes are shared, see kernel)
+    // Exactly one round of resident blocks (occupancy x CUs): a partial second round leaves most CUs idle at the
+    // end (512^3, 2 rows/lane: 1024 blocks at 768 resident ran 20% slower than 768 or 512). z-chunks >= 16
+    // planes (the warm-up planes of neighbouring chunks are shared, see kernel).
     const int64_t cols = int64_t(a.gx) * a.gy;
-    const int64_t targetBlocks = 256 * 4 * 8 / NW;
-    const int64_t nzc = std::max<int64_t>(1, (targetBlocks + cols - 1) / cols);
+    const int64_t targetBlocks = resident_blocks(a.fmask ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>
+                                                         : (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false>,
+                                                 64 * NW);
+    const int64_t nzc = std::max<int64_t>(1, targetBlocks / cols);
     zc = int(std::max<int64_t>(16, (nz + nzc - 1) / nzc));
   }
   a.zc = zc;
   a.gz = (nz + zc - 1) / zc;
   const uint32_t blocks = uint32_t(a.gx) * a.gy * a.gz;
   const dim3 block(64, NW);
-  if (tune.xcdRemap)
-    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true>), dim3(blocks), block, 0, stream, a);
+  if (a.fmask)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>), dim3(blocks), block, 0, stream, a);
+  else if (!tune.nontemporal)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, false, true, false>), dim3(blocks), block, 0, stream, a);
+  else if (tune.xcdRemap)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, false>), dim3(blocks), block, 0, stream, a);
   else
-    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, false>), dim3(blocks), block, 0, stream, a);
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, false, false>), dim3(blocks), block, 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }
 
 template <typename T, int KIND>
 static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
-                    const StencilTune &tune) {
+                    const StencilTune &tune, const HaloForwarder *fwd) {
   if (region.empty()) return;
   StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
+  a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
+  if (fwd) {
+    STENCIL_REQUIRE(region == dom.get_compute_region(), "halo forwarding needs the whole compute region");
+    STENCIL_REQUIRE(HaloForwarder::supported(dom, qi), "halo forwarding not supported for this layout");
+    const int par = dom.parity();
+    for (int k = 0; k < 3; ++k) {
+      a.fwm[k] = fwd->wm()[k];
+      a.fwp[k] = fwd->wp()[k];
+    }
+    a.fmask = fwd->mask(par);
+    for (int k = 0; k < 27; ++k) a.fd[k] = fwd->delta(par, k);
+  }
   if (dom.backend() == Backend::Host) {
     host_apply<T, KIND>(dom, a);
     return;
@@ -721,8 +897,12 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
   // vector loads and the right-edge neighbour stay inside the padded row (LocalDomain keeps >= V+1 tail elements)
   const bool fits = a.x0 + int64_t(a.nchunks) * V < a.px - dom.pad_x(qi);
   dom.set_device();
-  if (alignedLayout && fits && std::getenv("STENCIL_GENERIC_KERNEL") == nullptr) {
-    if (tune.variant == 1) {
+  STENCIL_REQUIRE(!fwd || (alignedLayout && fits), "halo forwarding needs the aligned vector layout");
+  if (alignedLayout && fits && (fwd || std::getenv("STENCIL_GENERIC_KERNEL") == nullptr)) {
+    if (fwd) {
+      // the forwarding epilogue needs registers: 2 rows per lane keeps it spill-free at >= 4 waves/SIMD
+      launch_lds<T, 2, 8, KIND>(a, tune, stream);
+    } else if (tune.variant == 1) {
       if (tune.ty == 4)
         launch_fast<T, 4, KIND>(a, tune, stream);
       else
@@ -744,7 +924,7 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
 }
 
 void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
-                    hipStream_t stream, const StencilTune &tune) {
+                    hipStream_t stream, const StencilTune &tune, const HaloForwarder *fwd) {
   STENCIL_REQUIRE(dom.radius().x(-1) >= 1 && dom.radius().x(1) >= 1 && dom.radius().y(-1) >= 1 &&
                       dom.radius().y(1) >= 1 && dom.radius().z(-1) >= 1 && dom.radius().z(1) >= 1,
                   "7-point stencil needs face radii >= 1");
@@ -757,14 +937,14 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
   const bool f64 = dt == DType::F64 || (dt == DType::Bytes && dom.elem_size(qi) == 8);
   if (f32) {
     if (kind == StencilKind::Jacobi)
-      apply_t<float, 0>(dom, qi, region, sph, stream, tune);
+      apply_t<float, 0>(dom, qi, region, sph, stream, tune, fwd);
     else
-      apply_t<float, 1>(dom, qi, region, sph, stream, tune);
+      apply_t<float, 1>(dom, qi, region, sph, stream, tune, fwd);
   } else if (f64) {
     if (kind == StencilKind::Jacobi)
-      apply_t<double, 0>(dom, qi, region, sph, stream, tune);
+      apply_t<double, 0>(dom, qi, region, sph, stream, tune, fwd);
     else
-      apply_t<double, 1>(dom, qi, region, sph, stream, tune);
+      apply_t<double, 1>(dom, qi, region, sph, stream, tune, fwd);
   } else {
     LOG_FATAL("stencil7 supports fp32/fp64 quantities only");
   }
@@ -858,6 +1038,95 @@ void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vecto
   else
     kind == StencilKind::Jacobi ? apply_regions_t<double, 0>(dom, qi, regions, sph, stream)
                                 : apply_regions_t<double, 1>(dom, qi, regions, sph, stream);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// halo forwarder tables
+// ---------------------------------------------------------------------------------------------------------
+static bool fp_quantity(const LocalDomain &dom, int64_t qi, int64_t *es) {
+  const DType dt = dom.dtype(qi);
+  *es = dom.elem_size(qi);
+  return dt == DType::F32 || dt == DType::F64 || (dt == DType::Bytes && (*es == 4 || *es == 8));
+}
+
+bool HaloForwarder::supported(const LocalDomain &dom, int64_t qi) {
+  int64_t es = 0;
+  if (dom.backend() != Backend::Device || !fp_quantity(dom, qi, &es)) return false;
+  const Radius &r = dom.radius();
+  const Dim3 sz = dom.size();
+  // a cell must not belong to both the low and the high slab of an axis
+  if (sz.x < r.x(1) + r.x(-1) || sz.y < r.y(1) + r.y(-1) || sz.z < r.z(1) + r.z(-1)) return false;
+  // one 16-B chunk never holds cells of both x slabs
+  if (sz.x < 2 * (16 / std::max<int64_t>(es, 1)) + r.x(1) + r.x(-1)) return false;
+  // same layout checks as the vector kernel (apply_t)
+  const int64_t V = 16 / es;
+  const Dim3 p = dom.pitch(qi);
+  const int64_t lox = r.x(-1), hix = lox + sz.x;
+  const int64_t x0 = lox - ((lox - r.x(-1)) % V + V) % V;
+  const int64_t nchunks = (hix - x0 + V - 1) / V;
+  const bool aligned = (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + x0 * es) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + x0 * es) % 16 == 0) &&
+                       (p.x * es) % 16 == 0;
+  return aligned && x0 + nchunks * V < p.x - dom.pad_x(qi);
+}
+
+HaloForwarder::HaloForwarder(const LocalDomain &src, int64_t qi, const std::vector<ForwardTarget> &targets) {
+  STENCIL_REQUIRE(supported(src, qi), "halo forwarding not supported for this sub-domain/quantity");
+  dev_ = src.gpu();
+  n_ = int(targets.size());
+  const Radius &r = src.radius();
+  // sending along +a feeds the receiver's -a halo (width = face radius on the -a side), and vice versa
+  wp_[0] = int(r.x(-1));
+  wp_[1] = int(r.y(-1));
+  wp_[2] = int(r.z(-1));
+  wm_[0] = int(r.x(1));
+  wm_[1] = int(r.y(1));
+  wm_[2] = int(r.z(1));
+  const int64_t es = src.elem_size(qi);
+  const int64_t V = 16 / es;
+  const Dim3 sp = src.pitch(qi);
+  src.set_device();
+  for (int par = 0; par < 2; ++par) {
+    // all sub-domains swap together: at sender parity `par` every receiver's next buffer is the one that is next
+    // (par == current parity) or curr (otherwise) right now
+    const bool now = src.parity() == par;
+    const char *srcNext = static_cast<const char *>(now ? src.next_data(qi) : src.curr_data(qi));
+    std::vector<CopySeg> rest;
+    for (const auto &ft : targets) {
+      const LocalDomain &d = *ft.dst;
+      STENCIL_REQUIRE(d.elem_size(qi) == es, "forward target element size");
+      const Dim3 dp = d.pitch(qi);
+      const char *dstNext = static_cast<const char *>(d.parity() == par ? d.next_data(qi) : d.curr_data(qi));
+      const int64_t byteGap = dstNext - srcNext;
+      const int k = int((ft.dir.x + 1) + 3 * (ft.dir.y + 1) + 9 * (ft.dir.z + 1));
+      // in-kernel when the receiver shares our pitches (so the offset is constant) and rows keep 16-B alignment
+      const bool samePitch = dp.x == sp.x && dp.y == sp.y;
+      const bool aligned = byteGap % es == 0 && (ft.dir.x != 0 || ((byteGap / es + ft.offset.x) % V == 0));
+      if (samePitch && aligned) {
+        mask_[par] |= 1u << k;
+        delta_[par][k] = byteGap / es + ft.offset.z * sp.x * sp.y + ft.offset.y * sp.x + ft.offset.x;
+      } else {
+        build_translate_segs_q(src, d, ft.dir, !now, qi, rest);
+      }
+    }
+    if (!rest.empty()) {
+      finalize_segs(rest);
+      rest_[par] = make_copy_plan(rest, dev_);
+      hasRest_ = true;
+    }
+  }
+}
+
+HaloForwarder::~HaloForwarder() {
+  for (auto &p : rest_)
+    if (p.dsegs) {
+      (void)hipSetDevice(dev_);
+      free_copy_plan(p);
+    }
+}
+
+void HaloForwarder::forward_rest(int parity, hipStream_t stream) const {
+  if (rest_[parity].dsegs) copy_plan_device(rest_[parity], stream);
 }
 
 // ---------------------------------------------------------------------------------------------------------

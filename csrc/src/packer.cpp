@@ -63,14 +63,17 @@ void build_unpack_segs(const LocalDomain &dom, const std::vector<Message> &msgs,
 }
 
 // direct translate src interior slab -> dst halo (same process)
-void build_translate_segs(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
+void build_translate_segs_q(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr, int64_t q,
                             std::vector<CopySeg> &out) {
-  for (int64_t q = 0; q < src.num_data(); ++q) {
-    const int64_t es = src.elem_size(q);
-    const Dim3 ext = src.halo_extent(-dir);
-    out.push_back(make_copy_seg(src.box(q, curr, src.halo_pos(dir, false)), dst.box(q, curr, dst.halo_pos(-dir, true)),
-                                ext, es));
-  }
+  const int64_t es = src.elem_size(q);
+  const Dim3 ext = src.halo_extent(-dir);
+  out.push_back(make_copy_seg(src.box(q, curr, src.halo_pos(dir, false)), dst.box(q, curr, dst.halo_pos(-dir, true)),
+                              ext, es));
+}
+
+void build_translate_segs(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
+                          std::vector<CopySeg> &out) {
+  for (int64_t q = 0; q < src.num_data(); ++q) build_translate_segs_q(src, dst, dir, curr, q, out);
 }
 
 

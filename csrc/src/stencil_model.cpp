@@ -36,6 +36,8 @@ StencilModel::~StencilModel() {
   }
   for (auto &g : graphExec_)
     if (g) (void)hipGraphExecDestroy(g);
+  for (auto &g : graphBlock_)
+    if (g) (void)hipGraphExecDestroy(g);
 }
 
 int64_t StencilModel::local_cells() const {
@@ -55,6 +57,12 @@ void StencilModel::init() {
   if (cfg_.overlap && cfg_.autoOverlap &&
       dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All))
     overlap_ = false;
+  auto &doms0 = dd_->domains();
+  forward_ = cfg_.forward && std::getenv("STENCIL_NO_FORWARD") == nullptr && dd_->world_size() == 1 &&
+             dd_->all_direct() && !doms0.empty();
+  for (const auto &d : doms0)
+    for (int64_t q = 0; q < d.num_data() && forward_; ++q) forward_ = HaloForwarder::supported(d, q);
+  if (forward_) overlap_ = false; // the halos travel inside the stencil kernel
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
@@ -79,6 +87,18 @@ void StencilModel::init() {
   synchronize();
   for (size_t di = 0; di < doms.size(); ++di)
     if (!compute_.empty()) dd_->record_ready(di, compute_[di]);
+  if (forward_) {
+    // from now on the kernels keep the halos current; fill them once for the initial state
+    dd_->exchange();
+    fwd_.resize(doms.size());
+    for (size_t di = 0; di < doms.size(); ++di) {
+      const auto targets = dd_->forward_targets(di);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        fwd_[di].emplace_back(new HaloForwarder(doms[di], q, targets));
+      stepDone_.emplace_back(doms[di].gpu());
+    }
+    for (size_t di = 0; di < doms.size(); ++di) stepDone_[di].record(compute_[di]);
+  }
 }
 
 void StencilModel::step() {
@@ -110,9 +130,54 @@ void StencilModel::step() {
   ++steps_;
 }
 
+void StencilModel::run(int iters) {
+  TraceRange tr("StencilModel::run");
+  auto &doms = dd_->domains();
+  while (graphs_ && iters >= kGraphSteps) {
+    const int p = doms[0].parity();
+    hipStream_t s = compute_[0].get();
+    if (!graphBlock_[p]) {
+      hipGraph_t g = nullptr;
+      HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      for (int k = 0; k < kGraphSteps; ++k) {
+        enqueue_step();
+        dd_->swap(); // pointers only; the captured kernels carry the buffers of each step
+      }
+      HIP_CHECK(hipStreamEndCapture(s, &g));
+      HIP_CHECK(hipGraphInstantiate(&graphBlock_[p], g, nullptr, nullptr, 0));
+      HIP_CHECK(hipGraphDestroy(g));
+    } else {
+      for (int k = 0; k < kGraphSteps; ++k) dd_->swap();
+    }
+    HIP_CHECK(hipGraphLaunch(graphBlock_[p], s));
+    steps_ += kGraphSteps;
+    iters -= kGraphSteps;
+  }
+  for (int i = 0; i < iters; ++i) step();
+}
+
 void StencilModel::enqueue_step() {
   auto &doms = dd_->domains();
   const bool device = !compute_.empty();
+  if (forward_) {
+    // step i of a sub-domain overwrites halos its neighbours read in step i-1 and reads halos they write in step
+    // i-1: with several sub-domains every stream first joins the previous step of all the others
+    const bool multi = doms.size() > 1;
+    for (size_t di = 0; di < doms.size(); ++di) {
+      hipStream_t s = compute_[di].get();
+      if (multi)
+        for (size_t dj = 0; dj < doms.size(); ++dj)
+          if (dj != di) stepDone_[dj].wait_on(s);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q) {
+        const HaloForwarder *f = fwd_[di][size_t(q)].get();
+        stencil7_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, cfg_.tune, f);
+        f->forward_rest(doms[di].parity(), s);
+      }
+    }
+    if (multi)
+      for (size_t di = 0; di < doms.size(); ++di) stepDone_[di].record(compute_[di]);
+    return;
+  }
   if (overlap_) {
     // exchange first: its pack/send kernels (high-priority comm stream) get CUs before the interior sweep fills them
     dd_->exchange_async();

@@ -21,7 +21,7 @@ class StencilModel:
     def __init__(self, size, kind=_C.StencilKind.Jacobi, radius: int = 1, all_directions: bool = False,
                  quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
                  placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, auto_overlap: bool = True,
-                 use_graph: bool = True, backend=None,
+                 use_graph: bool = True, forward: bool = False, backend=None,
                  tune: _C.StencilTune | None = None, group=None):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
@@ -37,6 +37,7 @@ class StencilModel:
         cfg.overlap = overlap
         cfg.auto_overlap = auto_overlap
         cfg.use_graph = use_graph
+        cfg.forward = forward
         if backend is not None:
             cfg.backend = backend
         if tune is not None:
@@ -65,6 +66,10 @@ class StencilModel:
 
     def overlapping(self) -> bool:
         return self._m.overlapping()
+
+    def forwarding(self) -> bool:
+        """True when the stencil kernels write the neighbours' halos directly (in-process exchanges only)."""
+        return self._m.forwarding()
 
     def cells(self) -> int:
         return self._m.cells()

@@ -77,16 +77,81 @@ def _gather(model):
 @pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("variant", [0, 1])
 def test_jacobi_device_matches_oracle(st, size, gpus, overlap, variant):
+    """exchange + stencil pipelines (forwarding off): overlap (interior/exchange/exterior) and whole-region."""
     t = st.StencilTune()
     t.variant = variant
-    m = st.Jacobi3D(size, gpus=gpus, overlap=overlap, auto_overlap=False, tune=t)
+    m = st.Jacobi3D(size, gpus=gpus, overlap=overlap, auto_overlap=False, tune=t, forward=False)
     m.init()
+    assert not m.forwarding()
     u = _gather(m)
     for _ in range(3):
         m.step()
         u = jacobi_step_reference(u)
     m.synchronize()
     assert torch.equal(_gather(m), u)
+
+
+def _check_halos(model, g, radius_dirs):
+    """Every halo cell in a direction with a message holds its periodic image of the global field g."""
+    from stencil2_amd.ops import periodic_gather
+    dd = model.domain
+    bad = 0
+    for di in range(dd.num_domains()):
+        d = dd.domain(di)
+        o, raw = d.accessor_origin(), d.raw_size()
+        full = model.field(di).cpu()
+        want = periodic_gather(g, (o.x, o.y, o.z), (raw.x, raw.y, raw.z))
+        cr = d.get_compute_region()
+        gz = torch.arange(raw.z).view(-1, 1, 1) + o.z
+        gy = torch.arange(raw.y).view(1, -1, 1) + o.y
+        gx = torch.arange(raw.x).view(1, 1, -1) + o.x
+        dz = (gz >= cr.hi.z).long() - (gz < cr.lo.z).long()
+        dy = (gy >= cr.hi.y).long() - (gy < cr.lo.y).long()
+        dx = (gx >= cr.hi.x).long() - (gx < cr.lo.x).long()
+        dz, dy, dx = torch.broadcast_tensors(dz, dy, dx)
+        mask = torch.zeros(full.shape, dtype=torch.bool)
+        for (xx, yy, zz) in radius_dirs:
+            mask |= (dx == xx) & (dy == yy) & (dz == zz)
+        bad += int((full[mask] != want[mask]).sum())
+    return bad
+
+
+_FACES = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
+_ALL26 = [(x, y, z) for z in (-1, 0, 1) for y in (-1, 0, 1) for x in (-1, 0, 1) if (x, y, z) != (0, 0, 0)]
+
+
+@pytest.mark.parametrize("size", [(32, 32, 32), (67, 45, 33), (130, 64, 40)])
+@pytest.mark.parametrize("gpus,methods", [([0], "All"), ([0, 0], "All"), ([0, 0, 0, 0], "All"), ([0, 0], "PeerCopy")])
+@pytest.mark.parametrize("fp64", [False, True])
+def test_jacobi_forwarding_matches_oracle(st, size, gpus, methods, fp64):
+    """Halo forwarding: the stencil kernel writes the receivers' halos (Kernel/PeerCopy targets); results stay
+    bitwise equal to the oracle and the new curr halos are valid after every step without any exchange()."""
+    m = st.Jacobi3D(size, gpus=gpus, fp64=fp64, methods=getattr(st.MethodFlags, methods), forward=True)
+    m.init()
+    assert m.forwarding()
+    u = _gather(m)
+    for _ in range(3):
+        m.step()
+        u = jacobi_step_reference(u)
+        m.synchronize()
+        assert torch.equal(_gather(m), u)
+        assert _check_halos(m, u, _FACES) == 0
+
+
+@pytest.mark.parametrize("gpus", [[0], [0, 0, 0]])
+def test_astaroth_forwarding_26dirs(st, gpus):
+    """radius 3 in all 26 directions: edge and corner halos are forwarded too."""
+    L = (48, 36, 30)
+    m = st.AstarothSim(L, quantities=2, gpus=gpus, forward=True)
+    m.init()
+    assert m.forwarding()
+    u = _gather(m)
+    for _ in range(2):
+        m.step()
+        u = astaroth_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+    assert _check_halos(m, u, _ALL26) == 0
 
 
 def test_jacobi_fp64_device(st):
@@ -102,7 +167,7 @@ def test_jacobi_fp64_device(st):
 
 def test_astaroth_device_matches_oracle(st):
     L = (40, 34, 28)
-    m = st.AstarothSim(L, quantities=2, gpus=[0, 0])
+    m = st.AstarothSim(L, quantities=2, gpus=[0, 0], forward=False)
     m.init()
     u = _gather(m)
     assert torch.allclose(u, astaroth_init_reference(L, 3, 10.0), atol=1e-6)
