@@ -2,8 +2,11 @@
 // GPU topology: distance/bandwidth between devices and peer-access management.
 // Parity: reference include/stencil/gpu_topology.hpp + src/gpu_topology.cpp:17-139
 //   (NVML distance: same 0.1, NVLink 1, PCIe levels 2-7; bandwidth = 1/distance; cached enable_peer / peer).
-// MI355X: the link type and hop count come from hipExtGetLinkTypeAndHopCount (xGMI vs PCIe), so a fully
-// connected 8-GPU xGMI node is a uniform mesh: distance 1.0 for every pair, 0.1 for self.
+// MI355X: the link type, hop count, link weight and min/max link bandwidth come from amd-smi (libamd_smi, loaded
+// at run time, devices matched by PCI address; the analogue of the reference's NVML queries), falling back to
+// hipExtGetLinkTypeAndHopCount. A fully connected 8-GPU xGMI node is a uniform mesh: distance 1.0 for every pair,
+// 0.1 for self.
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -26,8 +29,15 @@ struct LinkInfo {
   std::string type; // "self", "xgmi", "pcie", "unknown"
   int hops;
   double distance;
+  int64_t weight = -1;                 // amd-smi link weight (-1: unavailable)
+  int64_t minBwMBs = -1, maxBwMBs = -1; // amd-smi min/max io-link bandwidth (MB/s, -1: unavailable)
+  std::string source;                  // "amd-smi", "hip" or "none"
 };
 std::vector<LinkInfo> links();
+// NUMA node of a device (amd-smi), -1 if unknown; used to pin host-staged buffers / ranks
+int numa_node(int dev);
+// whether the amd-smi library was found and initialised
+bool smi_available();
 
 } // namespace gpu_topo
 } // namespace stencil

@@ -352,9 +352,13 @@ PYBIND11_MODULE(_C, m) {
     py::list l;
     for (auto &li : gpu_topo::links())
       l.append(py::dict(py::arg("src") = li.src, py::arg("dst") = li.dst, py::arg("type") = li.type,
-                        py::arg("hops") = li.hops, py::arg("distance") = li.distance));
+                        py::arg("hops") = li.hops, py::arg("distance") = li.distance, py::arg("weight") = li.weight,
+                        py::arg("min_bw_mbs") = li.minBwMBs, py::arg("max_bw_mbs") = li.maxBwMBs,
+                        py::arg("source") = li.source));
     return l;
   });
+  m.def("gpu_numa_node", &gpu_topo::numa_node);
+  m.def("amdsmi_available", &gpu_topo::smi_available);
 
   // ---------------- statistics ----------------
   py::class_<Statistics>(m, "Statistics")

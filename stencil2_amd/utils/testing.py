@@ -15,16 +15,16 @@ def encode(gz, gy, gx):
     return gx + 1000 * gy + 1000000 * gz
 
 
-def fill_coords(dd, q: int, poison: int = POISON):
-    """Poison whole allocations (curr and next), then write encode(global coord) into every interior cell."""
+def fill_coords(dd, q: int, poison: int = POISON, offset: int = 0):
+    """Poison whole allocations (curr and next), then write encode(global coord) + offset into every interior cell."""
     for di in range(dd.num_domains()):
         for curr in (True, False):
             t = dd.curr(di, q) if curr else dd.next(di, q)
             t.fill_(poison)
-    dd.fill_from_global(q, lambda z, y, x: encode(z, y, x))
+    dd.fill_from_global(q, lambda z, y, x: encode(z, y, x) + offset)
 
 
-def expected_full(dd, di: int, radius, poison: int = POISON, boundary=None) -> torch.Tensor:
+def expected_full(dd, di: int, radius, poison: int = POISON, boundary=None, offset: int = 0) -> torch.Tensor:
     d = dd.domain(di)
     org, raw, sz = d.accessor_origin(), d.raw_size(), d.size()
     cr = d.get_compute_region()
@@ -36,7 +36,7 @@ def expected_full(dd, di: int, radius, poison: int = POISON, boundary=None) -> t
     dy = (gy >= cr.hi.y).long() - (gy < cr.lo.y).long()
     dx = (gx >= cr.hi.x).long() - (gx < cr.lo.x).long()
     dz, dy, dx = torch.broadcast_tensors(dz, dy, dx)
-    want = encode(gz % Z, gy % Y, gx % X).expand(raw.z, raw.y, raw.x).clone()
+    want = (encode(gz % Z, gy % Y, gx % X) + offset).expand(raw.z, raw.y, raw.x).clone()
     filled = torch.zeros_like(want, dtype=torch.bool)
     for zz in (-1, 0, 1):
         for yy in (-1, 0, 1):
@@ -57,11 +57,15 @@ def expected_full(dd, di: int, radius, poison: int = POISON, boundary=None) -> t
     return want
 
 
-def check_exchange(dd, q: int, radius, poison: int = POISON, boundary=None):
+def check_exchange(dd, q: int, radius, poison: int = POISON, boundary=None, offset: int = 0):
     """Return the number of wrong cells over every local sub-domain."""
     bad = 0
     for di in range(dd.num_domains()):
-        got = dd.curr(di, q).cpu().long()
-        want = expected_full(dd, di, radius, poison, boundary)
+        t = dd.curr(di, q).cpu()
+        if t.is_floating_point():
+            # NaN poison (race canary) must never survive in a cell that should have been written
+            t = torch.nan_to_num(t, nan=float(poison))
+        got = t.long()
+        want = expected_full(dd, di, radius, poison, boundary, offset)
         bad += int((got != want).sum())
     return bad

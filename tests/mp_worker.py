@@ -41,6 +41,41 @@ def scenario_exchange(backend, methods, radius_name, size):
     return bad
 
 
+def scenario_canary(backend, methods, radius_name, size, iters=12):
+    """Race canary: every iteration writes iteration-tagged interiors, poisons every halo with NaN
+    (float) / -1 (int), then exchanges back to back with no barrier between ranks. A halo from another iteration
+    (missing credit: reference tx_cuda.cuh:270-283), a surviving poison cell or a touched interior cell fails."""
+    g = st.init_process_group()
+    radius = {"r1": st.Radius.constant(1), "fec": st.Radius.face_edge_corner(2, 1, 1)}[radius_name]
+    dd = st.DistributedDomain(*size, group=g)
+    dd.set_backend(backend)
+    dd.set_radius(radius)
+    if backend == st.Backend.Device:
+        dd.set_gpus([0])
+    dd.set_methods(methods)
+    q = dd.add_data("c", torch.int64)
+    qf = dd.add_data("f", torch.float64)
+    dd.realize()
+    bad = 0
+    for it in range(iters):
+        off = it * 10_000_000
+        fill_coords(dd, q, offset=off)
+        fill_coords(dd, qf, poison=-1, offset=off)
+        for di in range(dd.num_domains()):  # NaN-poison the float halos (interior stays)
+            t = dd.curr(di, qf)
+            inner = dd.curr_interior(di, qf).clone()
+            t.fill_(float("nan"))
+            dd.curr_interior(di, qf).copy_(inner)
+        before = [dd.curr_interior(di, q).clone() for di in range(dd.num_domains())]
+        dd.exchange()
+        bad += check_exchange(dd, q, radius, offset=off) + check_exchange(dd, qf, radius, offset=off)
+        for di in range(dd.num_domains()):
+            bad += int((dd.curr_interior(di, q) != before[di]).sum())
+        dd.swap()
+    print(f"rank {g.rank()} canary bad {bad}")
+    return bad
+
+
 def scenario_jacobi(backend, methods, size):
     g = st.init_process_group()
     gpus = [0] if backend == st.Backend.Device else [0]
@@ -70,6 +105,8 @@ def main():
         methods = methods | getattr(st.MethodFlags, name)
     if sc == "exchange":
         bad = scenario_exchange(backend, methods, sys.argv[2], tuple(int(v) for v in sys.argv[3].split(",")))
+    elif sc == "canary":
+        bad = scenario_canary(backend, methods, sys.argv[2], tuple(int(v) for v in sys.argv[3].split(",")))
     elif sc == "jacobi":
         bad = scenario_jacobi(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     else:

@@ -193,6 +193,16 @@ def test_colocated_ipc_jacobi_two_ranks():
         assert rc == 0, out[-3000:]
 
 
+@pytest.mark.parametrize("methods", ["Colocated|Kernel", "Staged|Kernel"])
+def test_race_canary_two_ranks_one_gpu(methods):
+    """Race canary over HIP IPC (double-buffered inboxes + credits) and the staged path, with jitter."""
+    outs = run_ranks(2, WORKER, ["canary", "fec", "20,12,10"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20",
+                                "STENCIL_JITTER_US": "200"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
 def test_staged_two_ranks_one_gpu():
     outs = run_ranks(2, WORKER, ["exchange", "r1", "16,12,10"], env_extra={"MP_DEVICE": "1", "MP_METHODS": "Staged|Kernel"})
     for rc, out in outs:
@@ -203,3 +213,18 @@ def test_smoke_entry():
     import __graft_entry__ as g
 
     g.smoke()
+
+
+def test_topology_links(st):
+    """GPU topology (reference gpu_topology.cpp NVML distance): amd-smi when available, HIP link query otherwise."""
+    from stencil2_amd import _C
+    links = _C.gpu_links()
+    n = st.device_count()
+    assert len(links) == n * n
+    for li in links:
+        if li["src"] == li["dst"]:
+            assert li["type"] == "self" and li["distance"] == pytest.approx(0.1)
+        else:
+            assert li["source"] in ("amd-smi", "hip", "none") and li["distance"] >= 0.5
+    assert _C.gpu_numa_node(0) >= -1
+    print("amd-smi:", _C.amdsmi_available(), "numa(0):", _C.gpu_numa_node(0))

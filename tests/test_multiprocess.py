@@ -29,3 +29,9 @@ def test_fake_two_nodes_nodeaware():
 
 def test_jacobi_ranks_match_oracle():
     _ok(run_ranks(3, WORKER, ["jacobi", "15,11,9"]))
+
+
+@pytest.mark.parametrize("n,radius", [(2, "r1"), (3, "fec")])
+def test_race_canary_staged(n, radius):
+    """NaN-poisoned halos, iteration-tagged interiors, back-to-back exchanges with random transport jitter."""
+    _ok(run_ranks(n, WORKER, ["canary", radius, "14,10,9"], env_extra={"STENCIL_JITTER_US": "300"}))
