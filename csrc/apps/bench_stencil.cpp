@@ -110,12 +110,16 @@ int main(int argc, char **argv) {
     }
   }
   struct Cfg {
-    int variant, ty, zc;
+    int variant, ty, zc, nw = 8;
   };
   std::vector<Cfg> cfgs;
   if (only.empty() || only == "lds")
     for (int ty : {2, 4, 8})
       for (int zc : {0, 8, 16, 32, 64}) cfgs.push_back({0, ty, zc});
+  if (only.empty() || only == "deep" || only == "lds")
+    for (int pf : {2, 3})
+      for (int nw : {4, 8, 16})
+        for (int zc : {0, 32, 64}) cfgs.push_back({pf, 2, zc, nw});
   if (only.empty() || only == "reg")
     for (int ty : {4, 8})
       for (int zc : {0, 16, 32}) cfgs.push_back({1, ty, zc});
@@ -171,9 +175,10 @@ int main(int argc, char **argv) {
     t.variant = c.variant;
     t.ty = c.ty;
     t.zchunk = c.zc;
+    t.nw = c.nw;
     const double us = timeit([&] { stencil7_apply(ld, 0, reg, StencilKind::Jacobi, sph, s, t); });
-    std::printf("stencil7,%d,%d,%d,%.2f,%.1f,%.3f\n", c.variant, c.ty, c.zc, us, cells / us / 1e3,
-                cells * 8 / us / 1e6);
+    std::printf("stencil7,%d,%d,%d,%.2f,%.1f,%.3f,nw%d\n", c.variant, c.ty, c.zc, us, cells / us / 1e3,
+                cells * 8 / us / 1e6, c.nw);
   }
   return 0;
 }

@@ -537,7 +537,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("zchunk", &StencilTune::zchunk)
       .def_readwrite("xcd_remap", &StencilTune::xcdRemap)
       .def_readwrite("nontemporal", &StencilTune::nontemporal)
-      .def_readwrite("alternate_z", &StencilTune::alternateZ);
+      .def_readwrite("alternate_z", &StencilTune::alternateZ)
+      .def_readwrite("nw", &StencilTune::nw);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())
       .def_readwrite("size", &StencilModelConfig::size)

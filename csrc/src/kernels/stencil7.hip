@@ -48,6 +48,7 @@ template <typename T> struct StencilArgs {
   int x0;                           // raw x of chunk 0 (16-B aligned in memory)
   int nchunks;                      // chunks covering [x0, hix)
   int rawYm1;                       // clamp for row loads
+  int rawZm1;                       // clamp for the deep z prefetch
   int zc;                           // planes per block
   int gx, gy, gz;                   // logical grid
   // spheres, raw coordinates
@@ -262,7 +263,9 @@ __device__ __forceinline__ void forward_edges(const StencilArgs<T> &a, T *dp, co
 // v3: block = NW waves stacked in y, TY rows per wave, one shared 16-B x-chunk column of 64 lanes. The y-halo rows of
 // every wave come from its neighbours through LDS (double-buffered by z parity, one barrier per z step), so HBM
 // reads per output row drop from (TY+2)/TY to (NW*TY+2)/(NW*TY).
-template <typename T, int TY, int NW, int KIND, bool NT, bool REMAP, bool FWD>
+// PF = z-planes of lookahead: 1 loads plane z+1 while computing plane z (the loads are consumed in the same step,
+// so only other waves hide their latency); 2 loads plane z+2, so every load has a whole step to land.
+template <typename T, int TY, int NW, int KIND, bool NT, bool REMAP, bool FWD, int PF = 1>
 __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void stencil7_lds_kernel(StencilArgs<T> a) {
   using VT = typename Vec16<T>::type;
   constexpr int V = Vec16<T>::N;
@@ -348,6 +351,11 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
   VT prev[TY], cur[TY], nxt[TY];
   T curL[TY], curR[TY], nxtL[TY], nxtR[TY];
   VT haloN; // block halo row of the next plane (wave 0: above, wave NW-1: below)
+  // PF >= 2: planes z+2 .. z+PF in flight (fut[k] = plane z+(k+2)dz)
+  constexpr int NF = PF > 1 ? PF - 1 : 1;
+  VT fut[NF][TY], futH[NF];
+  T futL[NF][TY], futR[NF][TY];
+  auto zclamp = [&](int zz) { return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz); };
 #pragma unroll
   for (int i = 0; i < TY; ++i) prev[i] = ld(rowp(ybase + i, z0 - dz));
 #pragma unroll
@@ -361,24 +369,63 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
   if (w == NW - 1) lds[0][2 * NW + 1][lane] = ld(rowp(yblk + NW * TY, z0));
   lds[0][slotTop][lane] = cur[0];
   lds[0][slotBot][lane] = cur[TY - 1];
+  if constexpr (PF >= 2) {
+    const int z1 = zclamp(z0 + dz);
+#pragma unroll
+    for (int i = 0; i < TY; ++i) {
+      const T *p = rowp(ybase + i, z1);
+      nxt[i] = ld(p);
+      nxtL[i] = edgeL ? p[-1] : T(0);
+      nxtR[i] = edgeR ? p[V] : T(0);
+    }
+    if (w == 0) haloN = ld(rowp(yblk - 1, z1));
+    if (w == NW - 1) haloN = ld(rowp(yblk + NW * TY, z1));
+#pragma unroll
+    for (int k = 0; k + 1 < NF; ++k) {
+      const int zk = zclamp(z0 + (k + 2) * dz);
+#pragma unroll
+      for (int i = 0; i < TY; ++i) {
+        const T *p = rowp(ybase + i, zk);
+        fut[k][i] = ld(p);
+        futL[k][i] = edgeL ? p[-1] : T(0);
+        futR[k][i] = edgeR ? p[V] : T(0);
+      }
+      if (w == 0) futH[k] = ld(rowp(yblk - 1, zk));
+      if (w == NW - 1) futH[k] = ld(rowp(yblk + NW * TY, zk));
+    }
+  }
   __syncthreads();
 
   const int r1sq = a.r1sq;
   int buf = 0;
   int z = z0;
   for (int step = 0; step < nzs; ++step, z += dz) {
-    const int zn = z + dz;
+    if constexpr (PF == 1) {
+      const int zn = z + dz;
 #pragma unroll
-    for (int i = 0; i < TY; ++i) nxt[i] = ld(rowp(ybase + i, zn));
-    if (w == 0) haloN = ld(rowp(yblk - 1, zn));
-    if (w == NW - 1) haloN = ld(rowp(yblk + NW * TY, zn));
-    if (step + 1 < nzs) {
+      for (int i = 0; i < TY; ++i) nxt[i] = ld(rowp(ybase + i, zn));
+      if (w == 0) haloN = ld(rowp(yblk - 1, zn));
+      if (w == NW - 1) haloN = ld(rowp(yblk + NW * TY, zn));
+      if (step + 1 < nzs) {
+#pragma unroll
+        for (int i = 0; i < TY; ++i) {
+          const T *p = rowp(ybase + i, zn);
+          nxtL[i] = edgeL ? p[-1] : T(0);
+          nxtR[i] = edgeR ? p[V] : T(0);
+        }
+      }
+    } else {
+      // plane z+PF (clamped into the allocation at the ends of the march; those values are never used)
+      const int zf = zclamp(z + PF * dz);
 #pragma unroll
       for (int i = 0; i < TY; ++i) {
-        const T *p = rowp(ybase + i, zn);
-        nxtL[i] = edgeL ? p[-1] : T(0);
-        nxtR[i] = edgeR ? p[V] : T(0);
+        const T *p = rowp(ybase + i, zf);
+        fut[NF - 1][i] = ld(p);
+        futL[NF - 1][i] = edgeL ? p[-1] : T(0);
+        futR[NF - 1][i] = edgeR ? p[V] : T(0);
       }
+      if (w == 0) futH[NF - 1] = ld(rowp(yblk - 1, zf));
+      if (w == NW - 1) futH[NF - 1] = ld(rowp(yblk + NW * TY, zf));
     }
     const VT above = lds[buf][slotAbove][lane];
     const VT below = lds[buf][slotBelow][lane];
@@ -515,6 +562,22 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
       cur[i] = nxt[i];
       curL[i] = nxtL[i];
       curR[i] = nxtR[i];
+      if constexpr (PF >= 2) {
+        nxt[i] = fut[0][i];
+        nxtL[i] = futL[0][i];
+        nxtR[i] = futR[0][i];
+#pragma unroll
+        for (int k = 0; k + 1 < NF; ++k) {
+          fut[k][i] = fut[k + 1][i];
+          futL[k][i] = futL[k + 1][i];
+          futR[k][i] = futR[k + 1][i];
+        }
+      }
+    }
+    if constexpr (PF >= 2) {
+      haloN = futH[0];
+#pragma unroll
+      for (int k = 0; k + 1 < NF; ++k) futH[k] = futH[k + 1];
     }
   }
 }
@@ -735,6 +798,7 @@ static StencilArgs<T> make_args(const LocalDomain &dom, int64_t qi, const Rect3 
   a.hiy = int(r.hi.y);
   a.hiz = int(r.hi.z);
   a.rawYm1 = int(dom.raw_size().y - 1);
+  a.rawZm1 = int(dom.raw_size().z - 1);
   if (kind == StencilKind::Jacobi && sph.enabled) {
     a.hx = int(sph.hot.x - org.x);
     a.hy = int(sph.hot.y - org.y);
@@ -844,9 +908,12 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
     // end (512^3, 2 rows/lane: 1024 blocks at 768 resident ran 20% slower than 768 or 512). z-chunks >= 16
     // planes (the warm-up planes of neighbouring chunks are shared, see kernel).
     const int64_t cols = int64_t(a.gx) * a.gy;
-    const int64_t targetBlocks = resident_blocks(a.fmask ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>
-                                                         : (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false>,
-                                                 64 * NW);
+    const void *kern = a.fmask ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>
+                       : tune.variant == 2 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 2>
+                       : tune.variant == 3 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 3>
+                       : tune.variant == 4 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 4>
+                                           : (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false>;
+    const int64_t targetBlocks = resident_blocks(kern, 64 * NW);
     const int64_t nzc = std::max<int64_t>(1, targetBlocks / cols);
     zc = int(std::max<int64_t>(16, (nz + nzc - 1) / nzc));
   }
@@ -856,6 +923,12 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
   const dim3 block(64, NW);
   if (a.fmask)
     hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>), dim3(blocks), block, 0, stream, a);
+  else if (tune.variant == 2)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 2>), dim3(blocks), block, 0, stream, a);
+  else if (tune.variant == 3)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 3>), dim3(blocks), block, 0, stream, a);
+  else if (tune.variant == 4)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 4>), dim3(blocks), block, 0, stream, a);
   else if (!tune.nontemporal)
     hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, false, true, false>), dim3(blocks), block, 0, stream, a);
   else if (tune.xcdRemap)
@@ -908,7 +981,17 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
       else
         launch_fast<T, 8, KIND>(a, tune, stream);
     } else {
-      if (tune.ty == 8)
+      if (tune.variant >= 2) {
+        // deep lookahead keeps PF planes of rows in registers: 1-2 rows per lane only
+        if (tune.ty == 1)
+          launch_lds<T, 1, 8, KIND>(a, tune, stream);
+        else if (tune.nw == 4)
+          launch_lds<T, 2, 4, KIND>(a, tune, stream);
+        else if (tune.nw == 16)
+          launch_lds<T, 2, 16, KIND>(a, tune, stream);
+        else
+          launch_lds<T, 2, 8, KIND>(a, tune, stream);
+      } else if (tune.ty == 8)
         launch_lds<T, 8, 4, KIND>(a, tune, stream);
       else if (tune.ty == 2)
         launch_lds<T, 2, 8, KIND>(a, tune, stream);

@@ -75,7 +75,7 @@ def _gather(model):
 @pytest.mark.parametrize("size", [(32, 32, 32), (67, 45, 33), (130, 64, 40)])
 @pytest.mark.parametrize("gpus", [[0], [0, 0]])
 @pytest.mark.parametrize("overlap", [True, False])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_jacobi_device_matches_oracle(st, size, gpus, overlap, variant):
     """exchange + stencil pipelines (forwarding off): overlap (interior/exchange/exterior) and whole-region."""
     t = st.StencilTune()
