@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--nt", type=int, default=1, help="non-temporal stencil stores")
     ap.add_argument("--altz", type=int, default=1, help="alternate the z-march direction every step")
     ap.add_argument("--ty", type=int, default=2, help="rows per lane of the stencil kernel (2/4/8)")
+    ap.add_argument("--nw", type=int, default=8, help="waves per block of the stencil kernel")
+    ap.add_argument("--temporal", type=int, default=2,
+                    help="steps fused per sweep: 2 = temporal blocking (one depth-2 halo exchange + one fused "
+                         "S(S(u)) sweep per two steps, bitwise equal to single steps), 1 = one exchange + sweep per step")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU)")
     args = ap.parse_args()
@@ -77,9 +81,10 @@ def main():
     tune.nontemporal = bool(args.nt)
     tune.alternate_z = bool(args.altz)
     tune.ty = args.ty
+    tune.nw = args.nw
     overlap = not args.no_overlap and args.overlap != "off"
     model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=overlap,
-                        auto_overlap=args.overlap == "auto", tune=tune, group=pg)
+                        auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg)
     model.init()
     model.run(args.warmup)
     model.synchronize()
@@ -132,7 +137,7 @@ def main():
                        "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
                        "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods),
                        "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
-                       "ty": args.ty},
+                       "ty": args.ty, "nw": args.nw, "temporal": model.temporal_blocking() and 2 or 1},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
                       "gcells_per_gpu": round(gcells / n, 3)},

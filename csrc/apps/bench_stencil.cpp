@@ -169,6 +169,39 @@ int main(int argc, char **argv) {
       std::printf("%s,0,2,%d,%.2f,%.1f,%.3f\n", names[mode], zc, us, cells / us / 1e3, cells * 8 / us / 1e6);
     }
   }
+  if (only == "one") {
+    // one launch of each default kernel (single step v2, fused pair) for counter collection
+    StencilTune t;
+    timeit([&] { stencil7_apply(ld, 0, reg, StencilKind::Jacobi, sph, s, t); });
+    LocalDomain l2(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
+    l2.set_radius(Radius::face_edge_corner(2, 1, 0));
+    l2.add_data<float>("d");
+    l2.realize();
+    jacobi_init(l2, 0, l2.get_full_region(), s);
+    timeit([&] { stencil7x2_apply(l2, 0, l2.get_compute_region(), StencilKind::Jacobi, sph, s, t); });
+    return 0;
+  }
+  for (int rep = 0; rep < reps; ++rep)
+  if (only.empty() || only == "x2") {
+    // two fused steps per sweep (temporal blocking) on a depth-2 domain; reported per STEP (two steps per launch)
+    LocalDomain l2(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
+    l2.set_radius(Radius::face_edge_corner(2, 1, 0));
+    l2.add_data<float>("d");
+    l2.realize();
+    const Rect3 reg2 = l2.get_compute_region();
+    jacobi_init(l2, 0, l2.get_full_region(), s);
+    s.sync();
+    for (int shape = 0; shape < 4; ++shape)
+      for (int zc : {0, 32, 64}) {
+        StencilTune t;
+        t.x2ty = shape <= 1 ? 1 : 2;
+        t.x2nw = shape == 0 ? 8 : (shape == 1 ? 16 : (shape == 2 ? 4 : 2));
+        t.zchunk = zc;
+        const double us = timeit([&] { stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t); }) / 2;
+        std::printf("stencil7x2,%d,%d,%d,%.2f,%.1f,%.3f,nw%d\n", shape, t.x2ty, zc, us, cells / us / 1e3,
+                    cells * 8 / us / 1e6, t.x2nw);
+      }
+  }
   for (int rep = 0; rep < reps; ++rep)
   for (const Cfg &c : cfgs) {
     StencilTune t;

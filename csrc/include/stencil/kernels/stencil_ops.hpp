@@ -44,6 +44,8 @@ struct StencilTune {
   int ty = 2;     // rows per lane (variant 0: 2/4/8, variant 1: 4/8)
   int zchunk = 0; // planes per block (0 = auto: exactly one round of resident blocks)
   int nw = 8;     // waves per block stacked in y (deep-lookahead variants: 4/8/16)
+  // fused-pair kernel (stencil7x2) shape: rows per lane x waves per block: 1x16 (default), 1x8, 2x4
+  int x2ty = 1, x2nw = 16;
   bool xcdRemap = true;
   bool nontemporal = true;
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous
@@ -100,6 +102,12 @@ private:
 // With `fwd`, region must be the whole compute region and the output is also forwarded into the receivers' halos.
 void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                     hipStream_t stream, const StencilTune &tune = StencilTune(), const HaloForwarder *fwd = nullptr);
+// Two fused steps (temporal blocking): dst(region) = S(S(src)), bitwise equal to two single steps. Needs halos of
+// depth 2 on the faces and 1 on the edges (Radius::face_edge_corner(2, 1, 0) or more) valid in src, a device
+// fp32/fp64 quantity and the aligned layout (stencil7x2_supported). Reads src once and writes dst once per two steps.
+bool stencil7x2_supported(const LocalDomain &dom, int64_t qi);
+void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
+                      hipStream_t stream, const StencilTune &tune = StencilTune());
 // same for several regions in one call (e.g. the exterior slabs)
 void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
                             const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());

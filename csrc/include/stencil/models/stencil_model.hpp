@@ -39,6 +39,10 @@ struct StencilModelConfig {
   // Off by default: on one MI355X the scattered x-face stores cost the kernel more (~+23 us at 512^3) than the
   // separate copy-plan exchange does (~19 us), see BASELINE.md / bench_stencil.
   bool forward = false;
+  // steps fused per sweep: 2 = temporal blocking (stencil7x2: one depth-2 exchange and one read+write of the field
+  // per two steps, bitwise equal to two single steps); 1 = one exchange + one sweep per step. run(n) advances in
+  // fused pairs (a trailing odd step is a single step); step() is always one step.
+  int temporal = 1;
   bool setBackend = false;
   Backend backend = Backend::Device;
   StencilTune tune;
@@ -66,6 +70,7 @@ public:
   const Spheres &spheres() const { return sph_; }
   bool overlapping() const { return overlap_; }
   bool forwarding() const { return forward_; }
+  bool temporal_blocking() const { return pairs_; }
 
 private:
   StencilModelConfig cfg_;
@@ -78,11 +83,13 @@ private:
   bool overlap_ = true;
   bool graphs_ = false;
   bool forward_ = false;
+  bool pairs_ = false; // temporal blocking active
   std::vector<std::vector<std::unique_ptr<HaloForwarder>>> fwd_; // [domain][quantity]
   std::vector<Event> stepDone_;                                    // forwarding with several sub-domains
   hipGraphExec_t graphExec_[2] = {nullptr, nullptr};
   hipGraphExec_t graphBlock_[2] = {nullptr, nullptr}; // kGraphSteps steps starting at parity p
-  void enqueue_step();
+  void enqueue_step(int k = 1); // k = 1: one step; k = 2: a fused pair (temporal blocking)
+  bool pair_ok() const { return pairs_; }
   int64_t steps_ = 0;
 };
 

@@ -538,7 +538,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("xcd_remap", &StencilTune::xcdRemap)
       .def_readwrite("nontemporal", &StencilTune::nontemporal)
       .def_readwrite("alternate_z", &StencilTune::alternateZ)
-      .def_readwrite("nw", &StencilTune::nw);
+      .def_readwrite("nw", &StencilTune::nw)
+      .def_readwrite("x2ty", &StencilTune::x2ty)
+      .def_readwrite("x2nw", &StencilTune::x2nw);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())
       .def_readwrite("size", &StencilModelConfig::size)
@@ -554,6 +556,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("auto_overlap", &StencilModelConfig::autoOverlap)
       .def_readwrite("use_graph", &StencilModelConfig::useGraph)
       .def_readwrite("forward", &StencilModelConfig::forward)
+      .def_readwrite("temporal", &StencilModelConfig::temporal)
       .def_property(
           "backend", [](const StencilModelConfig &c) { return c.backend; },
           [](StencilModelConfig &c, Backend b) {
@@ -577,6 +580,7 @@ PYBIND11_MODULE(_C, m) {
       .def("steps_done", &StencilModel::steps_done)
       .def("overlapping", &StencilModel::overlapping)
       .def("forwarding", &StencilModel::forwarding)
+      .def("temporal_blocking", &StencilModel::temporal_blocking)
       .def("compute_stream", [](StencilModel &mdl, size_t di) { return reinterpret_cast<uintptr_t>(mdl.compute_stream(di)); })
       .def("domain",
            [](std::shared_ptr<StencilModel> mdl) {

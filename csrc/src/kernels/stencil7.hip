@@ -8,79 +8,11 @@
 #include <mutex>
 
 #include "stencil/domain/packer.hpp"
+#include "stencil_common.hpp"
 #include "stencil/kernels/stencil_ops.hpp"
 #include "stencil/rt/hip_check.hpp"
 
 namespace stencil {
-
-template <typename T> struct Vec16;
-typedef float nf4 __attribute__((ext_vector_type(4)));
-typedef double nd2 __attribute__((ext_vector_type(2)));
-template <> struct Vec16<float> {
-  using type = float4;
-  using native = nf4;
-  static constexpr int N = 4;
-};
-template <> struct Vec16<double> {
-  using type = double2;
-  using native = nd2;
-  static constexpr int N = 2;
-};
-
-template <typename T> __device__ __forceinline__ T vget(const typename Vec16<T>::type &v, int i);
-template <> __device__ __forceinline__ float vget<float>(const float4 &v, int i) {
-  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
-}
-template <> __device__ __forceinline__ double vget<double>(const double2 &v, int i) { return i == 0 ? v.x : v.y; }
-
-template <typename T> __device__ __forceinline__ T shfl_up1(T v);
-template <typename T> __device__ __forceinline__ T shfl_down1(T v);
-template <> __device__ __forceinline__ float shfl_up1<float>(float v) { return __shfl_up(v, 1, 64); }
-template <> __device__ __forceinline__ float shfl_down1<float>(float v) { return __shfl_down(v, 1, 64); }
-template <> __device__ __forceinline__ double shfl_up1<double>(double v) { return __shfl_up(v, 1, 64); }
-template <> __device__ __forceinline__ double shfl_down1<double>(double v) { return __shfl_down(v, 1, 64); }
-
-template <typename T> struct StencilArgs {
-  const T *src; // raw [0,0,0] of curr
-  T *dst;       // raw [0,0,0] of next
-  int64_t px, pxy;
-  int lox, loy, loz, hix, hiy, hiz; // region, raw coordinates
-  int x0;                           // raw x of chunk 0 (16-B aligned in memory)
-  int nchunks;                      // chunks covering [x0, hix)
-  int rawYm1;                       // clamp for row loads
-  int rawZm1;                       // clamp for the deep z prefetch
-  int zc;                           // planes per block
-  int gx, gy, gz;                   // logical grid
-  // spheres, raw coordinates
-  int hx, hy, hz, cx, cy, cz;
-  int r1sq; // (radius+1)^2, 0 = disabled
-  // halo forwarding (FWD kernels): cells within fwm[a] of the low face send along -a, within fwp[a] of the high
-  // face along +a; the receiving halo cell of direction k = (dx+1) + 3(dy+1) + 9(dz+1) is at (own output address +
-  // fd[k]) for every k set in fmask (receivers with our pitches; the rest is copied after the kernel)
-  int flip; // reverse every block's z-march direction (alternated per step, see StencilTune::alternateZ)
-  int fwm[3], fwp[3];
-  uint32_t fmask;
-  int64_t fd[27];
-};
-
-
-// bijective XCD-aware remap: consecutive logical ids land on the same XCD (blocks b, b+8, ... share one)
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t hw, uint32_t n) {
-  const uint32_t q = n / 8, r = n % 8, xcd = hw % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + hw / 8;
-}
-
-// x / 6 rounded to nearest-even, bit-identical to IEEE division. fp32: two FMAs around the reciprocal (verified
-// exhaustively over all 2^32 inputs for |x| >= 2^-100; the subnormal-result range takes the true division).
-template <typename T> __device__ __forceinline__ T div6(T x) { return x / T(6); }
-template <> __device__ __forceinline__ float div6<float>(float x) {
-  constexpr float c = 1.0f / 6.0f;
-  const float q0 = x * c;
-  const float r = __builtin_fmaf(-q0, 6.0f, x);
-  float q = __builtin_fmaf(r, c, q0);
-  if (__builtin_expect(__builtin_fabsf(x) < 0x1p-100f, 0)) q = x / 6.0f;
-  return q;
-}
 
 // 2.5D z-march. Lane = one 16-B x-chunk; wave = 64 chunks x TY rows; block = 4 waves stacked in y.
 // Per z step a lane issues TY+2 row loads of plane z+1 (plus the two wave-edge scalars), then emits TY rows of
@@ -780,37 +712,6 @@ __global__ __launch_bounds__(256) void stencil7_shell_kernel(StencilArgs<T> a, S
 // ---------------------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------------------
-template <typename T>
-static StencilArgs<T> make_args(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind,
-                                const Spheres &sph) {
-  StencilArgs<T> a{};
-  const Dim3 org = dom.accessor_origin();
-  const Dim3 p = dom.pitch(qi);
-  a.src = static_cast<const T *>(dom.curr_data(qi));
-  a.dst = static_cast<T *>(dom.next_data(qi));
-  a.px = p.x;
-  a.pxy = p.x * p.y;
-  const Rect3 r(region.lo - org, region.hi - org);
-  a.lox = int(r.lo.x);
-  a.loy = int(r.lo.y);
-  a.loz = int(r.lo.z);
-  a.hix = int(r.hi.x);
-  a.hiy = int(r.hi.y);
-  a.hiz = int(r.hi.z);
-  a.rawYm1 = int(dom.raw_size().y - 1);
-  a.rawZm1 = int(dom.raw_size().z - 1);
-  if (kind == StencilKind::Jacobi && sph.enabled) {
-    a.hx = int(sph.hot.x - org.x);
-    a.hy = int(sph.hot.y - org.y);
-    a.hz = int(sph.hot.z - org.z);
-    a.cx = int(sph.cold.x - org.x);
-    a.cy = int(sph.cold.y - org.y);
-    a.cz = int(sph.cold.z - org.z);
-    a.r1sq = int((sph.radius + 1) * (sph.radius + 1));
-  }
-  return a;
-}
-
 template <typename T, int KIND>
 static void host_apply(const LocalDomain &dom, const StencilArgs<T> &a) {
   (void)dom;

@@ -1,5 +1,6 @@
 #include "stencil/models/stencil_model.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "stencil/rt/hip_check.hpp"
@@ -9,13 +10,22 @@ namespace stencil {
 
 StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::ProcGroup> pg) : cfg_(cfg) {
   dd_.reset(new DistributedDomain(cfg.size.x, cfg.size.y, cfg.size.z, pg));
+  Radius r = Radius::constant(0);
   if (cfg.allDirections) {
-    dd_->set_radius(cfg.radius);
+    r = Radius::constant(cfg.radius);
   } else {
-    Radius r = Radius::constant(0);
     r.set_face(cfg.radius);
-    dd_->set_radius(r);
   }
+  if (cfg.temporal >= 2) {
+    // S o S of a 7-point stencil reaches 2 cells along an axis and 1 cell diagonally (edges), never corners
+    for (int i = 0; i < 27; ++i) {
+      const Dim3 d = dir_from_index(i);
+      const int nz = (d.x != 0) + (d.y != 0) + (d.z != 0);
+      if (nz == 1) r.dir(d) = std::max<int64_t>(r.dir(d), 2);
+      if (nz == 2) r.dir(d) = std::max<int64_t>(r.dir(d), 1);
+    }
+  }
+  dd_->set_radius(r);
   dd_->set_methods(cfg.methods);
   dd_->set_placement(cfg.placement);
   if (!cfg.gpus.empty()) dd_->set_gpus(cfg.gpus);
@@ -63,6 +73,10 @@ void StencilModel::init() {
   for (const auto &d : doms0)
     for (int64_t q = 0; q < d.num_data() && forward_; ++q) forward_ = HaloForwarder::supported(d, q);
   if (forward_) overlap_ = false; // the halos travel inside the stencil kernel
+  pairs_ = cfg_.temporal >= 2 && !forward_ && !doms0.empty();
+  for (const auto &d : doms0)
+    for (int64_t q = 0; q < d.num_data() && pairs_; ++q) pairs_ = stencil7x2_supported(d, q);
+  if (pairs_) overlap_ = false; // exchange (depth 2) -> fused pair on the whole region
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
@@ -133,32 +147,56 @@ void StencilModel::step() {
 void StencilModel::run(int iters) {
   TraceRange tr("StencilModel::run");
   auto &doms = dd_->domains();
+  const int per = pairs_ ? 2 : 1; // steps per enqueued sweep
+  const int sweeps = kGraphSteps / per;  // sweeps per graph block (an even number: the block keeps the parity)
   while (graphs_ && iters >= kGraphSteps) {
     const int p = doms[0].parity();
     hipStream_t s = compute_[0].get();
     if (!graphBlock_[p]) {
       hipGraph_t g = nullptr;
       HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      for (int k = 0; k < kGraphSteps; ++k) {
-        enqueue_step();
-        dd_->swap(); // pointers only; the captured kernels carry the buffers of each step
+      for (int k = 0; k < sweeps; ++k) {
+        enqueue_step(per);
+        dd_->swap(); // pointers only; the captured kernels carry the buffers of each sweep
       }
       HIP_CHECK(hipStreamEndCapture(s, &g));
       HIP_CHECK(hipGraphInstantiate(&graphBlock_[p], g, nullptr, nullptr, 0));
       HIP_CHECK(hipGraphDestroy(g));
     } else {
-      for (int k = 0; k < kGraphSteps; ++k) dd_->swap();
+      for (int k = 0; k < sweeps; ++k) dd_->swap();
     }
     HIP_CHECK(hipGraphLaunch(graphBlock_[p], s));
     steps_ += kGraphSteps;
     iters -= kGraphSteps;
   }
+  const bool device = !compute_.empty();
+  const bool singleStream = device && !overlap_ && doms.size() == 1;
+  while (pairs_ && iters >= 2) {
+    enqueue_step(2);
+    dd_->swap();
+    if (device && !singleStream)
+      for (size_t di = 0; di < doms.size(); ++di) dd_->record_ready(di, compute_[di]);
+    steps_ += 2;
+    iters -= 2;
+  }
   for (int i = 0; i < iters; ++i) step();
 }
 
-void StencilModel::enqueue_step() {
+void StencilModel::enqueue_step(int k) {
   auto &doms = dd_->domains();
   const bool device = !compute_.empty();
+  if (k == 2) {
+    // temporal blocking: one depth-2 exchange, then S o S on every sub-domain
+    const bool single = device && doms.size() == 1;
+    dd_->exchange_async(single ? compute_[0].get() : nullptr);
+    for (size_t di = 0; di < doms.size(); ++di) {
+      hipStream_t s = device ? compute_[di].get() : nullptr;
+      if (!single) dd_->wait_exchange(di, s);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7x2_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, cfg_.tune);
+    }
+    return;
+  }
   if (forward_) {
     // step i of a sub-domain overwrites halos its neighbours read in step i-1 and reads halos they write in step
     // i-1: with several sub-domains every stream first joins the previous step of all the others

@@ -21,7 +21,7 @@ class StencilModel:
     def __init__(self, size, kind=_C.StencilKind.Jacobi, radius: int = 1, all_directions: bool = False,
                  quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
                  placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, auto_overlap: bool = True,
-                 use_graph: bool = True, forward: bool = False, backend=None,
+                 use_graph: bool = True, forward: bool = False, temporal: int = 1, backend=None,
                  tune: _C.StencilTune | None = None, group=None):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
@@ -38,6 +38,7 @@ class StencilModel:
         cfg.auto_overlap = auto_overlap
         cfg.use_graph = use_graph
         cfg.forward = forward
+        cfg.temporal = temporal
         if backend is not None:
             cfg.backend = backend
         if tune is not None:
@@ -66,6 +67,10 @@ class StencilModel:
 
     def overlapping(self) -> bool:
         return self._m.overlapping()
+
+    def temporal_blocking(self) -> bool:
+        """True when run() advances in fused pairs of steps (stencil7x2, one depth-2 exchange per pair)."""
+        return self._m.temporal_blocking()
 
     def forwarding(self) -> bool:
         """True when the stencil kernels write the neighbours' halos directly (in-process exchanges only)."""

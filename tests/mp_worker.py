@@ -79,12 +79,16 @@ def scenario_canary(backend, methods, radius_name, size, iters=12):
 def scenario_jacobi(backend, methods, size):
     g = st.init_process_group()
     gpus = [0] if backend == st.Backend.Device else [0]
-    m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g)
+    temporal = int(os.environ.get("MP_TEMPORAL", "1"))
+    m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g, temporal=temporal)
     m.init()
     L = m.domain.size()
     u = torch.full((L.z, L.y, L.x), 0.5)
     for _ in range(3):
         m.step()
+        u = jacobi_step_reference(u)
+    m.run(5)  # fused pairs when temporal blocking is on
+    for _ in range(5):
         u = jacobi_step_reference(u)
     m.synchronize()
     bad = 0

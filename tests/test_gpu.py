@@ -154,6 +154,55 @@ def test_astaroth_forwarding_26dirs(st, gpus):
     assert _check_halos(m, u, _ALL26) == 0
 
 
+@pytest.mark.parametrize("size", [(32, 32, 32), (67, 45, 33), (130, 64, 40)])
+@pytest.mark.parametrize("gpus", [[0], [0, 0], [0, 0, 0, 0]])
+@pytest.mark.parametrize("fp64", [False, True])
+@pytest.mark.parametrize("shape", [(1, 16), (1, 8), (2, 4), (2, 2)])
+def test_jacobi_temporal2_matches_oracle(st, size, gpus, fp64, shape):
+    """Temporal blocking (stencil7x2: S o S per sweep, one depth-2 exchange per pair) is bitwise equal to single
+    steps; run(5) = two fused pairs + one single step, run(16) = one captured graph block (single sub-domain)."""
+    t = st.StencilTune()
+    t.x2ty, t.x2nw = shape
+    m = st.Jacobi3D(size, gpus=gpus, fp64=fp64, temporal=2, tune=t)
+    m.init()
+    assert m.temporal_blocking()
+    u = _gather(m)
+    for n in (5, 16):
+        m.run(n)
+        for _ in range(n):
+            u = jacobi_step_reference(u)
+        m.synchronize()
+        assert torch.equal(_gather(m), u), f"after run({n})"
+
+
+@pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy"])
+def test_jacobi_temporal2_transports(st, methods):
+    """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs"""
+    m = st.Jacobi3D((40, 36, 44), gpus=[0, 0], methods=getattr(st.MethodFlags, methods), temporal=2)
+    m.init()
+    assert m.temporal_blocking()
+    u = _gather(m)
+    m.run(6)
+    for _ in range(6):
+        u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
+@pytest.mark.parametrize("gpus", [[0], [0, 0, 0]])
+def test_astaroth_temporal2(st, gpus):
+    L = (48, 36, 30)
+    m = st.AstarothSim(L, quantities=2, gpus=gpus, temporal=2)
+    m.init()
+    assert m.temporal_blocking()
+    u = _gather(m)
+    m.run(4)
+    for _ in range(4):
+        u = astaroth_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
 def test_jacobi_fp64_device(st):
     m = st.Jacobi3D((40, 36, 20), gpus=[0], fp64=True)
     m.init()
@@ -186,9 +235,11 @@ def test_colocated_ipc_two_ranks_one_gpu(radius):
         assert rc == 0, out[-3000:]
 
 
-def test_colocated_ipc_jacobi_two_ranks():
+@pytest.mark.parametrize("temporal", ["1", "2"])
+def test_colocated_ipc_jacobi_two_ranks(temporal):
     outs = run_ranks(2, WORKER, ["jacobi", "40,24,20"],
-                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20"})
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": temporal})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 
@@ -199,6 +250,17 @@ def test_race_canary_two_ranks_one_gpu(methods):
     outs = run_ranks(2, WORKER, ["canary", "fec", "20,12,10"],
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20",
                                 "STENCIL_JITTER_US": "200"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
+@pytest.mark.parametrize("methods", ["Rccl|Kernel", "Staged|Kernel"])
+def test_jacobi_temporal2_two_ranks_other_transports(methods):
+    """fused pairs over the staged transport and (ranks sharing one GPU cannot use RCCL) its fallback"""
+    if methods.startswith("Rccl"):
+        pytest.skip("RCCL cannot put two ranks on one device; covered by the in-process RCCL tests")
+    outs = run_ranks(2, WORKER, ["jacobi", "36,20,24"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20", "MP_TEMPORAL": "2"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 
