@@ -191,16 +191,17 @@ int main(int argc, char **argv) {
     const Rect3 reg2 = l2.get_compute_region();
     jacobi_init(l2, 0, l2.get_full_region(), s);
     s.sync();
-    for (int shape = 0; shape < 4; ++shape)
-      for (int zc : {0, 32, 64}) {
-        StencilTune t;
-        t.x2ty = shape <= 1 ? 1 : 2;
-        t.x2nw = shape == 0 ? 8 : (shape == 1 ? 16 : (shape == 2 ? 4 : 2));
-        t.zchunk = zc;
-        const double us = timeit([&] { stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t); }) / 2;
-        std::printf("stencil7x2,%d,%d,%d,%.2f,%.1f,%.3f,nw%d\n", shape, t.x2ty, zc, us, cells / us / 1e3,
-                    cells * 8 / us / 1e6, t.x2nw);
-      }
+    for (int nw : {12, 16})
+      for (int pf : {2, 3})
+        for (int zc : {0, 32, 43, 52, 64, 86, 128}) {
+          StencilTune t;
+          t.x2nw = nw;
+          t.x2pf = pf;
+          t.zchunk = zc;
+          const double us = timeit([&] { stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t); }) / 2;
+          std::printf("stencil7x2,%d,%d,%d,%.2f,%.1f,%.3f,nw%d\n", pf, 1, zc, us, cells / us / 1e3, cells * 8 / us / 1e6,
+                      nw);
+        }
   }
   for (int rep = 0; rep < reps; ++rep)
   for (const Cfg &c : cfgs) {

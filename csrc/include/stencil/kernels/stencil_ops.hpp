@@ -44,8 +44,9 @@ struct StencilTune {
   int ty = 2;     // rows per lane (variant 0: 2/4/8, variant 1: 4/8)
   int zchunk = 0; // planes per block (0 = auto: exactly one round of resident blocks)
   int nw = 8;     // waves per block stacked in y (deep-lookahead variants: 4/8/16)
-  // fused-pair kernel (stencil7x2) shape: rows per lane x waves per block: 1x16 (default), 1x8, 2x4
-  int x2ty = 1, x2nw = 16;
+  // fused-pair kernel (stencil7x2): waves per block (8/12/16, one src row each, NW-4 output rows) and planes of
+  // z lookahead (2/3/4)
+  int x2nw = 16, x2pf = 2;
   bool xcdRemap = true;
   bool nontemporal = true;
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous

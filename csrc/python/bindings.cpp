@@ -539,7 +539,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("nontemporal", &StencilTune::nontemporal)
       .def_readwrite("alternate_z", &StencilTune::alternateZ)
       .def_readwrite("nw", &StencilTune::nw)
-      .def_readwrite("x2ty", &StencilTune::x2ty)
+      .def_readwrite("x2pf", &StencilTune::x2pf)
       .def_readwrite("x2nw", &StencilTune::x2nw);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())

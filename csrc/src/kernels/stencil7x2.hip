@@ -5,14 +5,14 @@
 // (faces 2, edges 1: the 25-point footprint of S o S) per two steps instead of two exchanges of depth 1. This is
 // the "halo multiplier" / deep-halo item of the reference's future-work list (README.md:218-220), built for CDNA4:
 //
-//   block  = NW waves stacked in y, TY rows per wave, one 64-lane column of 16-B x-chunks (as stencil7_lds_kernel)
+//   block  = NW waves stacked in y, one src row per wave (the outer 2 rows on each side are a redundant y halo),
+//            one 64-lane column of 16-B x-chunks (as stencil7_lds_kernel)
 //   step t = output plane z (z-march direction dz = +-1):
-//     1. load src plane z+3dz (lookahead)          (rows of this wave + the block-edge waves' halo rows)
-//     2. u1 = S(src) at plane z+dz for own rows    (y-neighbours of the wave's top/bottom rows: LDS; block edges:
-//        plus u1 one cell outside the wave's x range (edge lanes) and, in the block-edge waves, one row outside
-//        the block in y (the block halo u1 row), so S(u1) never needs another block's u1
+//     1. issue the load of src plane z+(2+PF)dz    (PF planes of lookahead in registers)
+//     2. u1 = S(src) at plane z+dz for the wave's row (y-neighbours: adjacent waves through LDS), plus u1 one cell
+//        outside the wave's x range on the edge lanes, so S(u1) never needs another wave's registers
 //     3. u2 = S(u1) at plane z from the register window u1(z-dz), u1(z), u1(z+dz) + LDS y-neighbours
-//     4. publish src/u1 boundary rows for the next step (double-buffered LDS, one barrier per step)
+//     4. publish the src row of plane z+2dz and the u1 row of plane z+dz (double-buffered LDS, one barrier)
 // Summation order and the /6 are the single-step kernel's, and every u1 value is computed exactly as the single
 // step computes it, so S(S(src)) is bitwise equal to two sequential single steps (tests compare with torch).
 #include <hip/hip_runtime.h>
@@ -26,15 +26,22 @@
 
 namespace stencil {
 
-template <typename T, int TY, int NW, int KIND, bool REMAP, int MINW>
-__global__ __launch_bounds__(64 * NW, MINW) void stencil7x2_kernel(StencilArgs<T> a) {
+// Block = NW waves, ONE src row per wave: the block's src rows are [yblk-2, yblk-2+NW); u1 is valid on the inner
+// NW-2 of them and u2 (the output) on the inner NW-4, so the block writes YO = NW-4 rows and every wave runs the
+// same code (the two outer rows on each side are a redundant y halo, re-read from L2 by the neighbouring block).
+// z: the src window holds planes z .. z+(2+PF)dz; the last PF planes are in flight, so a row load is issued PF
+// steps before it is consumed.
+template <typename T, int NW, int PF, int KIND, bool REMAP>
+__global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a) {
   using VT = typename Vec16<T>::type;
   using NV = typename Vec16<T>::native;
   constexpr int V = Vec16<T>::N;
-  static_assert(NW >= 2, "block-edge waves must differ");
-  __shared__ VT cs[2][2 * NW][64];     // src rows of plane z+2dz: wave w's top row at 2w, bottom row at 2w+1
-  __shared__ VT us[2][2 * NW + 2][64]; // u1 rows of plane z+dz: same slots + block halo rows (2NW above, 2NW+1 below)
-  __shared__ T ce[2][2 * NW][2];       // src edge scalars of the published rows: [0] at x-1 (lane 0), [1] at x+V
+  constexpr int YO = NW - 4;
+  constexpr int NC = 3 + PF; // src window planes
+  static_assert(NW > 4, "a block needs more than its 4 halo rows");
+  __shared__ VT cs[2][NW][64]; // src row of every wave, plane z+2dz at publish (= z+dz when read)
+  __shared__ VT us[2][NW][64]; // u1 row of every wave, plane z+dz at publish (= z when read)
+  __shared__ T ce[2][NW][2];   // src edge scalars of the published rows: [0] at x-1 (lane 0), [1] at x+V
 
   const uint32_t nb = uint32_t(a.gx) * a.gy * a.gz;
   const uint32_t lb = REMAP ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
@@ -47,8 +54,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void stencil7x2_kernel(StencilArgs<T
   const bool cvalid = c < a.nchunks;
   const int cl = cvalid ? c : a.nchunks - 1;
   const int xb = a.x0 + cl * V;
-  const int yblk = a.loy + NW * TY * by;
-  const int ybase = yblk + TY * w;
+  const int yblk = a.loy + YO * by; // first output row of the block
+  const int y = yblk - 2 + w;       // this wave's row
   const int zs = a.loz + bz * a.zc;
   const int ze = min(zs + a.zc, a.hiz);
   if (yblk >= a.hiy || zs >= ze) return; // block-uniform
@@ -60,17 +67,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void stencil7x2_kernel(StencilArgs<T
   const bool edgeL = lane == 0;
   const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
   const bool fullX = xb >= a.lox && xb + V <= a.hix;
-  const bool top = w == 0, bot = w == NW - 1;
-  const bool edgeWave = top || bot;
-  const int hy1 = top ? yblk - 1 : yblk + NW * TY;     // block halo row (top: above, bottom: below)
-  const int hy2 = top ? yblk - 2 : yblk + NW * TY + 1; // its outer neighbour
-  const int slotTop = 2 * w, slotBot = 2 * w + 1;
-  const int slotAbove = top ? 0 : 2 * (w - 1) + 1, slotBelow = bot ? 0 : 2 * (w + 1);
+  const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy && cvalid;
+  const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1; // outer waves: garbage u1, never consumed
 
-  auto rowp = [&](int y, int z) -> const T * {
-    y = y < 0 ? 0 : (y > a.rawYm1 ? a.rawYm1 : y);
-    return a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
-  };
+  const int yc = y < 0 ? 0 : (y > a.rawYm1 ? a.rawYm1 : y);
+  const T *rowbase = a.src + int64_t(yc) * a.px + xb;
+  auto zcl = [&](int zz) { return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz); };
+  auto rowp = [&](int zz) -> const T * { return rowbase + int64_t(zcl(zz)) * a.pxy; };
   auto ld = [&](const T *p) -> VT { return *reinterpret_cast<const VT *>(p); };
   auto toVT = [&](const T (&o)[V]) -> VT {
     VT v;
@@ -85,13 +88,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void stencil7x2_kernel(StencilArgs<T
     }
     return v;
   };
-  // Sphere membership of a row (raw y, plane P): the y/z part of both squared distances, computed once per row;
-  // `hit` is false for the ~97% of rows no sphere reaches, so their cells skip the per-cell test (wave-uniform).
+  // sphere membership of the row at plane P: y/z part once per row, per-cell test only for the few hit rows
   struct RowSph {
     int dh, dc;
     bool hit;
   };
-  auto row_sph = [&](int y, int P) -> RowSph {
+  auto row_sph = [&](int P) -> RowSph {
     RowSph r{0, 0, false};
     if (KIND == 0 && a.r1sq > 0) {
       r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void stencil7x2_kernel(StencilArgs<T
     const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
     return hot ? T(1) : (cold ? T(0) : v);
   };
-  // S at the row chunk `cm` (plane P, raw row y): x-neighbours by shuffles (+ the edge scalars at the wave edges)
+  // S at this wave's row chunk `cm`: x-neighbours by shuffles (+ edge scalars at the wave edges)
   auto apply_row = [&](const VT &cm, const VT &up, const VT &dn, const VT &zp, const VT &zm, T eL, T eR,
                        const RowSph &rs, T (&o)[V]) {
     const T sl = shfl_up1<T>(vget<T>(cm, V - 1));
@@ -125,56 +127,33 @@ __global__ __launch_bounds__(64 * NW, MINW) void stencil7x2_kernel(StencilArgs<T
     }
   };
 
-  // ---- register windows (one plane of lookahead: every load has a whole step to land) ----
-  VT C0[TY], C1[TY], C2[TY], C3[TY]; // src own rows, planes z, z+dz, z+2dz, z+3dz (in flight)
-  T C0L[TY], C0R[TY], C1L[TY], C1R[TY], C2L[TY], C2R[TY], C3L[TY], C3R[TY]; // src at x-1 / x+V (edge lanes)
-  T C1LL[TY], C1RR[TY], C2LL[TY], C2RR[TY]; // src at x-2 / x+V+1, planes z+dz, z+2dz (in flight)
-  VT H0, H1, H2, H3;                        // block halo row hy1, planes z .. z+3dz (edge waves)
-  T H1L = T(0), H1R = T(0), H2L = T(0), H2R = T(0), H3L = T(0), H3R = T(0);
-  VT G1, G2;                                // row hy2, planes z+dz, z+2dz (in flight)
-  VT Ub[TY], Uc[TY], Ua[TY]; // u1 own rows, planes z-dz, z, z+dz
-  T UcL[TY], UcR[TY], UaL[TY], UaR[TY];
-  VT uH; // u1 block halo row, plane z+dz (edge waves)
-
-  auto zcl = [&](int zz) { return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz); };
-  auto load_row = [&](int y, int z, VT &v, T &L, T &R) {
-    const T *p = rowp(y, z);
+  // ---- windows ----
+  VT C[NC];                // src planes z + k dz, k = 0 .. NC-1 (the last PF in flight)
+  T CL[NC], CR[NC];        // src at x-1 / x+V (edge lanes)
+  T LLa, RRa, LLb, RRb;    // src at x-2 / x+V+1: plane z+dz (a), plane z+2dz (b, in flight)
+  VT Ub, Uc, Ua;           // u1 planes z-dz, z, z+dz
+  T UcL, UcR, UaL, UaR;    // u1 at x-1 / x+V, planes z and z+dz
+  auto load_row = [&](int zz, VT &v, T &L, T &R) {
+    const T *p = rowp(zz);
     v = ld(p);
     L = edgeL ? p[-1] : T(0);
     R = edgeR ? p[V] : T(0);
   };
-  auto load_outer = [&](int y, int z, T &LL, T &RR) {
-    const T *p = rowp(y, z);
-    LL = edgeL ? p[-2] : T(0);
-    RR = edgeR ? p[V + 1] : T(0);
+  auto load_outer = [&](int zz, T &L2, T &R2) {
+    const T *p = rowp(zz);
+    L2 = edgeL ? p[-2] : T(0);
+    R2 = edgeR ? p[V + 1] : T(0);
   };
 
-  // ---- warm-up: src planes z0-2dz .. z0; the loop starts two planes early (u1 only) ----
+  // warm-up: the loop starts two planes early (t = -2: u1 only), window planes z0-2dz .. z0+(PF-1)dz
   {
-    const int zA = z0 - 2 * dz, zB = z0 - dz, zC = z0;
+    const int zw = z0 - 2 * dz;
 #pragma unroll
-    for (int i = 0; i < TY; ++i) {
-      load_row(ybase + i, zA, C0[i], C0L[i], C0R[i]);
-      load_row(ybase + i, zB, C1[i], C1L[i], C1R[i]);
-      load_row(ybase + i, zC, C2[i], C2L[i], C2R[i]);
-      load_outer(ybase + i, zB, C1LL[i], C1RR[i]);
-    }
-    if (edgeWave) {
-      H0 = ld(rowp(hy1, zA));
-      load_row(hy1, zB, H1, H1L, H1R);
-      load_row(hy1, zC, H2, H2L, H2R);
-      G1 = ld(rowp(hy2, zB));
-    }
-    cs[0][slotTop][lane] = C1[0];
-    cs[0][slotBot][lane] = C1[TY - 1];
-    if (edgeL) {
-      ce[0][slotTop][0] = C1L[0];
-      ce[0][slotBot][0] = C1L[TY - 1];
-    }
-    if (edgeR) {
-      ce[0][slotTop][1] = C1R[0];
-      ce[0][slotBot][1] = C1R[TY - 1];
-    }
+    for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, C[k], CL[k], CR[k]);
+    load_outer(zw + dz, LLa, RRa);
+    cs[0][w][lane] = C[1];
+    if (edgeL) ce[0][w][0] = CL[1];
+    if (edgeR) ce[0][w][1] = CR[1];
     __syncthreads();
   }
 
@@ -182,127 +161,62 @@ __global__ __launch_bounds__(64 * NW, MINW) void stencil7x2_kernel(StencilArgs<T
   for (int t = -2; t < nzs; ++t) {
     const int z = z0 + t * dz;
     const int P = z + dz;
-    // 1. lookahead loads: src plane z+3dz (+ the outer x scalars and the hy2 row of plane z+2dz)
+    // 1. lookahead loads
+    load_row(z + (NC - 1) * dz, C[NC - 1], CL[NC - 1], CR[NC - 1]);
+    load_outer(z + 2 * dz, LLb, RRb);
+    // 2. u1 at plane z+dz
+    const VT cA = cs[buf][wA][lane], cB = cs[buf][wB][lane];
+    const T cAL = edgeL ? ce[buf][wA][0] : T(0), cAR = edgeR ? ce[buf][wA][1] : T(0);
+    const T cBL = edgeL ? ce[buf][wB][0] : T(0), cBR = edgeR ? ce[buf][wB][1] : T(0);
     {
-      const int z3 = zcl(z + 3 * dz), z2 = zcl(z + 2 * dz);
-#pragma unroll
-      for (int i = 0; i < TY; ++i) {
-        load_row(ybase + i, z3, C3[i], C3L[i], C3R[i]);
-        load_outer(ybase + i, z2, C2LL[i], C2RR[i]);
-      }
-      if (edgeWave) {
-        load_row(hy1, z3, H3, H3L, H3R);
-        G2 = ld(rowp(hy2, z2));
-      }
-    }
-    // src rows at plane z+dz next to this wave's rows (other waves through LDS, block edges from registers)
-    const VT cAbove = top ? H1 : cs[buf][slotAbove][lane];
-    const VT cBelow = bot ? H1 : cs[buf][slotBelow][lane];
-    const T cAboveL = top ? H1L : (edgeL ? ce[buf][slotAbove][0] : T(0));
-    const T cAboveR = top ? H1R : (edgeR ? ce[buf][slotAbove][1] : T(0));
-    const T cBelowL = bot ? H1L : (edgeL ? ce[buf][slotBelow][0] : T(0));
-    const T cBelowR = bot ? H1R : (edgeR ? ce[buf][slotBelow][1] : T(0));
-
-    // 2. u1 at plane z+dz: own rows, their wave-edge scalars, and the block halo row
-#pragma unroll
-    for (int i = 0; i < TY; ++i) {
-      const int y = ybase + i;
-      const VT &up = i == 0 ? cAbove : C1[i - 1];
-      const VT &dn = i == TY - 1 ? cBelow : C1[i + 1];
+      const RowSph rs = row_sph(P);
       T o[V];
-      const RowSph rs = row_sph(y, P);
-      apply_row(C1[i], up, dn, down ? C0[i] : C2[i], down ? C2[i] : C0[i], C1L[i], C1R[i], rs, o);
-      Ua[i] = toVT(o);
-      // one cell outside the wave's x range (meaningful on the edge lanes only; branch-free elsewhere)
-      const T upL = i == 0 ? cAboveL : C1L[i - 1], upR = i == 0 ? cAboveR : C1R[i - 1];
-      const T dnL = i == TY - 1 ? cBelowL : C1L[i + 1], dnR = i == TY - 1 ? cBelowR : C1R[i + 1];
-      UaL[i] = fix(rs, xb - 1,
-                   sum6<T, KIND>(vget<T>(C1[i], 0), C1LL[i], dnL, upL, down ? C0L[i] : C2L[i], down ? C2L[i] : C0L[i]));
-      UaR[i] = fix(rs, xb + V,
-                   sum6<T, KIND>(C1RR[i], vget<T>(C1[i], V - 1), dnR, upR, down ? C0R[i] : C2R[i],
-                                 down ? C2R[i] : C0R[i]));
+      apply_row(C[1], cA, cB, down ? C[0] : C[2], down ? C[2] : C[0], CL[1], CR[1], rs, o);
+      Ua = toVT(o);
+      UaL = fix(rs, xb - 1, sum6<T, KIND>(vget<T>(C[1], 0), LLa, cBL, cAL, down ? CL[0] : CL[2], down ? CL[2] : CL[0]));
+      UaR = fix(rs, xb + V,
+                sum6<T, KIND>(RRa, vget<T>(C[1], V - 1), cBR, cAR, down ? CR[0] : CR[2], down ? CR[2] : CR[0]));
     }
-    if (edgeWave) { // u1 of the block halo row (one row outside the block)
-      T o[V];
-      const VT &up = top ? G1 : C1[TY - 1];
-      const VT &dn = top ? C1[0] : G1;
-      apply_row(H1, up, dn, down ? H0 : H2, down ? H2 : H0, H1L, H1R, row_sph(hy1, P), o);
-      uH = toVT(o);
-    }
-
-    // 3. u2 at plane z (once the u1 window is full)
+    // 3. u2 at plane z
     if (t >= 0) {
-      const VT uAbove = top ? us[buf][2 * NW][lane] : us[buf][slotAbove][lane];
-      const VT uBelow = bot ? us[buf][2 * NW + 1][lane] : us[buf][slotBelow][lane];
+      const VT uA = us[buf][wA][lane], uB = us[buf][wB][lane];
+      T o[V];
+      apply_row(Uc, uA, uB, down ? Ub : Ua, down ? Ua : Ub, UcL, UcR, row_sph(z), o);
+      if (outRow) {
+        T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+        if (fullX) {
+          NV v;
 #pragma unroll
-      for (int i = 0; i < TY; ++i) {
-        const int y = ybase + i;
-        const VT &up = i == 0 ? uAbove : Uc[i - 1];
-        const VT &dn = i == TY - 1 ? uBelow : Uc[i + 1];
-        T o[V];
-        apply_row(Uc[i], up, dn, down ? Ub[i] : Ua[i], down ? Ua[i] : Ub[i], UcL[i], UcR[i], row_sph(y, z), o);
-        if (cvalid && y < a.hiy) {
-          T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
-          if (fullX) {
-            NV v;
+          for (int e = 0; e < V; ++e) v[e] = o[e];
+          __builtin_nontemporal_store(v, reinterpret_cast<NV *>(dp));
+        } else {
 #pragma unroll
-            for (int e = 0; e < V; ++e) v[e] = o[e];
-            __builtin_nontemporal_store(v, reinterpret_cast<NV *>(dp));
-          } else {
-#pragma unroll
-            for (int e = 0; e < V; ++e)
-              if (xb + e >= a.lox && xb + e < a.hix) dp[e] = o[e];
-          }
+          for (int e = 0; e < V; ++e)
+            if (xb + e >= a.lox && xb + e < a.hix) dp[e] = o[e];
         }
       }
     }
-
-    // 4. publish src plane z+2dz and u1 plane z+dz boundary rows for the next step
+    // 4. publish src plane z+2dz and u1 plane z+dz
     const int nbuf = buf ^ 1;
-    cs[nbuf][slotTop][lane] = C2[0];
-    cs[nbuf][slotBot][lane] = C2[TY - 1];
-    if (edgeL) {
-      ce[nbuf][slotTop][0] = C2L[0];
-      ce[nbuf][slotBot][0] = C2L[TY - 1];
-    }
-    if (edgeR) {
-      ce[nbuf][slotTop][1] = C2R[0];
-      ce[nbuf][slotBot][1] = C2R[TY - 1];
-    }
-    us[nbuf][slotTop][lane] = Ua[0];
-    us[nbuf][slotBot][lane] = Ua[TY - 1];
-    if (top) us[nbuf][2 * NW][lane] = uH;
-    if (bot) us[nbuf][2 * NW + 1][lane] = uH;
+    cs[nbuf][w][lane] = C[2];
+    if (edgeL) ce[nbuf][w][0] = CL[2];
+    if (edgeR) ce[nbuf][w][1] = CR[2];
+    us[nbuf][w][lane] = Ua;
     __syncthreads();
     buf = nbuf;
-
-    // 5. rotate the windows
+    // 5. rotate
 #pragma unroll
-    for (int i = 0; i < TY; ++i) {
-      C0[i] = C1[i];
-      C0L[i] = C1L[i];
-      C0R[i] = C1R[i];
-      C1[i] = C2[i];
-      C1L[i] = C2L[i];
-      C1R[i] = C2R[i];
-      C2[i] = C3[i];
-      C2L[i] = C3L[i];
-      C2R[i] = C3R[i];
-      C1LL[i] = C2LL[i];
-      C1RR[i] = C2RR[i];
-      Ub[i] = Uc[i];
-      Uc[i] = Ua[i];
-      UcL[i] = UaL[i];
-      UcR[i] = UaR[i];
+    for (int k = 0; k < NC - 1; ++k) {
+      C[k] = C[k + 1];
+      CL[k] = CL[k + 1];
+      CR[k] = CR[k + 1];
     }
-    H0 = H1;
-    H1 = H2;
-    H2 = H3;
-    H1L = H2L;
-    H1R = H2R;
-    H2L = H3L;
-    H2R = H3R;
-    G1 = G2;
+    LLa = LLb;
+    RRa = RRb;
+    Ub = Uc;
+    Uc = Ua;
+    UcL = UaL;
+    UcR = UaR;
   }
 }
 
@@ -344,10 +258,10 @@ bool stencil7x2_supported(const LocalDomain &dom, int64_t qi) {
   return aligned && lox - 2 + dom.pad_x(qi) >= 0 && lox + nchunks * V + 1 < p.x - dom.pad_x(qi);
 }
 
-template <typename T, int KIND, int TY, int NW, int MINW>
+template <typename T, int KIND, int NW, int PF>
 static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
                        const StencilTune &tune) {
-  constexpr int V = Vec16<T>::N;
+  constexpr int V = Vec16<T>::N, YO = NW - 4;
   StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   const int rxm = int(dom.radius().x(-1));
@@ -356,24 +270,20 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.nchunks = (a.hix - a.x0 + V - 1) / V;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = (a.nchunks + 63) / 64;
-  a.gy = (ny + NW * TY - 1) / (NW * TY);
-  const void *kern = tune.xcdRemap ? (const void *)stencil7x2_kernel<T, TY, NW, KIND, true, MINW>
-                                   : (const void *)stencil7x2_kernel<T, TY, NW, KIND, false, MINW>;
+  a.gy = (ny + YO - 1) / YO;
+  const void *kern = tune.xcdRemap ? (const void *)stencil7x2_kernel<T, NW, PF, KIND, true>
+                                   : (const void *)stencil7x2_kernel<T, NW, PF, KIND, false>;
   int zc = tune.zchunk;
-  if (zc <= 0) {
-    // one round of resident blocks; each block re-reads 2 warm-up planes, so keep z-chunks >= 16 planes
-    const int64_t cols = int64_t(a.gx) * a.gy;
-    const int64_t nzc = std::max<int64_t>(1, x2_resident_blocks(kern, 64 * NW) / cols);
-    zc = int(std::max<int64_t>(16, (nz + nzc - 1) / nzc));
-  }
+  if (zc <= 0) // each z-chunk re-reads 4 warm-up planes (2 src + 2 for u1)
+    zc = pick_zchunk(int64_t(a.gx) * a.gy, nz, x2_resident_blocks(kern, 64 * NW), 4, 16);
   a.zc = zc;
   a.gz = (nz + zc - 1) / zc;
   const uint32_t blocks = uint32_t(a.gx) * a.gy * a.gz;
   dom.set_device();
   if (tune.xcdRemap)
-    hipLaunchKernelGGL((stencil7x2_kernel<T, TY, NW, KIND, true, MINW>), dim3(blocks), dim3(64, NW), 0, stream, a);
+    hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, true>), dim3(blocks), dim3(64, NW), 0, stream, a);
   else
-    hipLaunchKernelGGL((stencil7x2_kernel<T, TY, NW, KIND, false, MINW>), dim3(blocks), dim3(64, NW), 0, stream, a);
+    hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, false>), dim3(blocks), dim3(64, NW), 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -389,18 +299,21 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   const bool jac = kind == StencilKind::Jacobi;
   // shapes (rows per lane, waves per block, min waves/SIMD): 1x8 keeps everything in registers at 6 waves/SIMD;
   // 2x4 at 3 waves/SIMD; 2x8 at 4 (spills)
-  // shape = rows per lane x waves per block (min waves/SIMD): 1x8 (4), 1x16 (4), 2x4 (3); x2nw == 2 selects 2x4 (2)
-  const int shape = tune.x2ty == 2 ? (tune.x2nw == 2 ? 3 : 1) : (tune.x2nw == 16 ? 2 : 0);
+  // shape = waves per block (one src row each; NW-4 output rows) x planes of z lookahead
+  const int shape = (tune.x2nw == 8 ? 0 : (tune.x2nw == 12 ? 3 : 6)) + (tune.x2pf <= 2 ? 0 : (tune.x2pf == 3 ? 1 : 2));
 #define X2_LAUNCH(TT, K)                                                                                           \
   do {                                                                                                             \
-    if (shape == 0)                                                                                                \
-      apply_x2_t<TT, K, 1, 8, 4>(dom, qi, region, sph, stream, tune);                                              \
-    else if (shape == 1)                                                                                           \
-      apply_x2_t<TT, K, 2, 4, 3>(dom, qi, region, sph, stream, tune);                                              \
-    else if (shape == 2)                                                                                           \
-      apply_x2_t<TT, K, 1, 16, 4>(dom, qi, region, sph, stream, tune);                                             \
-    else                                                                                                           \
-      apply_x2_t<TT, K, 2, 4, 2>(dom, qi, region, sph, stream, tune);                                              \
+    switch (shape) {                                                                                               \
+    case 0: apply_x2_t<TT, K, 8, 2>(dom, qi, region, sph, stream, tune); break;                                    \
+    case 1: apply_x2_t<TT, K, 8, 3>(dom, qi, region, sph, stream, tune); break;                                    \
+    case 2: apply_x2_t<TT, K, 8, 4>(dom, qi, region, sph, stream, tune); break;                                    \
+    case 3: apply_x2_t<TT, K, 12, 2>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 4: apply_x2_t<TT, K, 12, 3>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 5: apply_x2_t<TT, K, 12, 4>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 6: apply_x2_t<TT, K, 16, 2>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 7: apply_x2_t<TT, K, 16, 3>(dom, qi, region, sph, stream, tune); break;                                   \
+    default: apply_x2_t<TT, K, 16, 4>(dom, qi, region, sph, stream, tune); break;                                  \
+    }                                                                                                              \
   } while (0)
   if (f32) {
     if (jac)

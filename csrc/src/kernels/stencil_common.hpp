@@ -112,6 +112,27 @@ inline StencilArgs<T> make_args(const LocalDomain &dom, int64_t qi, const Rect3 
 }
 
 
+// z-chunk length for a z-marching launch of `cols` block columns over nz planes with `resident` blocks resident
+// at once: maximise (useful planes / planes read) x (blocks / block slots of the rounds), i.e. balance the warm-up
+// planes each chunk re-reads (`warm`) against a partly empty last round of blocks.
+inline int pick_zchunk(int64_t cols, int nz, int64_t resident, int warm, int minZc = 8) {
+  int best = nz;
+  double bestEff = -1;
+  for (int gz = 1; gz <= nz; ++gz) {
+    const int zc = (nz + gz - 1) / gz;
+    if (zc < minZc && gz > 1) break;
+    const int64_t blocks = cols * ((nz + zc - 1) / zc);
+    const int64_t rounds = (blocks + resident - 1) / resident;
+    const double fill = double(blocks) / double(rounds * resident);
+    const double eff = fill * double(zc) / double(zc + warm);
+    if (eff > bestEff + 1e-9) {
+      bestEff = eff;
+      best = zc;
+    }
+  }
+  return best;
+}
+
 // Jacobi: sum order +x,-x,+y,-y,+z,-z (reference bin/jacobi3d.cu:72-83); Astaroth: -x,-y,-z,+x,+y,+z
 // (bin/astaroth_sim.cu:72-81); then the exact /6
 template <typename T, int KIND>
