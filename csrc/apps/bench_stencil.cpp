@@ -182,6 +182,33 @@ int main(int argc, char **argv) {
     return 0;
   }
   for (int rep = 0; rep < reps; ++rep)
+  if (only == "x2pp") {
+    // the fused pair as the model runs it: ping-pong (swap after every launch), so every launch reads what the
+    // previous one wrote; non-temporal stores and the alternating z-march on/off
+    LocalDomain l2(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
+    l2.set_radius(Radius::face_edge_corner(2, 1, 0));
+    l2.add_data<float>("d");
+    l2.realize();
+    const Rect3 reg2 = l2.get_compute_region();
+    jacobi_init(l2, 0, l2.get_full_region(), s);
+    fill_value(l2, 0, 0.5, false, s);
+    s.sync();
+    for (int nt = 0; nt < 2; ++nt)
+      for (int alt = 0; alt < 2; ++alt)
+        for (int zc : {0, 64}) {
+          StencilTune t;
+          t.nontemporal = nt;
+          t.alternateZ = alt;
+          t.zchunk = zc;
+          const double us = timeit([&] {
+            stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t);
+            l2.swap();
+          }) / 2;
+          std::printf("x2pp_nt%d_alt%d,%d,1,%d,%.2f,%.1f,%.3f,nw%d\n", nt, alt, t.x2pf, zc, us, cells / us / 1e3,
+                      cells * 8 / us / 1e6, t.x2nw);
+        }
+  }
+  for (int rep = 0; rep < reps; ++rep)
   if (only.empty() || only == "x2") {
     // two fused steps per sweep (temporal blocking) on a depth-2 domain; reported per STEP (two steps per launch)
     LocalDomain l2(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);

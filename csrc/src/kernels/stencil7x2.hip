@@ -20,27 +20,99 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <type_traits>
 
 #include "stencil/rt/hip_check.hpp"
 #include "stencil_common.hpp"
 
 namespace stencil {
 
+// Packed-math helpers. A wave64 fp32 VALU op covers 64 lanes x 1 value; v_pk_{add,mul,fma}_f32 cover 64 x 2 at the
+// same issue cost, so rows are summed as pairs (2 pk ops per 4-float chunk per term). fp64 has no packed form: the
+// pair type is then two scalar ops. IEEE per element, so results are bitwise those of the scalar code.
+template <typename T> struct Pk;
+template <> struct Pk<float> { typedef float t __attribute__((ext_vector_type(2))); };
+template <> struct Pk<double> { typedef double t __attribute__((ext_vector_type(2))); };
+
+// whole-wave lane shifts on the DPP path (a VALU mov, no LDS round trip as with ds_bpermute): lane i receives
+// lane i-1 (wave_shr:1) / lane i+1 (wave_shl:1); the lanes shifted in from outside the wave get 0 and are replaced
+// by the edge scalars
+__device__ __forceinline__ int dpp_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ int dpp_shl1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }
+template <typename T> __device__ __forceinline__ T from_prev_lane(T v);
+template <typename T> __device__ __forceinline__ T from_next_lane(T v);
+template <> __device__ __forceinline__ float from_prev_lane<float>(float v) { return __int_as_float(dpp_shr1(__float_as_int(v))); }
+template <> __device__ __forceinline__ float from_next_lane<float>(float v) { return __int_as_float(dpp_shl1(__float_as_int(v))); }
+template <> __device__ __forceinline__ double from_prev_lane<double>(double v) {
+  const int64_t b = __double_as_longlong(v);
+  return __longlong_as_double(int64_t(uint32_t(dpp_shr1(int(b)))) | (int64_t(dpp_shr1(int(b >> 32))) << 32));
+}
+template <> __device__ __forceinline__ double from_next_lane<double>(double v) {
+  const int64_t b = __double_as_longlong(v);
+  return __longlong_as_double(int64_t(uint32_t(dpp_shl1(int(b)))) | (int64_t(dpp_shl1(int(b >> 32))) << 32));
+}
+
+// Six-term sums in the reference's order (sum6 in stencil_common.hpp), element-wise over a vector type. The fp32
+// sums start from the first term instead of 0 + first term: the two differ only in the sign of an all-zero sum,
+// and the exact /6 below maps both zeros to +0 as the 0-started sum does. fp64 keeps the 0 start (true division).
+template <typename T, int KIND, typename X>
+__device__ __forceinline__ X sum6v(const X &vpx, const X &vmx, const X &vpy, const X &vmy, const X &vpz, const X &vmz) {
+  X s;
+  if constexpr (KIND == 0) {
+    s = std::is_same<T, float>::value ? vpx : X(T(0)) + vpx;
+    s += vmx;
+    s += vpy;
+    s += vmy;
+    s += vpz;
+    s += vmz;
+  } else {
+    s = std::is_same<T, float>::value ? vmx : X(T(0)) + vmx;
+    s += vmy;
+    s += vmz;
+    s += vpx;
+    s += vpy;
+    s += vpz;
+  }
+  return s;
+}
+// exact element-wise /6 (div6): fp32 two FMAs around the reciprocal, packed; sums with 0 < |s| < 2^-100 (where the
+// FMA form is not exact) take the true division in a branch no wave normally enters
+template <typename T, typename X, int N> __device__ __forceinline__ X div6v(const X &s) {
+  if constexpr (std::is_same<T, float>::value) {
+    const X c = X(1.0f / 6.0f), six = X(6.0f);
+    const X q0 = s * c;
+    const X r = __builtin_elementwise_fma(-q0, six, s);
+    X q = __builtin_elementwise_fma(r, c, q0);
+    float m = __builtin_fabsf(s[0]);
+#pragma unroll
+    for (int e = 1; e < N; ++e) m = __builtin_fminf(m, __builtin_fabsf(s[e]));
+    if (__builtin_expect(m < 0x1p-100f, 0)) {
+#pragma unroll
+      for (int e = 0; e < N; ++e)
+        if (__builtin_fabsf(s[e]) < 0x1p-100f && s[e] != 0.0f) q[e] = s[e] / 6.0f;
+    }
+    return q;
+  } else {
+    return s / X(T(6));
+  }
+}
+
 // Block = NW waves, ONE src row per wave: the block's src rows are [yblk-2, yblk-2+NW); u1 is valid on the inner
 // NW-2 of them and u2 (the output) on the inner NW-4, so the block writes YO = NW-4 rows and every wave runs the
 // same code (the two outer rows on each side are a redundant y halo, re-read from L2 by the neighbouring block).
 // z: the src window holds planes z .. z+(2+PF)dz; the last PF planes are in flight, so a row load is issued PF
-// steps before it is consumed.
+// steps before it is consumed. The march direction is a template argument of the loop body (DOWN), so selecting
+// the +z / -z neighbour costs nothing.
 template <typename T, int NW, int PF, int KIND, bool REMAP>
 __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a) {
-  using VT = typename Vec16<T>::type;
   using NV = typename Vec16<T>::native;
+  using P2 = typename Pk<T>::t;
   constexpr int V = Vec16<T>::N;
   constexpr int YO = NW - 4;
   constexpr int NC = 3 + PF; // src window planes
   static_assert(NW > 4, "a block needs more than its 4 halo rows");
-  __shared__ VT cs[2][NW][64]; // src row of every wave, plane z+2dz at publish (= z+dz when read)
-  __shared__ VT us[2][NW][64]; // u1 row of every wave, plane z+dz at publish (= z when read)
+  __shared__ NV cs[2][NW][64]; // src row of every wave, plane z+2dz at publish (= z+dz when read)
+  __shared__ NV us[2][NW][64]; // u1 row of every wave, plane z+dz at publish (= z when read)
   __shared__ T ce[2][NW][2];   // src edge scalars of the published rows: [0] at x-1 (lane 0), [1] at x+V
 
   const uint32_t nb = uint32_t(a.gx) * a.gy * a.gz;
@@ -60,8 +132,6 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
   const int ze = min(zs + a.zc, a.hiz);
   if (yblk >= a.hiy || zs >= ze) return; // block-uniform
   const bool down = ((bz & 1) != 0) != (a.flip != 0);
-  const int dz = down ? -1 : 1;
-  const int z0 = down ? ze - 1 : zs;
   const int nzs = ze - zs;
 
   const bool edgeL = lane == 0;
@@ -74,20 +144,6 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
   const T *rowbase = a.src + int64_t(yc) * a.px + xb;
   auto zcl = [&](int zz) { return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz); };
   auto rowp = [&](int zz) -> const T * { return rowbase + int64_t(zcl(zz)) * a.pxy; };
-  auto ld = [&](const T *p) -> VT { return *reinterpret_cast<const VT *>(p); };
-  auto toVT = [&](const T (&o)[V]) -> VT {
-    VT v;
-    if constexpr (V == 4) {
-      v.x = o[0];
-      v.y = o[1];
-      v.z = o[2];
-      v.w = o[3];
-    } else {
-      v.x = o[0];
-      v.y = o[1];
-    }
-    return v;
-  };
   // sphere membership of the row at plane P: y/z part once per row, per-cell test only for the few hit rows
   struct RowSph {
     int dh, dc;
@@ -103,121 +159,132 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
     return r;
   };
   auto fix = [&](const RowSph &rs, int x, T v) -> T {
-    if (KIND != 0 || !rs.hit) return v;
     const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
     const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
     return hot ? T(1) : (cold ? T(0) : v);
   };
-  // S at this wave's row chunk `cm`: x-neighbours by shuffles (+ edge scalars at the wave edges)
-  auto apply_row = [&](const VT &cm, const VT &up, const VT &dn, const VT &zp, const VT &zm, T eL, T eR,
-                       const RowSph &rs, T (&o)[V]) {
-    const T sl = shfl_up1<T>(vget<T>(cm, V - 1));
-    const T sr = shfl_down1<T>(vget<T>(cm, 0));
+  // S at this wave's row chunk `cm`: x-neighbours by DPP lane shifts (+ edge scalars at the wave edges)
+  auto apply_row = [&](const NV &cm, const NV &up, const NV &dn, const NV &zp, const NV &zm, T eL, T eR,
+                       const RowSph &rs) -> NV {
+    const T sl = from_prev_lane<T>(cm[V - 1]);
+    const T sr = from_next_lane<T>(cm[0]);
     const T left = edgeL ? eL : sl;
     const T right = edgeR ? eR : sr;
+    NV vpx, vmx;
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const T vpx = e < V - 1 ? vget<T>(cm, e + 1) : right;
-      const T vmx = e > 0 ? vget<T>(cm, e - 1) : left;
-      o[e] = sum6<T, KIND>(vpx, vmx, vget<T>(dn, e), vget<T>(up, e), vget<T>(zp, e), vget<T>(zm, e));
+      vpx[e] = e < V - 1 ? cm[e + 1] : right;
+      vmx[e] = e > 0 ? cm[e - 1] : left;
     }
-    if (rs.hit) {
+    NV o = div6v<T, NV, V>(sum6v<T, KIND>(vpx, vmx, dn, up, zp, zm));
+    if (KIND == 0 && rs.hit) {
 #pragma unroll
       for (int e = 0; e < V; ++e) o[e] = fix(rs, xb + e, o[e]);
     }
+    return o;
   };
 
-  // ---- windows ----
-  VT C[NC];                // src planes z + k dz, k = 0 .. NC-1 (the last PF in flight)
-  T CL[NC], CR[NC];        // src at x-1 / x+V (edge lanes)
-  T LLa, RRa, LLb, RRb;    // src at x-2 / x+V+1: plane z+dz (a), plane z+2dz (b, in flight)
-  VT Ub, Uc, Ua;           // u1 planes z-dz, z, z+dz
-  T UcL, UcR, UaL, UaR;    // u1 at x-1 / x+V, planes z and z+dz
-  auto load_row = [&](int zz, VT &v, T &L, T &R) {
-    const T *p = rowp(zz);
-    v = ld(p);
-    L = edgeL ? p[-1] : T(0);
-    R = edgeR ? p[V] : T(0);
-  };
-  auto load_outer = [&](int zz, T &L2, T &R2) {
-    const T *p = rowp(zz);
-    L2 = edgeL ? p[-2] : T(0);
-    R2 = edgeR ? p[V + 1] : T(0);
-  };
+  auto march = [&](auto downTag) {
+    constexpr bool DOWN = decltype(downTag)::value;
+    constexpr int dz = DOWN ? -1 : 1;
+    const int z0 = DOWN ? ze - 1 : zs;
+    // ---- windows ----
+    NV C[NC];             // src planes z + k dz, k = 0 .. NC-1 (the last PF in flight)
+    T CL[NC], CR[NC];     // src at x-1 / x+V (edge lanes)
+    T LLa, RRa, LLb, RRb; // src at x-2 / x+V+1: plane z+dz (a), plane z+2dz (b, in flight)
+    NV Ub, Uc, Ua;        // u1 planes z-dz, z, z+dz
+    P2 UcE, UaE;          // u1 at (x-1, x+V), planes z and z+dz
+    auto load_row = [&](int zz, NV &v, T &L, T &R) {
+      const T *p = rowp(zz);
+      v = *reinterpret_cast<const NV *>(p);
+      L = edgeL ? p[-1] : T(0);
+      R = edgeR ? p[V] : T(0);
+    };
+    auto load_outer = [&](int zz, T &L2, T &R2) {
+      const T *p = rowp(zz);
+      L2 = edgeL ? p[-2] : T(0);
+      R2 = edgeR ? p[V + 1] : T(0);
+    };
 
-  // warm-up: the loop starts two planes early (t = -2: u1 only), window planes z0-2dz .. z0+(PF-1)dz
-  {
-    const int zw = z0 - 2 * dz;
-#pragma unroll
-    for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, C[k], CL[k], CR[k]);
-    load_outer(zw + dz, LLa, RRa);
-    cs[0][w][lane] = C[1];
-    if (edgeL) ce[0][w][0] = CL[1];
-    if (edgeR) ce[0][w][1] = CR[1];
-    __syncthreads();
-  }
-
-  int buf = 0;
-  for (int t = -2; t < nzs; ++t) {
-    const int z = z0 + t * dz;
-    const int P = z + dz;
-    // 1. lookahead loads
-    load_row(z + (NC - 1) * dz, C[NC - 1], CL[NC - 1], CR[NC - 1]);
-    load_outer(z + 2 * dz, LLb, RRb);
-    // 2. u1 at plane z+dz
-    const VT cA = cs[buf][wA][lane], cB = cs[buf][wB][lane];
-    const T cAL = edgeL ? ce[buf][wA][0] : T(0), cAR = edgeR ? ce[buf][wA][1] : T(0);
-    const T cBL = edgeL ? ce[buf][wB][0] : T(0), cBR = edgeR ? ce[buf][wB][1] : T(0);
+    // warm-up: the loop starts two planes early (t = -2: u1 only), window planes z0-2dz .. z0+(PF-1)dz
     {
-      const RowSph rs = row_sph(P);
-      T o[V];
-      apply_row(C[1], cA, cB, down ? C[0] : C[2], down ? C[2] : C[0], CL[1], CR[1], rs, o);
-      Ua = toVT(o);
-      UaL = fix(rs, xb - 1, sum6<T, KIND>(vget<T>(C[1], 0), LLa, cBL, cAL, down ? CL[0] : CL[2], down ? CL[2] : CL[0]));
-      UaR = fix(rs, xb + V,
-                sum6<T, KIND>(RRa, vget<T>(C[1], V - 1), cBR, cAR, down ? CR[0] : CR[2], down ? CR[2] : CR[0]));
+      const int zw = z0 - 2 * dz;
+#pragma unroll
+      for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, C[k], CL[k], CR[k]);
+      load_outer(zw + dz, LLa, RRa);
+      cs[0][w][lane] = C[1];
+      if (edgeL) ce[0][w][0] = CL[1];
+      if (edgeR) ce[0][w][1] = CR[1];
+      __syncthreads();
     }
-    // 3. u2 at plane z
-    if (t >= 0) {
-      const VT uA = us[buf][wA][lane], uB = us[buf][wB][lane];
-      T o[V];
-      apply_row(Uc, uA, uB, down ? Ub : Ua, down ? Ua : Ub, UcL, UcR, row_sph(z), o);
-      if (outRow) {
-        T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
-        if (fullX) {
-          NV v;
-#pragma unroll
-          for (int e = 0; e < V; ++e) v[e] = o[e];
-          __builtin_nontemporal_store(v, reinterpret_cast<NV *>(dp));
-        } else {
-#pragma unroll
-          for (int e = 0; e < V; ++e)
-            if (xb + e >= a.lox && xb + e < a.hix) dp[e] = o[e];
+
+    int buf = 0;
+    for (int t = -2; t < nzs; ++t) {
+      const int z = z0 + t * dz;
+      const int P = z + dz;
+      // 1. lookahead loads
+      load_row(z + (NC - 1) * dz, C[NC - 1], CL[NC - 1], CR[NC - 1]);
+      load_outer(z + 2 * dz, LLb, RRb);
+      // 2. u1 at plane z+dz (row + the two edge cells as one pair)
+      const NV cA = cs[buf][wA][lane], cB = cs[buf][wB][lane];
+      const T cAL = edgeL ? ce[buf][wA][0] : T(0), cAR = edgeR ? ce[buf][wA][1] : T(0);
+      const T cBL = edgeL ? ce[buf][wB][0] : T(0), cBR = edgeR ? ce[buf][wB][1] : T(0);
+      {
+        const RowSph rs = row_sph(P);
+        Ua = apply_row(C[1], cA, cB, DOWN ? C[0] : C[2], DOWN ? C[2] : C[0], CL[1], CR[1], rs);
+        const P2 epx = {C[1][0], RRa}, emx = {LLa, C[1][V - 1]}, epy = {cBL, cBR}, emy = {cAL, cAR};
+        const P2 ezp = DOWN ? P2{CL[0], CR[0]} : P2{CL[2], CR[2]};
+        const P2 ezm = DOWN ? P2{CL[2], CR[2]} : P2{CL[0], CR[0]};
+        UaE = div6v<T, P2, 2>(sum6v<T, KIND>(epx, emx, epy, emy, ezp, ezm));
+        if (KIND == 0 && rs.hit) {
+          UaE[0] = fix(rs, xb - 1, UaE[0]);
+          UaE[1] = fix(rs, xb + V, UaE[1]);
         }
       }
-    }
-    // 4. publish src plane z+2dz and u1 plane z+dz
-    const int nbuf = buf ^ 1;
-    cs[nbuf][w][lane] = C[2];
-    if (edgeL) ce[nbuf][w][0] = CL[2];
-    if (edgeR) ce[nbuf][w][1] = CR[2];
-    us[nbuf][w][lane] = Ua;
-    __syncthreads();
-    buf = nbuf;
-    // 5. rotate
+      // 3. u2 at plane z
+      if (t >= 0) {
+        const NV uA = us[buf][wA][lane], uB = us[buf][wB][lane];
+        const NV o = apply_row(Uc, uA, uB, DOWN ? Ub : Ua, DOWN ? Ua : Ub, UcE[0], UcE[1], row_sph(z));
+        if (outRow) {
+          T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+          if (fullX) {
+            if (a.nt)
+              __builtin_nontemporal_store(o, reinterpret_cast<NV *>(dp));
+            else
+              *reinterpret_cast<NV *>(dp) = o;
+          } else {
 #pragma unroll
-    for (int k = 0; k < NC - 1; ++k) {
-      C[k] = C[k + 1];
-      CL[k] = CL[k + 1];
-      CR[k] = CR[k + 1];
+            for (int e = 0; e < V; ++e)
+              if (xb + e >= a.lox && xb + e < a.hix) dp[e] = o[e];
+          }
+        }
+      }
+      // 4. publish src plane z+2dz and u1 plane z+dz
+      const int nbuf = buf ^ 1;
+      cs[nbuf][w][lane] = C[2];
+      if (edgeL) ce[nbuf][w][0] = CL[2];
+      if (edgeR) ce[nbuf][w][1] = CR[2];
+      us[nbuf][w][lane] = Ua;
+      __syncthreads();
+      buf = nbuf;
+      // 5. rotate
+#pragma unroll
+      for (int k = 0; k < NC - 1; ++k) {
+        C[k] = C[k + 1];
+        CL[k] = CL[k + 1];
+        CR[k] = CR[k + 1];
+      }
+      LLa = LLb;
+      RRa = RRb;
+      Ub = Uc;
+      Uc = Ua;
+      UcE = UaE;
     }
-    LLa = LLb;
-    RRa = RRb;
-    Ub = Uc;
-    Uc = Ua;
-    UcL = UaL;
-    UcR = UaR;
-  }
+  };
+  if (down)
+    march(std::true_type{});
+  else
+    march(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -264,6 +331,7 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   constexpr int V = Vec16<T>::N, YO = NW - 4;
   StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
+  a.nt = tune.nontemporal ? 1 : 0;
   const int rxm = int(dom.radius().x(-1));
   const int off = ((a.lox - rxm) % V + V) % V;
   a.x0 = a.lox - off;

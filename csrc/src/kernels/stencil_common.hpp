@@ -53,6 +53,7 @@ template <typename T> struct StencilArgs {
   // halo forwarding (FWD kernels): cells within fwm[a] of the low face send along -a, within fwp[a] of the high
   // face along +a; the receiving halo cell of direction k = (dx+1) + 3(dy+1) + 9(dz+1) is at (own output address +
   // fd[k]) for every k set in fmask (receivers with our pitches; the rest is copied after the kernel)
+  int nt;   // non-temporal output stores (block-uniform)
   int flip; // reverse every block's z-march direction (alternated per step, see StencilTune::alternateZ)
   int fwm[3], fwp[3];
   uint32_t fmask;

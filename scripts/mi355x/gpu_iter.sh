@@ -1,11 +1,10 @@
 #!/bin/bash
-# iteration loop: correctness, tuning sweep, bench, kernel profile
+# one iteration on the GPU: selected GPU tests (PYTEST_K), kernel sweep (SWEEP, bench_stencil --only), bench
+set -o pipefail
 export STENCIL_SKIP_BUILD=1 STENCIL_PLAN_FILE=0 PYTHONPATH=$GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 120 ./build/bin/stencil_ctest --all > gpurun_out/ctest.log 2>&1 || { echo "ctest failed"; tail gpurun_out/ctest.log; exit 1; }
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail gpurun_out/smoke.log; exit 1; }
-timeout -k 10 600 python scripts/mi355x/tune_jacobi.py 512 > gpurun_out/tune.log 2>&1 || { echo tune failed; tail gpurun_out/tune.log; exit 1; }
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench1.log 2>&1
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --exchange-iters 5 > gpurun_out/prof/bench.log 2>&1
+mkdir -p gpurun_out/iter
+step() { local name=$1 lim=$2; shift 2; echo "== $name"; timeout -k 10 $lim "$@" > gpurun_out/iter/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; grep -v amdgpu.ids gpurun_out/iter/$name.log | tail -${TAILN:-4} | cut -c1-400; return $rc; }
+step pytest 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "${PYTEST_K:-temporal or special}" &&
+for s in ${SWEEP:-x2 x2pp}; do TAILN=40 step sweep_$s 200 ./build/bin/bench_stencil --only $s || exit 1; done &&
+step bench 300 python bench.py --steps 64 --warmup 16
 echo "done rc=$?"

@@ -175,6 +175,42 @@ def test_jacobi_temporal2_matches_oracle(st, size, gpus, fp64, shape):
         assert torch.equal(_gather(m), u), f"after run({n})"
 
 
+@pytest.mark.parametrize("temporal", [1, 2])
+@pytest.mark.parametrize("kind", ["jacobi", "astaroth"])
+def test_stencil_special_values_bitwise(st, temporal, kind):
+    """Fields with signed zeros, values below 2^-100 (the exact-/6 slow path), subnormals and mixed signs: the packed
+    fp32 sums and the FMA division must stay bitwise equal to the torch oracle (0-started sums, IEEE division)."""
+    from stencil2_amd.ops import astaroth_step_reference
+    size = (72, 20, 18)
+    if kind == "jacobi":
+        m = st.Jacobi3D(size, gpus=[0, 0], temporal=temporal)
+        ref = jacobi_step_reference
+    else:
+        m = st.AstarothSim(size, quantities=1, gpus=[0, 0], temporal=temporal)
+        ref = astaroth_step_reference
+    m.init()
+    g = torch.Generator().manual_seed(7)
+    pool = torch.tensor([0.0, -0.0, 1e-35, -1e-35, 3e-39, -3e-39, 1e-45, 0.5, -0.25, 7.0], dtype=torch.float32)
+    dd = m.domain
+    for di in range(dd.num_domains()):
+        it = m.interior(di)
+        idx = torch.randint(0, len(pool), tuple(it.shape), generator=g)
+        vals = pool[idx] * torch.where(torch.rand(tuple(it.shape), generator=g) < 0.3,
+                                       torch.rand(tuple(it.shape), generator=g), torch.ones(()))
+        # whole planes of zeros and of tiny values, so some six-neighbour sums are exactly +-0 or tiny
+        vals[3:6] = -0.0
+        vals[8:10] = 2e-36
+        it.copy_(vals.to(it.device))
+    torch.cuda.synchronize()
+    u = _gather(m)
+    m.run(4)
+    for _ in range(4):
+        u = ref(u)
+    m.synchronize()
+    got = _gather(m)
+    assert torch.equal(got.view(torch.int32), u.view(torch.int32)), int((got.view(torch.int32) != u.view(torch.int32)).sum())
+
+
 @pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy"])
 def test_jacobi_temporal2_transports(st, methods):
     """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs"""
