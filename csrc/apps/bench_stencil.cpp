@@ -219,8 +219,8 @@ int main(int argc, char **argv) {
     jacobi_init(l2, 0, l2.get_full_region(), s);
     s.sync();
     for (int nw : {12, 16})
-      for (int pf : {2, 3})
-        for (int zc : {0, 32, 43, 52, 64, 86, 128}) {
+      for (int pf : {1, 2, 3})
+        for (int zc : {0, 43, 64, 128}) {
           StencilTune t;
           t.x2nw = nw;
           t.x2pf = pf;

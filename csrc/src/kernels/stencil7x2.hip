@@ -21,6 +21,7 @@
 #include <map>
 #include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "stencil/rt/hip_check.hpp"
 #include "stencil_common.hpp"
@@ -97,6 +98,11 @@ template <typename T, typename X, int N> __device__ __forceinline__ X div6v(cons
   }
 }
 
+// calls f(integral_constant<I>) for I = 0, 1, ... while it returns true; true if all did
+template <typename F, int... I> __device__ __forceinline__ bool run_phases(F &f, std::integer_sequence<int, I...>) {
+  return (f(std::integral_constant<int, I>{}) && ...);
+}
+
 // Block = NW waves, ONE src row per wave: the block's src rows are [yblk-2, yblk-2+NW); u1 is valid on the inner
 // NW-2 of them and u2 (the output) on the inner NW-4, so the block writes YO = NW-4 rows and every wave runs the
 // same code (the two outer rows on each side are a redundant y halo, re-read from L2 by the neighbouring block).
@@ -141,9 +147,14 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1; // outer waves: garbage u1, never consumed
 
   const int yc = y < 0 ? 0 : (y > a.rawYm1 ? a.rawYm1 : y);
-  const T *rowbase = a.src + int64_t(yc) * a.px + xb;
+  // addresses = wave-uniform plane base (SGPRs) + a 32-bit per-lane byte offset within the plane, so the loads and
+  // stores use the saddr + voffset form and each lane holds one offset VGPR instead of 64-bit pointers
+  const uint32_t rowoff = uint32_t((yc * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+  const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
   auto zcl = [&](int zz) { return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz); };
-  auto rowp = [&](int zz) -> const T * { return rowbase + int64_t(zcl(zz)) * a.pxy; };
+  auto rowp = [&](int zz) -> const T * {
+    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy) + rowoff);
+  };
   // sphere membership of the row at plane P: y/z part once per row, per-cell test only for the few hit rows
   struct RowSph {
     int dh, dc;
@@ -188,30 +199,31 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
     constexpr bool DOWN = decltype(downTag)::value;
     constexpr int dz = DOWN ? -1 : 1;
     const int z0 = DOWN ? ze - 1 : zs;
-    // ---- windows ----
-    NV C[NC];             // src planes z + k dz, k = 0 .. NC-1 (the last PF in flight)
+    // ---- windows: a ring of NC src planes; the step of phase k (t+2 = k mod NC) finds plane z + j dz in slot
+    // (k+j) mod NC. The loop is unrolled over the NC phases, so a plane's registers never move while its load is
+    // in flight (a register rotation would force a wait on the load right after issuing it). ----
+    NV C[NC];             // src rows
     T CL[NC], CR[NC];     // src at x-1 / x+V (edge lanes)
-    T LLa, RRa, LLb, RRb; // src at x-2 / x+V+1: plane z+dz (a), plane z+2dz (b, in flight)
+    T LL[NC], RR[NC];     // src at x-2 / x+V+1 (edge lanes)
     NV Ub, Uc, Ua;        // u1 planes z-dz, z, z+dz
     P2 UcE, UaE;          // u1 at (x-1, x+V), planes z and z+dz
-    auto load_row = [&](int zz, NV &v, T &L, T &R) {
+    auto load_row = [&](int zz, int k) {
       const T *p = rowp(zz);
-      v = *reinterpret_cast<const NV *>(p);
-      L = edgeL ? p[-1] : T(0);
-      R = edgeR ? p[V] : T(0);
-    };
-    auto load_outer = [&](int zz, T &L2, T &R2) {
-      const T *p = rowp(zz);
-      L2 = edgeL ? p[-2] : T(0);
-      R2 = edgeR ? p[V + 1] : T(0);
+      // every lane loads the edge scalars (in-row addresses, same cache lines as the chunk; only the edge lanes
+      // use them): masked loads would sit behind exec branches, and the waitcnt pass, counting the path that skips
+      // them, would then wait on this step's own loads and void the lookahead
+      C[k] = *reinterpret_cast<const NV *>(p);
+      CL[k] = p[-1];
+      CR[k] = p[V];
+      LL[k] = p[-2];
+      RR[k] = p[V + 1];
     };
 
-    // warm-up: the loop starts two planes early (t = -2: u1 only), window planes z0-2dz .. z0+(PF-1)dz
+    // warm-up: the loop starts two planes early (t = -2: u1 only), window planes z0-2dz .. z0+(NC-2)dz
     {
       const int zw = z0 - 2 * dz;
 #pragma unroll
-      for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, C[k], CL[k], CR[k]);
-      load_outer(zw + dz, LLa, RRa);
+      for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, k);
       cs[0][w][lane] = C[1];
       if (edgeL) ce[0][w][0] = CL[1];
       if (edgeR) ce[0][w][1] = CR[1];
@@ -219,22 +231,25 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
     }
 
     int buf = 0;
-    for (int t = -2; t < nzs; ++t) {
+    int t = -2;
+    auto step = [&](auto phase) -> bool {
+      constexpr int k = decltype(phase)::value;
+      constexpr int s0 = k % NC, s1 = (k + 1) % NC, s2 = (k + 2) % NC, sn = (k + NC - 1) % NC;
+      if (t >= nzs) return false;
       const int z = z0 + t * dz;
       const int P = z + dz;
-      // 1. lookahead loads
-      load_row(z + (NC - 1) * dz, C[NC - 1], CL[NC - 1], CR[NC - 1]);
-      load_outer(z + 2 * dz, LLb, RRb);
+      // 1. lookahead load into the slot of the plane that died last step
+      load_row(z + (NC - 1) * dz, sn);
       // 2. u1 at plane z+dz (row + the two edge cells as one pair)
       const NV cA = cs[buf][wA][lane], cB = cs[buf][wB][lane];
-      const T cAL = edgeL ? ce[buf][wA][0] : T(0), cAR = edgeR ? ce[buf][wA][1] : T(0);
-      const T cBL = edgeL ? ce[buf][wB][0] : T(0), cBR = edgeR ? ce[buf][wB][1] : T(0);
+      const T cAL = ce[buf][wA][0], cAR = ce[buf][wA][1]; // LDS broadcasts
+      const T cBL = ce[buf][wB][0], cBR = ce[buf][wB][1];
       {
         const RowSph rs = row_sph(P);
-        Ua = apply_row(C[1], cA, cB, DOWN ? C[0] : C[2], DOWN ? C[2] : C[0], CL[1], CR[1], rs);
-        const P2 epx = {C[1][0], RRa}, emx = {LLa, C[1][V - 1]}, epy = {cBL, cBR}, emy = {cAL, cAR};
-        const P2 ezp = DOWN ? P2{CL[0], CR[0]} : P2{CL[2], CR[2]};
-        const P2 ezm = DOWN ? P2{CL[2], CR[2]} : P2{CL[0], CR[0]};
+        Ua = apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], CL[s1], CR[s1], rs);
+        const P2 epx = {C[s1][0], RR[s1]}, emx = {LL[s1], C[s1][V - 1]}, epy = {cBL, cBR}, emy = {cAL, cAR};
+        const P2 ezp = DOWN ? P2{CL[s0], CR[s0]} : P2{CL[s2], CR[s2]};
+        const P2 ezm = DOWN ? P2{CL[s2], CR[s2]} : P2{CL[s0], CR[s0]};
         UaE = div6v<T, P2, 2>(sum6v<T, KIND>(epx, emx, epy, emy, ezp, ezm));
         if (KIND == 0 && rs.hit) {
           UaE[0] = fix(rs, xb - 1, UaE[0]);
@@ -246,7 +261,7 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
         const NV uA = us[buf][wA][lane], uB = us[buf][wB][lane];
         const NV o = apply_row(Uc, uA, uB, DOWN ? Ub : Ua, DOWN ? Ua : Ub, UcE[0], UcE[1], row_sph(z));
         if (outRow) {
-          T *dp = a.dst + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+          T *dp = reinterpret_cast<T *>(reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff);
           if (fullX) {
             if (a.nt)
               __builtin_nontemporal_store(o, reinterpret_cast<NV *>(dp));
@@ -261,24 +276,20 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
       }
       // 4. publish src plane z+2dz and u1 plane z+dz
       const int nbuf = buf ^ 1;
-      cs[nbuf][w][lane] = C[2];
-      if (edgeL) ce[nbuf][w][0] = CL[2];
-      if (edgeR) ce[nbuf][w][1] = CR[2];
+      cs[nbuf][w][lane] = C[s2];
+      if (edgeL) ce[nbuf][w][0] = CL[s2];
+      if (edgeR) ce[nbuf][w][1] = CR[s2];
       us[nbuf][w][lane] = Ua;
       __syncthreads();
       buf = nbuf;
-      // 5. rotate
-#pragma unroll
-      for (int k = 0; k < NC - 1; ++k) {
-        C[k] = C[k + 1];
-        CL[k] = CL[k + 1];
-        CR[k] = CR[k + 1];
-      }
-      LLa = LLb;
-      RRa = RRb;
+      // 5. the u1 window (computed values: plain moves)
       Ub = Uc;
       Uc = Ua;
       UcE = UaE;
+      ++t;
+      return true;
+    };
+    while (run_phases(step, std::make_integer_sequence<int, NC>{})) {
     }
   };
   if (down)
@@ -368,19 +379,19 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   // shapes (rows per lane, waves per block, min waves/SIMD): 1x8 keeps everything in registers at 6 waves/SIMD;
   // 2x4 at 3 waves/SIMD; 2x8 at 4 (spills)
   // shape = waves per block (one src row each; NW-4 output rows) x planes of z lookahead
-  const int shape = (tune.x2nw == 8 ? 0 : (tune.x2nw == 12 ? 3 : 6)) + (tune.x2pf <= 2 ? 0 : (tune.x2pf == 3 ? 1 : 2));
+  const int shape = (tune.x2nw == 8 ? 0 : (tune.x2nw == 12 ? 3 : 6)) + (tune.x2pf <= 1 ? 0 : (tune.x2pf == 2 ? 1 : 2));
 #define X2_LAUNCH(TT, K)                                                                                           \
   do {                                                                                                             \
     switch (shape) {                                                                                               \
-    case 0: apply_x2_t<TT, K, 8, 2>(dom, qi, region, sph, stream, tune); break;                                    \
-    case 1: apply_x2_t<TT, K, 8, 3>(dom, qi, region, sph, stream, tune); break;                                    \
-    case 2: apply_x2_t<TT, K, 8, 4>(dom, qi, region, sph, stream, tune); break;                                    \
-    case 3: apply_x2_t<TT, K, 12, 2>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 4: apply_x2_t<TT, K, 12, 3>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 5: apply_x2_t<TT, K, 12, 4>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 6: apply_x2_t<TT, K, 16, 2>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 7: apply_x2_t<TT, K, 16, 3>(dom, qi, region, sph, stream, tune); break;                                   \
-    default: apply_x2_t<TT, K, 16, 4>(dom, qi, region, sph, stream, tune); break;                                  \
+    case 0: apply_x2_t<TT, K, 8, 1>(dom, qi, region, sph, stream, tune); break;                                    \
+    case 1: apply_x2_t<TT, K, 8, 2>(dom, qi, region, sph, stream, tune); break;                                    \
+    case 2: apply_x2_t<TT, K, 8, 3>(dom, qi, region, sph, stream, tune); break;                                    \
+    case 3: apply_x2_t<TT, K, 12, 1>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 4: apply_x2_t<TT, K, 12, 2>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 5: apply_x2_t<TT, K, 12, 3>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 6: apply_x2_t<TT, K, 16, 1>(dom, qi, region, sph, stream, tune); break;                                   \
+    case 7: apply_x2_t<TT, K, 16, 2>(dom, qi, region, sph, stream, tune); break;                                   \
+    default: apply_x2_t<TT, K, 16, 3>(dom, qi, region, sph, stream, tune); break;                                  \
     }                                                                                                              \
   } while (0)
   if (f32) {
