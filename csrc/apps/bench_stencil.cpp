@@ -193,13 +193,16 @@ int main(int argc, char **argv) {
     jacobi_init(l2, 0, l2.get_full_region(), s);
     fill_value(l2, 0, 0.5, false, s);
     s.sync();
-    for (int nt = 0; nt < 2; ++nt)
-      for (int alt = 0; alt < 2; ++alt)
-        for (int zc : {0, 64}) {
+    for (int nw : {12, 16})
+      for (int pf : {1, 2, 3})
+        for (int zc : {0, 64, 128}) {
+          const int nt = 1, alt = 1;
           StencilTune t;
           t.nontemporal = nt;
           t.alternateZ = alt;
           t.zchunk = zc;
+          t.x2nw = nw;
+          t.x2pf = pf;
           const double us = timeit([&] {
             stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t);
             l2.swap();

@@ -1,0 +1,14 @@
+#!/bin/bash
+# PMC counters (one pass per counter group) of one launch of each default stencil kernel (bench_stencil --only one)
+set -o pipefail
+export STENCIL_SKIP_BUILD=1 STENCIL_PLAN_FILE=0 PYTHONPATH=$GRAFT_REPO_ROOT
+OUT=gpurun_out/pmc
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+i=0
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"; do
+  i=$((i+1))
+  timeout -s KILL 60 rocprofv3 --pmc $pmc --output-format csv -d $OUT/p$i -o run -- ./build/bin/bench_stencil --only one --iters 2 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $OUT/p$i.log; exit 1; }
+done
+python3 scripts/mi355x/summarize_pmc.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
