@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--nt", type=int, default=1, help="non-temporal stencil stores")
     ap.add_argument("--altz", type=int, default=1, help="alternate the z-march direction every step")
     ap.add_argument("--ty", type=int, default=2, help="rows per lane of the stencil kernel (2/4/8)")
+    ap.add_argument("--variant", type=int, default=2,
+                    help="single-step kernel variant (2: VALU LDS z-march, 8: MFMA x-line update; needs --temporal 1)")
     ap.add_argument("--nw", type=int, default=8, help="waves per block of the stencil kernel")
     ap.add_argument("--x2nw", type=int, default=16, help="waves per block of the fused two-step kernel (8/12/16)")
     ap.add_argument("--x2pf", type=int, default=2, help="planes of z lookahead of the fused two-step kernel (2/3/4)")
@@ -85,6 +87,7 @@ def main():
     tune.alternate_z = bool(args.altz)
     tune.ty = args.ty
     tune.nw = args.nw
+    tune.variant = args.variant
     tune.x2nw = args.x2nw
     tune.x2pf = args.x2pf
     tune.zchunk = args.zchunk
@@ -143,7 +146,7 @@ def main():
                        "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
                        "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods),
                        "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
-                       "ty": args.ty, "nw": args.nw, "x2nw": args.x2nw, "x2pf": args.x2pf, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1},
+                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
                       "gcells_per_gpu": round(gcells / n, 3)},

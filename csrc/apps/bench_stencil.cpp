@@ -169,10 +169,25 @@ int main(int argc, char **argv) {
       std::printf("%s,0,2,%d,%.2f,%.1f,%.3f\n", names[mode], zc, us, cells / us / 1e3, cells * 8 / us / 1e6);
     }
   }
+  for (int rep = 0; rep < reps; ++rep)
+  if (only.empty() || only == "mfma") {
+    // the matrix-core line update (x pair on MFMA) against the VALU single step on the same domain
+    for (int zc : {0, 16, 64}) {
+      StencilTune t;
+      t.variant = StencilTune::kMfma;
+      t.zchunk = zc;
+      const double us = timeit([&] { stencil7_apply(ld, 0, reg, StencilKind::Jacobi, sph, s, t); });
+      std::printf("stencil7_mfma,%d,0,%d,%.2f,%.1f,%.3f\n", StencilTune::kMfma, zc, us, cells / us / 1e3,
+                  cells * 8 / us / 1e6);
+    }
+  }
   if (only == "one") {
-    // one launch of each default kernel (single step v2, fused pair) for counter collection
+    // one launch of each default kernel (single step v2, fused pair, MFMA variant) for counter collection
     StencilTune t;
     timeit([&] { stencil7_apply(ld, 0, reg, StencilKind::Jacobi, sph, s, t); });
+    StencilTune tm;
+    tm.variant = StencilTune::kMfma;
+    timeit([&] { stencil7_apply(ld, 0, reg, StencilKind::Jacobi, sph, s, tm); });
     LocalDomain l2(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
     l2.set_radius(Radius::face_edge_corner(2, 1, 0));
     l2.add_data<float>("d");

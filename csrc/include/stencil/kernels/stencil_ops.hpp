@@ -41,6 +41,8 @@ struct StencilTune {
   //    3/4: 3/4 planes), 0: LDS kernel with 1 plane (the loads are consumed in the step that issues them),
   //    1: register-only kernel. 512^3 fp32 on one MI355X: 201 us (v2) vs 212 us (v0) per sweep.
   int variant = 2;
+  // variant kMfma: the x line update on the matrix cores (stencil7_mfma.hip; fp32 Jacobi, for counter comparison)
+  static constexpr int kMfma = 8;
   int ty = 2;     // rows per lane (variant 0: 2/4/8, variant 1: 4/8)
   int zchunk = 0; // planes per block (0 = auto: exactly one round of resident blocks)
   int nw = 8;     // waves per block stacked in y (deep-lookahead variants: 4/8/16)
@@ -109,6 +111,10 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
 bool stencil7x2_supported(const LocalDomain &dom, int64_t qi);
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune = StencilTune());
+// MFMA variant of the single step (fp32 Jacobi; StencilTune::variant == kMfma routes stencil7_apply here)
+bool stencil7_mfma_supported(const LocalDomain &dom, int64_t qi);
+void stencil7_mfma_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
+                         hipStream_t stream, const StencilTune &tune = StencilTune());
 // same for several regions in one call (e.g. the exterior slabs)
 void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
                             const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());

@@ -916,6 +916,11 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
   STENCIL_REQUIRE(region.empty() || (cr.contains(region.lo) && region.hi.all_ge(region.lo) &&
                                      region.hi.x <= cr.hi.x && region.hi.y <= cr.hi.y && region.hi.z <= cr.hi.z),
                   "stencil region " << region << " outside compute region " << cr);
+  if (tune.variant == StencilTune::kMfma) {
+    STENCIL_REQUIRE(fwd == nullptr, "the MFMA variant does not forward halos");
+    stencil7_mfma_apply(dom, qi, region, kind, sph, stream, tune);
+    return;
+  }
   const DType dt = dom.dtype(qi);
   const bool f32 = dt == DType::F32 || (dt == DType::Bytes && dom.elem_size(qi) == 4);
   const bool f64 = dt == DType::F64 || (dt == DType::Bytes && dom.elem_size(qi) == 8);

@@ -175,6 +175,45 @@ def test_jacobi_temporal2_matches_oracle(st, size, gpus, fp64, shape):
         assert torch.equal(_gather(m), u), f"after run({n})"
 
 
+@pytest.mark.parametrize("size", [(32, 32, 32), (67, 45, 33), (130, 70, 20)])
+@pytest.mark.parametrize("gpus", [[0], [0, 0]])
+def test_jacobi_mfma_variant_matches_oracle(st, size, gpus):
+    """The matrix-core x-line update (StencilTune.variant = 8) is bitwise equal to the torch oracle: the banded
+    16x16x4 fp32 MFMA sums exactly two exact products per output (a single rounding of vpx + vmx)."""
+    t = st.StencilTune()
+    t.variant = 8
+    m = st.Jacobi3D(size, gpus=gpus, temporal=1, tune=t)
+    m.init()
+    u = _gather(m)
+    m.run(3)
+    for _ in range(3):
+        u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
+def test_jacobi_mfma_variant_special_values(st):
+    """signed zeros, tiny and subnormal values through the MFMA band product (finite inputs)"""
+    t = st.StencilTune()
+    t.variant = 8
+    m = st.Jacobi3D((72, 20, 18), gpus=[0], temporal=1, tune=t)
+    m.init()
+    g = torch.Generator().manual_seed(3)
+    pool = torch.tensor([0.0, -0.0, 1e-35, -1e-35, 3e-39, -3e-39, 1e-45, 0.5, -0.25, 7.0], dtype=torch.float32)
+    it = m.interior(0)
+    vals = pool[torch.randint(0, len(pool), tuple(it.shape), generator=g)]
+    vals[3:6] = -0.0
+    it.copy_(vals.to(it.device))
+    torch.cuda.synchronize()
+    u = _gather(m)
+    m.run(2)
+    for _ in range(2):
+        u = jacobi_step_reference(u)
+    m.synchronize()
+    got = _gather(m)
+    assert torch.equal(got.view(torch.int32), u.view(torch.int32)), int((got.view(torch.int32) != u.view(torch.int32)).sum())
+
+
 @pytest.mark.parametrize("temporal", [1, 2])
 @pytest.mark.parametrize("kind", ["jacobi", "astaroth"])
 def test_stencil_special_values_bitwise(st, temporal, kind):
