@@ -82,6 +82,50 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # Transport pre-flight (multi-process only): one exchange of a coordinate-encoded field on a small grid with the
+    # model's radius and methods, checked cell by cell on every rank (the reference tests' oracle). If any rank sees
+    # a wrong halo or an error, every rank drops the co-located IPC path and uses RCCL instead, so a scaling run
+    # never times silently corrupted halos.
+    preflight = "skipped"
+    if world > 1:
+        from stencil2_amd.utils.testing import check_exchange, fill_coords
+
+        bad = 0
+        try:
+            pl = st.DistributedDomain(*(3 * [max(24, L // 8)]), group=pg)
+            r = st.Radius.constant(0)
+            r.set_face(2 if args.temporal >= 2 else 1)
+            if args.temporal >= 2:
+                r.set_edge(1)
+            pl.set_radius(r)
+            q = pl.add_data("coords", torch.int32)
+            pl.set_methods(methods)
+            pl.set_gpus([device])
+            pl.realize()
+            for it in range(2):
+                fill_coords(pl, q, offset=it)
+                pl.exchange()
+                torch.cuda.synchronize()
+                bad += check_exchange(pl, q, r, offset=it)
+            del pl
+        except Exception as e:  # noqa: BLE001 - any failure means: do not trust this transport set
+            print(f"rank {rank}: transport pre-flight failed: {e}", file=sys.stderr, flush=True)
+            bad += 1 << 20
+        if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # exercises the fallback (rehearsal scripts)
+            bad += 1
+        tb = torch.tensor([bad], dtype=torch.int64, device=red_dev)
+        dist.all_reduce(tb, op=dist.ReduceOp.SUM)
+        if int(tb.item()) == 0:
+            preflight = "ok"
+        else:
+            preflight = f"failed ({int(tb.item())} bad cells); colocated disabled"
+            methods = st.MethodFlags(int(methods) & ~int(st.MethodFlags.Colocated))
+            if shared:  # ranks sharing a GPU (rehearsal): RCCL refuses two ranks on one device
+                methods = st.MethodFlags(int(methods) & ~int(st.MethodFlags.Rccl) | int(st.MethodFlags.Staged))
+            if rank == 0:
+                print(f"transport pre-flight: {preflight}", file=sys.stderr, flush=True)
+        barrier()
+
     tune = st.StencilTune()
     tune.nontemporal = bool(args.nt)
     tune.alternate_z = bool(args.altz)
@@ -144,7 +188,7 @@ def main():
             "data": "synthetic (reference Jacobi3D initial condition: 0.5 + hot/cold spheres)",
             "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": L,
                        "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
-                       "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods),
+                       "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods), "preflight": preflight,
                        "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
                        "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
