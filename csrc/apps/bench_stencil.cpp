@@ -197,6 +197,37 @@ int main(int argc, char **argv) {
     return 0;
   }
   for (int rep = 0; rep < reps; ++rep)
+  if (only == "ext") {
+    // overlapped fused pair pieces on a depth-2 domain: whole sweep, interior sweep, exterior (thin-slab kernels)
+    LocalDomain l2(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
+    l2.set_radius(Radius::face_edge_corner(2, 1, 0));
+    l2.add_data<float>("d");
+    l2.realize();
+    jacobi_init(l2, 0, l2.get_full_region(), s);
+    s.sync();
+    const Rect3 c = l2.get_compute_region();
+    for (int sx : {2, 4}) {
+    const Rect3 in(c.lo + Dim3(sx, 2, 2), c.hi - Dim3(sx, 2, 2));
+    std::printf("# interior shrink x=%d\n", sx);
+    StencilTune t;
+    const double whole = timeit([&] { stencil7x2_apply(l2, 0, c, StencilKind::Jacobi, sph, s, t); });
+    const double inner = timeit([&] { stencil7x2_apply(l2, 0, in, StencilKind::Jacobi, sph, s, t); });
+    const double outer = timeit([&] { stencil7x2_apply_exterior(l2, 0, in, StencilKind::Jacobi, sph, s, t); });
+    Stream s2(0, Priority::HIGH);
+    Event e(0);
+    const double both = timeit([&] {
+      e.record(s);
+      e.wait_on(s2);
+      stencil7x2_apply_exterior(l2, 0, in, StencilKind::Jacobi, sph, s2, t);
+      stencil7x2_apply(l2, 0, in, StencilKind::Jacobi, sph, s, t);
+      e.record(s2);
+      e.wait_on(s);
+    });
+    std::printf("x2_whole,0,0,0,%.2f,0,0\nx2_interior,0,0,0,%.2f,0,0\nx2_exterior,0,0,0,%.2f,0,0\nx2_int+ext_concurrent,0,0,0,%.2f,0,0\n",
+                whole, inner, outer, both);
+    }
+  }
+  for (int rep = 0; rep < reps; ++rep)
   if (only == "x2pp") {
     // the fused pair as the model runs it: ping-pong (swap after every launch), so every launch reads what the
     // previous one wrote; non-temporal stores and the alternating z-march on/off

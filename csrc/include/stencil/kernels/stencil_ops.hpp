@@ -111,6 +111,13 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
 bool stencil7x2_supported(const LocalDomain &dom, int64_t qi);
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune = StencilTune());
+// S o S on several small regions (the exterior slabs of an overlapped fused pair), one thread per cell
+void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
+                              const Spheres &sph, hipStream_t stream);
+// S o S on the compute region minus `interior` (the exterior of an overlapped fused pair): z slabs and y slabs by
+// the sweep kernel (6 waves per block for 2-row slabs), thin x slabs by a lanes-on-rows kernel
+void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &interior, StencilKind kind,
+                               const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());
 // MFMA variant of the single step (fp32 Jacobi; StencilTune::variant == kMfma routes stencil7_apply here)
 bool stencil7_mfma_supported(const LocalDomain &dom, int64_t qi);
 void stencil7_mfma_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,

@@ -298,6 +298,156 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
     march(std::false_type{});
 }
 
+// S o S on a few small boxes (the exterior slabs of an overlapped step: interior sweep during the exchange, these
+// after it). One thread per output cell: u2 = S of the six u1 neighbours, each u1 = S of its six src neighbours,
+// in the single step's summation order with the exact /6 and the spheres, i.e. the same bits as the sweep kernel
+// (whose u1 of a halo cell equals the neighbour's own u1 there, as two single steps with an exchange between).
+constexpr int kMaxX2Regions = 8;
+struct X2Regions {
+  int lo[kMaxX2Regions][3];
+  int ext[kMaxX2Regions][3];
+  int64_t begin[kMaxX2Regions + 1];
+  int n;
+};
+
+template <typename T, int KIND>
+__global__ __launch_bounds__(256) void stencil7x2_regions_kernel(StencilArgs<T> a, X2Regions rt) {
+  const int64_t total = rt.begin[rt.n];
+  const int64_t px = a.px, pxy = a.pxy;
+  auto u1 = [&](int x, int y, int z) -> T {
+    const T *p = a.src + int64_t(z) * pxy + int64_t(y) * px + x;
+    const T v = sum6<T, KIND>(p[1], p[-1], p[px], p[-px], p[pxy], p[-pxy]); // sum6 includes the exact /6
+    return KIND == 0 ? sphere_fix(a, x, y, z, v) : v;
+  };
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+    int k = 0;
+    while (k + 1 < rt.n && rt.begin[k + 1] <= i) ++k;
+    const int64_t li = i - rt.begin[k];
+    const int nx = rt.ext[k][0], ny = rt.ext[k][1];
+    const int x = rt.lo[k][0] + int(li % nx);
+    const int y = rt.lo[k][1] + int((li / nx) % ny);
+    const int z = rt.lo[k][2] + int(li / (int64_t(nx) * ny));
+    const T vpx = u1(x + 1, y, z), vmx = u1(x - 1, y, z), vpy = u1(x, y + 1, z), vmy = u1(x, y - 1, z);
+    const T vpz = u1(x, y, z + 1), vmz = u1(x, y, z - 1);
+    T v = sum6<T, KIND>(vpx, vmx, vpy, vmy, vpz, vmz);
+    if (KIND == 0) v = sphere_fix(a, x, y, z, v);
+    a.dst[int64_t(z) * pxy + int64_t(y) * px + x] = v;
+  }
+}
+
+// S o S on thin slabs (the exterior of an overlapped fused pair: thickness <= NT along axis THIN). A z march over a
+// 2-cell slab has too little parallelism and a chunk-per-lane sweep leaves most lanes idle on x slabs, so each wave
+// takes a short tile: lanes along axis LANE (60 outputs + a 2-lane halo each side, neighbours by DPP), the slab's
+// thin extent plus 2 cells each side in registers, and BC planes (+2 each side) along axis MARCH, all loaded up
+// front (one memory round trip per wave). u1 on the tile interior, then u2 on the slab; sums in the reference
+// order +x,-x,+y,-y,+z,-z whatever the roles of the axes, exact /6 and spheres as the sweep: the same bits.
+constexpr int kThinBC = 4;
+struct ThinTable {
+  int lo[2][3], hi[2][3]; // raw boxes (up to two slabs of one orientation)
+  int wbegin[3];
+  int n;
+};
+
+template <int THIN, int LANE, int MARCH, int AX, int SGN, typename T, int N0, int N1>
+__device__ __forceinline__ T thin_nbr(const T (&v)[N0][N1], int ti, int bi) {
+  if constexpr (AX == THIN)
+    return v[ti + SGN][bi];
+  else if constexpr (AX == MARCH)
+    return v[ti][bi + SGN];
+  else
+    return SGN > 0 ? from_next_lane<T>(v[ti][bi]) : from_prev_lane<T>(v[ti][bi]);
+}
+
+template <typename T, int KIND, int THIN, int LANE, int MARCH, int NT>
+__global__ __launch_bounds__(256) void stencil7x2_thin_kernel(StencilArgs<T> a, ThinTable tb) {
+  constexpr int NTV = NT + 4, NB = kThinBC + 4; // src window: thin cells t0-2 .. t0+NT+1, planes b0-2 .. b0+BC+1
+  const int wave = int(blockIdx.x) * 4 + int(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wave >= tb.wbegin[tb.n]) return; // wave-uniform
+  const int k = (tb.n > 1 && wave >= tb.wbegin[1]) ? 1 : 0;
+  const int lw = wave - tb.wbegin[k];
+  const int ng = (tb.hi[k][LANE] - tb.lo[k][LANE] + 59) / 60;
+  const int g = lw % ng, bb = lw / ng;
+  const int t0 = tb.lo[k][THIN], nt = tb.hi[k][THIN] - t0;
+  const int b0 = tb.lo[k][MARCH] + bb * kThinBC;
+  const int cl = tb.lo[k][LANE] - 2 + 60 * g + lane;
+  const int64_t st[3] = {1, a.px, a.pxy};
+  const int rawm1[3] = {int(a.px) - 1, a.rawYm1, a.rawZm1};
+  auto clampc = [&](int c, int ax) { return c < 0 ? 0 : (c > rawm1[ax] ? rawm1[ax] : c); };
+  const T *lp = a.src + int64_t(clampc(cl, LANE)) * st[LANE];
+  T v[NTV][NB];
+  if constexpr (THIN == 0) {
+    // x slabs: each lane's thin window is contiguous in its row. Load it as aligned 16-B vectors (one cache line
+    // per row and plane instead of one per value: the lanes sit on 64 different rows) and pick the window out with
+    // a wave-uniform offset
+    using NV = typename Vec16<T>::native;
+    constexpr int V = Vec16<T>::N;
+    const int xw = t0 - 2;                                      // first x of the window (raw)
+    const int xa = xw - (((xw - a.x0) % V) + V) % V;            // a.x0: a 16-B aligned raw x
+    const int off = xw - xa;                                    // 0 .. V-1, wave-uniform
+    auto fill = [&](auto offTag) {
+      constexpr int O = decltype(offTag)::value;
+      constexpr int NL = (NTV + O + V - 1) / V; // vectors covering the window (never past it by a whole vector)
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi) {
+        const T *pp = lp + int64_t(clampc(b0 - 2 + bi, MARCH)) * st[MARCH] + xa;
+        NV w[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) w[j] = *reinterpret_cast<const NV *>(pp + j * V);
+#pragma unroll
+        for (int ti = 0; ti < NTV; ++ti) v[ti][bi] = w[(ti + O) / V][(ti + O) % V];
+      }
+    };
+    if constexpr (V == 4) {
+      switch (off) {
+      case 0: fill(std::integral_constant<int, 0>{}); break;
+      case 1: fill(std::integral_constant<int, 1>{}); break;
+      case 2: fill(std::integral_constant<int, 2>{}); break;
+      default: fill(std::integral_constant<int, 3>{}); break;
+      }
+    } else {
+      if (off == 0)
+        fill(std::integral_constant<int, 0>{});
+      else
+        fill(std::integral_constant<int, 1>{});
+    }
+  } else {
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi) {
+      const T *pp = lp + int64_t(clampc(b0 - 2 + bi, MARCH)) * st[MARCH];
+#pragma unroll
+      for (int ti = 0; ti < NTV; ++ti) v[ti][bi] = pp[int64_t(clampc(t0 - 2 + ti, THIN)) * st[THIN]];
+    }
+  }
+  auto coord = [&](int ax, int ti, int bi) { return ax == THIN ? t0 - 2 + ti : (ax == MARCH ? b0 - 2 + bi : cl); };
+  // u1 on thin cells t0-1 .. t0+NT, planes b0-1 .. b0+BC (array index = src index - 1)
+  T u[NTV - 2][NB - 2];
+#pragma unroll
+  for (int ti = 1; ti < NTV - 1; ++ti)
+#pragma unroll
+    for (int bi = 1; bi < NB - 1; ++bi) {
+      T r = sum6<T, KIND>(thin_nbr<THIN, LANE, MARCH, 0, 1>(v, ti, bi), thin_nbr<THIN, LANE, MARCH, 0, -1>(v, ti, bi),
+                          thin_nbr<THIN, LANE, MARCH, 1, 1>(v, ti, bi), thin_nbr<THIN, LANE, MARCH, 1, -1>(v, ti, bi),
+                          thin_nbr<THIN, LANE, MARCH, 2, 1>(v, ti, bi), thin_nbr<THIN, LANE, MARCH, 2, -1>(v, ti, bi));
+      if (KIND == 0) r = sphere_fix(a, coord(0, ti, bi), coord(1, ti, bi), coord(2, ti, bi), r);
+      u[ti - 1][bi - 1] = r;
+    }
+  const bool outLane = lane >= 2 && lane < 62 && cl < tb.hi[k][LANE];
+#pragma unroll
+  for (int ti = 2; ti < NT + 2; ++ti)
+#pragma unroll
+    for (int bi = 2; bi < NB - 2; ++bi) {
+      const int ui = ti - 1, uj = bi - 1;
+      T r = sum6<T, KIND>(thin_nbr<THIN, LANE, MARCH, 0, 1>(u, ui, uj), thin_nbr<THIN, LANE, MARCH, 0, -1>(u, ui, uj),
+                          thin_nbr<THIN, LANE, MARCH, 1, 1>(u, ui, uj), thin_nbr<THIN, LANE, MARCH, 1, -1>(u, ui, uj),
+                          thin_nbr<THIN, LANE, MARCH, 2, 1>(u, ui, uj), thin_nbr<THIN, LANE, MARCH, 2, -1>(u, ui, uj));
+      const int x = coord(0, ti, bi), y = coord(1, ti, bi), z = coord(2, ti, bi);
+      if (KIND == 0) r = sphere_fix(a, x, y, z, r);
+      if (outLane && ti - 2 < nt && b0 - 2 + bi < tb.hi[k][MARCH])
+        a.dst[int64_t(z) * a.pxy + int64_t(y) * a.px + x] = r;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------------------
@@ -406,6 +556,139 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
       X2_LAUNCH(double, 1);
   }
 #undef X2_LAUNCH
+}
+
+template <typename T, int KIND>
+static void apply_x2_regions_t(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &rs, const Spheres &sph,
+                               hipStream_t stream) {
+  StencilArgs<T> a = make_args<T>(dom, qi, dom.get_compute_region(), KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth,
+                                  sph);
+  const Dim3 org = dom.accessor_origin();
+  for (size_t k0 = 0; k0 < rs.size(); k0 += kMaxX2Regions) {
+    X2Regions rt{};
+    for (size_t k = k0; k < rs.size() && rt.n < kMaxX2Regions; ++k) {
+      const Rect3 r(rs[k].lo - org, rs[k].hi - org);
+      const Dim3 e = r.extent();
+      rt.lo[rt.n][0] = int(r.lo.x);
+      rt.lo[rt.n][1] = int(r.lo.y);
+      rt.lo[rt.n][2] = int(r.lo.z);
+      rt.ext[rt.n][0] = int(e.x);
+      rt.ext[rt.n][1] = int(e.y);
+      rt.ext[rt.n][2] = int(e.z);
+      rt.begin[rt.n + 1] = rt.begin[rt.n] + e.flatten();
+      ++rt.n;
+    }
+    const int64_t total = rt.begin[rt.n];
+    if (total == 0) continue;
+    const int blocks = int(std::min<int64_t>((total + 255) / 256, 16384));
+    hipLaunchKernelGGL((stencil7x2_regions_kernel<T, KIND>), dim3(blocks), dim3(256), 0, stream, a, rt);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
+void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
+                              const Spheres &sph, hipStream_t stream) {
+  STENCIL_REQUIRE(stencil7x2_supported(dom, qi), "two-step stencil needs a device fp32/fp64 quantity with depth-2 halos");
+  const Rect3 cr = dom.get_compute_region();
+  std::vector<Rect3> rs;
+  for (const auto &r : regions) {
+    if (r.empty()) continue;
+    STENCIL_REQUIRE(cr.contains(r.lo) && r.hi.x <= cr.hi.x && r.hi.y <= cr.hi.y && r.hi.z <= cr.hi.z,
+                    "stencil region " << r << " outside compute region " << cr);
+    rs.push_back(r);
+  }
+  if (rs.empty()) return;
+  dom.set_device();
+  const bool f32 = dom.elem_size(qi) == 4;
+  if (f32)
+    kind == StencilKind::Jacobi ? apply_x2_regions_t<float, 0>(dom, qi, rs, sph, stream)
+                                : apply_x2_regions_t<float, 1>(dom, qi, rs, sph, stream);
+  else
+    kind == StencilKind::Jacobi ? apply_x2_regions_t<double, 0>(dom, qi, rs, sph, stream)
+                                : apply_x2_regions_t<double, 1>(dom, qi, rs, sph, stream);
+}
+
+template <typename T, int KIND, int THIN, int LANE, int MARCH>
+static void launch_thin(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &slabs, const Spheres &sph,
+                        hipStream_t stream) {
+  if (slabs.empty()) return;
+  const Dim3 org = dom.accessor_origin();
+  ThinTable tb{};
+  int maxT = 0;
+  for (const Rect3 &g : slabs) {
+    const Rect3 r(g.lo - org, g.hi - org);
+    const int i = tb.n++;
+    const int64_t lo[3] = {r.lo.x, r.lo.y, r.lo.z}, hi[3] = {r.hi.x, r.hi.y, r.hi.z};
+    for (int d = 0; d < 3; ++d) {
+      tb.lo[i][d] = int(lo[d]);
+      tb.hi[i][d] = int(hi[d]);
+    }
+    maxT = std::max(maxT, int(hi[THIN] - lo[THIN]));
+    const int waves = int((hi[LANE] - lo[LANE] + 59) / 60) * int((hi[MARCH] - lo[MARCH] + kThinBC - 1) / kThinBC);
+    tb.wbegin[i + 1] = tb.wbegin[i] + waves;
+  }
+  if (tb.wbegin[tb.n] == 0) return;
+  StencilArgs<T> a = make_args<T>(dom, qi, dom.get_compute_region(), KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth,
+                                  sph);
+  a.x0 = int(dom.radius().x(-1)); // raw x of the first interior cell: 16-B aligned (stencil7x2_supported)
+  const uint32_t blocks = uint32_t((tb.wbegin[tb.n] + 3) / 4);
+  if (maxT <= 2)
+    hipLaunchKernelGGL((stencil7x2_thin_kernel<T, KIND, THIN, LANE, MARCH, 2>), dim3(blocks), dim3(256), 0, stream, a, tb);
+  else
+    hipLaunchKernelGGL((stencil7x2_thin_kernel<T, KIND, THIN, LANE, MARCH, 4>), dim3(blocks), dim3(256), 0, stream, a, tb);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T, int KIND>
+static void apply_exterior_t(const LocalDomain &dom, int64_t qi, const Rect3 &c, const Rect3 &in, const Spheres &sph,
+                             hipStream_t stream) {
+  auto nonempty = [](std::initializer_list<Rect3> l) {
+    std::vector<Rect3> v;
+    for (const Rect3 &r : l)
+      if (!r.empty()) v.push_back(r);
+    return v;
+  };
+  // z slabs (whole x-y planes): lanes on x, march in y; y slabs (interior z): lanes on x, march in z; x slabs
+  // (interior y, z): lanes on y, march in z
+  const auto zs = nonempty({Rect3(c.lo, Dim3(c.hi.x, c.hi.y, in.lo.z)), Rect3(Dim3(c.lo.x, c.lo.y, in.hi.z), c.hi)});
+  const auto ys = nonempty({Rect3(Dim3(c.lo.x, c.lo.y, in.lo.z), Dim3(c.hi.x, in.lo.y, in.hi.z)),
+                            Rect3(Dim3(c.lo.x, in.hi.y, in.lo.z), Dim3(c.hi.x, c.hi.y, in.hi.z))});
+  const auto xs = nonempty({Rect3(Dim3(c.lo.x, in.lo.y, in.lo.z), Dim3(in.lo.x, in.hi.y, in.hi.z)),
+                            Rect3(Dim3(in.hi.x, in.lo.y, in.lo.z), Dim3(c.hi.x, in.hi.y, in.hi.z))});
+  launch_thin<T, KIND, 2, 0, 1>(dom, qi, zs, sph, stream);
+  launch_thin<T, KIND, 1, 0, 2>(dom, qi, ys, sph, stream);
+  launch_thin<T, KIND, 0, 1, 2>(dom, qi, xs, sph, stream);
+}
+
+void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &interior, StencilKind kind,
+                               const Spheres &sph, hipStream_t stream, const StencilTune &tune) {
+  const Rect3 c = dom.get_compute_region();
+  const Rect3 &in = interior;
+  if (in.empty()) {
+    stencil7x2_apply(dom, qi, c, kind, sph, stream, tune);
+    return;
+  }
+  STENCIL_REQUIRE(stencil7x2_supported(dom, qi), "two-step stencil needs a device fp32/fp64 quantity with depth-2 halos");
+  STENCIL_REQUIRE(c.contains(in.lo) && in.hi.x <= c.hi.x && in.hi.y <= c.hi.y && in.hi.z <= c.hi.z,
+                  "interior " << in << " outside compute region " << c);
+  const Dim3 lo = in.lo - c.lo, hi = c.hi - in.hi;
+  if (std::max({lo.x, lo.y, lo.z, hi.x, hi.y, hi.z}) > 4) {
+    // thick shells: the thread-per-cell kernel
+    std::vector<Rect3> ext = {Rect3(c.lo, Dim3(c.hi.x, c.hi.y, in.lo.z)), Rect3(Dim3(c.lo.x, c.lo.y, in.hi.z), c.hi),
+                              Rect3(Dim3(c.lo.x, c.lo.y, in.lo.z), Dim3(c.hi.x, in.lo.y, in.hi.z)),
+                              Rect3(Dim3(c.lo.x, in.hi.y, in.lo.z), Dim3(c.hi.x, c.hi.y, in.hi.z)),
+                              Rect3(Dim3(c.lo.x, in.lo.y, in.lo.z), Dim3(in.lo.x, in.hi.y, in.hi.z)),
+                              Rect3(Dim3(in.hi.x, in.lo.y, in.lo.z), Dim3(c.hi.x, in.hi.y, in.hi.z))};
+    stencil7x2_apply_regions(dom, qi, ext, kind, sph, stream);
+    return;
+  }
+  dom.set_device();
+  const bool f32 = dom.elem_size(qi) == 4, jac = kind == StencilKind::Jacobi;
+  if (f32)
+    jac ? apply_exterior_t<float, 0>(dom, qi, c, in, sph, stream) : apply_exterior_t<float, 1>(dom, qi, c, in, sph, stream);
+  else
+    jac ? apply_exterior_t<double, 0>(dom, qi, c, in, sph, stream)
+        : apply_exterior_t<double, 1>(dom, qi, c, in, sph, stream);
 }
 
 } // namespace stencil

@@ -76,7 +76,14 @@ void StencilModel::init() {
   pairs_ = cfg_.temporal >= 2 && !forward_ && !doms0.empty();
   for (const auto &d : doms0)
     for (int64_t q = 0; q < d.num_data() && pairs_; ++q) pairs_ = stencil7x2_supported(d, q);
-  if (pairs_) overlap_ = false; // exchange (depth 2) -> fused pair on the whole region
+  // fused pairs overlap like single steps: S o S of the interior (2 cells from every face that receives a halo)
+  // during the depth-2 exchange, the exterior slabs after it; without a non-empty interior: exchange, then sweep
+  // Measured on one MI355X (512^3, bench_stencil --only ext): interior sweep 308 us + thin-slab exterior 64 us when
+  // run concurrently = 387 us vs 296 us for one whole sweep, i.e. the split costs ~90 us of the ~100 us of xGMI
+  // exchange it could hide. So `auto` keeps fused pairs un-overlapped; overlap=on (auto off) forces the split.
+  if (pairs_ && cfg_.autoOverlap) overlap_ = false;
+  if (pairs_ && overlap_)
+    for (const auto &r : dd_->get_interior()) overlap_ = overlap_ && !r.empty();
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
@@ -185,6 +192,22 @@ void StencilModel::run(int iters) {
 void StencilModel::enqueue_step(int k) {
   auto &doms = dd_->domains();
   const bool device = !compute_.empty();
+  if (k == 2 && overlap_) {
+    // temporal blocking, overlapped: interior S o S on the compute stream while the depth-2 exchange runs on the
+    // comm stream, then the exterior slabs on the comm stream behind it; the compute stream joins them
+    dd_->exchange_async();
+    for (size_t di = 0; di < doms.size(); ++di)
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7x2_apply(doms[di], q, interiors_[di], cfg_.kind, sph_, compute_[di].get(), cfg_.tune);
+    for (size_t di = 0; di < doms.size(); ++di) {
+      hipStream_t s = dd_->comm_stream(di);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7x2_apply_exterior(doms[di], q, interiors_[di], cfg_.kind, sph_, s, cfg_.tune);
+      exteriorDone_[di].record(s);
+      exteriorDone_[di].wait_on(compute_[di]);
+    }
+    return;
+  }
   if (k == 2) {
     // temporal blocking: one depth-2 exchange, then S o S on every sub-domain
     const bool single = device && doms.size() == 1;

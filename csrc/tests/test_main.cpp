@@ -12,6 +12,8 @@
 #include "stencil/core/array.hpp"
 #include "stencil/core/boundary.hpp"
 #include "stencil/domain/distributed_domain.hpp"
+#include "stencil/kernels/stencil_ops.hpp"
+#include "stencil/rt/stream.hpp"
 #include "stencil/rt/allocator.hpp"
 #include "stencil/rt/statistics.hpp"
 #include "stencil/topo/partition.hpp"
@@ -281,6 +283,62 @@ TEST(gpu_allocators_array, true) {
   back = a.to_host();
   CHECK(back[0] == 0.0 && back[2] == 0.0);
 }
+
+// the fused pair split as an overlapped step runs it (interior sweep + exterior slabs, thread per cell) must give
+// the same bits as one sweep of the whole compute region
+static void check_x2_split(StencilKind kind) {
+  LocalDomain ld(Dim3(40, 36, 44), Dim3(0, 0, 0), 0, Backend::Device);
+  ld.set_radius(Radius::face_edge_corner(2, 1, 0));
+  ld.add_data<float>("d");
+  ld.realize();
+  Stream s(0);
+  const Rect3 cr = ld.get_compute_region();
+  const Spheres sph = kind == StencilKind::Jacobi ? Spheres::jacobi(Rect3(Dim3(0, 0, 0), Dim3(40, 36, 44))) : Spheres();
+  astaroth_init(ld, 0, 10.0, s); // sin-wave interior, -10 halo: every cell distinct enough to catch a wrong read
+  const size_t n = size_t(ld.buffer_bytes(0) / 4);
+  auto next_to_host = [&]() {
+    std::vector<float> h(n);
+    s.sync();
+    HIP_CHECK(hipMemcpy(h.data(), static_cast<char *>(ld.next_data(0)) - ld.pad_x(0) * 4, n * 4, hipMemcpyDeviceToHost));
+    return h;
+  };
+  fill_value(ld, 0, 0.0, false, s);
+  stencil7x2_apply(ld, 0, cr, kind, sph, s);
+  const auto whole = next_to_host();
+  fill_value(ld, 0, 0.0, false, s);
+  Rect3 in = cr;
+  in.lo = in.lo + Dim3(2, 2, 2);
+  in.hi = in.hi - Dim3(2, 2, 2);
+  stencil7x2_apply(ld, 0, in, kind, sph, s);
+  std::vector<Rect3> ext;
+  ext.push_back(Rect3(Dim3(cr.lo.x, cr.lo.y, cr.lo.z), Dim3(cr.hi.x, cr.hi.y, in.lo.z)));
+  ext.push_back(Rect3(Dim3(cr.lo.x, cr.lo.y, in.hi.z), Dim3(cr.hi.x, cr.hi.y, cr.hi.z)));
+  ext.push_back(Rect3(Dim3(cr.lo.x, cr.lo.y, in.lo.z), Dim3(cr.hi.x, in.lo.y, in.hi.z)));
+  ext.push_back(Rect3(Dim3(cr.lo.x, in.hi.y, in.lo.z), Dim3(cr.hi.x, cr.hi.y, in.hi.z)));
+  ext.push_back(Rect3(Dim3(cr.lo.x, in.lo.y, in.lo.z), Dim3(in.lo.x, in.hi.y, in.hi.z)));
+  ext.push_back(Rect3(Dim3(in.hi.x, in.lo.y, in.lo.z), Dim3(cr.hi.x, in.hi.y, in.hi.z)));
+  stencil7x2_apply_regions(ld, 0, ext, kind, sph, s);
+  const auto split = next_to_host();
+  int64_t bad = 0;
+  for (size_t i = 0; i < n; ++i) bad += std::memcmp(&whole[i], &split[i], 4) != 0;
+  if (bad) std::fprintf(stderr, "  regions: %lld cells differ\n", (long long)bad);
+  CHECK(bad == 0);
+  // the overlapped model's exterior (sweep for z/y slabs, lanes-on-rows for x slabs), x slabs 2 and 1 thick
+  for (int tx : {2, 1}) {
+    fill_value(ld, 0, 0.0, false, s);
+    Rect3 in2 = in;
+    in2.hi.x = cr.hi.x - tx;
+    stencil7x2_apply(ld, 0, in2, kind, sph, s);
+    stencil7x2_apply_exterior(ld, 0, in2, kind, sph, s);
+    const auto ex = next_to_host();
+    int64_t bad2 = 0;
+    for (size_t i = 0; i < n; ++i) bad2 += std::memcmp(&whole[i], &ex[i], 4) != 0;
+    if (bad2) std::fprintf(stderr, "  exterior (x slab %d): %lld cells differ\n", tx, (long long)bad2);
+    CHECK(bad2 == 0);
+  }
+}
+TEST(gpu_x2_split_regions_jacobi, true) { check_x2_split(StencilKind::Jacobi); }
+TEST(gpu_x2_split_regions_astaroth, true) { check_x2_split(StencilKind::Astaroth); }
 
 int main(int argc, char **argv) {
   bool cpu = true, gpu = false;

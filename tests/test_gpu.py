@@ -250,6 +250,27 @@ def test_stencil_special_values_bitwise(st, temporal, kind):
     assert torch.equal(got.view(torch.int32), u.view(torch.int32)), int((got.view(torch.int32) != u.view(torch.int32)).sum())
 
 
+@pytest.mark.parametrize("methods", ["All", "Rccl", "Staged"])
+@pytest.mark.parametrize("size,gpus", [((40, 36, 44), [0, 0]), ((67, 45, 33), [0, 0, 0, 0]), ((30, 28, 26), [0])])
+@pytest.mark.parametrize("kind", ["jacobi", "astaroth"])
+def test_temporal2_overlapped(st, methods, size, gpus, kind):
+    """Overlapped fused pairs: S o S of the interior during the depth-2 exchange, the exterior slabs (thread per
+    cell, stencil7x2_regions_kernel) after it -- bitwise equal to single steps."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    m = cls(size, gpus=gpus, methods=getattr(st.MethodFlags, methods), temporal=2, overlap=True,
+            auto_overlap=False, **kw)
+    m.init()
+    assert m.temporal_blocking() and m.overlapping()
+    u = _gather(m)
+    m.run(7)  # three overlapped pairs and one single (overlapped) step
+    for _ in range(7):
+        u = ref(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
 @pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy"])
 def test_jacobi_temporal2_transports(st, methods):
     """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs"""
