@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--temporal", type=int, default=2,
                     help="steps fused per sweep: 2 = temporal blocking (one depth-2 halo exchange + one fused "
                          "S(S(u)) sweep per two steps, bitwise equal to single steps), 1 = one exchange + sweep per step")
+    ap.add_argument("--axis-cost", default="2,1,1",
+                    help="NodeAware partition cost per interface cell of x,y,z cuts (1,1,1 = the reference's rule)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU)")
     args = ap.parse_args()
@@ -98,6 +100,7 @@ def main():
             if args.temporal >= 2:
                 r.set_edge(1)
             pl.set_radius(r)
+            pl.set_axis_cost(st.Dim3(*(int(v) for v in args.axis_cost.split(","))))  # the model's decomposition
             q = pl.add_data("coords", torch.int32)
             pl.set_methods(methods)
             pl.set_gpus([device])
@@ -137,7 +140,8 @@ def main():
     tune.zchunk = args.zchunk
     overlap = not args.no_overlap and args.overlap != "off"
     model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=overlap,
-                        auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg)
+                        auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
+                        axis_cost=tuple(int(v) for v in args.axis_cost.split(",")))
     model.init()
     model.run(args.warmup)
     model.synchronize()
@@ -188,7 +192,10 @@ def main():
             "data": "synthetic (reference Jacobi3D initial condition: 0.5 + hot/cold spheres)",
             "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": L,
                        "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
-                       "parallelism": f"domain-decomp{n}", "methods": st.methods_to_string(methods), "preflight": preflight,
+                       "parallelism": f"domain-decomp{n}",
+                       "decomposition": "x".join(str(v) for v in (model.domain.placement_dim().x,
+                                                                   model.domain.placement_dim().y,
+                                                                   model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
                        "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
                        "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),

@@ -241,12 +241,13 @@ int main(int argc, char **argv) {
     s.sync();
     for (int nw : {12, 16})
       for (int pf : {1, 2, 3})
-        for (int zc : {0, 64, 128}) {
+        for (int zc : {-1, 0, 64, 128}) { // -1: fixed auto z-chunks (x2sched 0); 0: balanced segments
           const int nt = 1, alt = 1;
           StencilTune t;
           t.nontemporal = nt;
           t.alternateZ = alt;
-          t.zchunk = zc;
+          t.zchunk = zc < 0 ? 0 : zc;
+          t.x2sched = zc < 0 ? 0 : 1;
           t.x2nw = nw;
           t.x2pf = pf;
           const double us = timeit([&] {

@@ -84,6 +84,9 @@ public:
   MethodFlags methods() const { return flags_; }
   bool any_methods(MethodFlags m) const { return (m && flags_); }
   void set_placement(PlacementStrategy s) { strategy_ = s; }
+  // NodeAware partition: relative cost per interface cell of cuts normal to x/y/z (NodePartition; default 1,1,1)
+  void set_axis_cost(const Dim3 &c) { axisCost_ = c; }
+  const Dim3 &axis_cost() const { return axisCost_; }
   void set_gpus(const std::vector<int> &gpus) { gpus_ = gpus; }
   const std::vector<int> &gpus() const { return gpus_; }
   void set_backend(Backend b) { backend_ = b; backendSet_ = true; }
@@ -106,6 +109,12 @@ public:
   Rect3 get_compute_region() const { return Rect3(Dim3(0, 0, 0), size_); }
   std::vector<Rect3> get_interior() const;
   std::vector<std::vector<Rect3>> get_exterior() const;
+  // MI355X extension: the part of each local domain's compute region that a stencil reaching `reach` cells along
+  // an axis can update from halos filled by the same-device translate (Kernel method) alone, i.e. it is shrunk
+  // only at the faces whose halo arrives over IPC / RCCL / staged / peer transports. Safe to compute once
+  // wait_translated() has been passed, while those transports are still in flight; the rest (thin slabs at the
+  // remote faces) after wait_exchange(). Equals get_compute_region() for a purely same-GPU exchange.
+  std::vector<Rect3> get_local_interior(int reach) const;
   const Placement &placement() const { return *placement_; }
   Dim3 subdomain_idx(int64_t di) const { return placement_->get_idx(rank(), int(di)); }
   uint64_t exchange_bytes_for_method(MethodFlags m) const; // summed over all ranks, per exchange
@@ -130,6 +139,9 @@ public:
   void record_ready(size_t di, hipStream_t s);
   // make `s` wait until the halos of domain di from the last exchange are written
   void wait_exchange(size_t di, hipStream_t s);
+  // make `s` wait until the same-device (Kernel) halo copies of the last exchange_async() are written (the halos
+  // get_local_interior() relies on); needs the comm streams, i.e. exchange_async() without a caller stream
+  void wait_translated(size_t di, hipStream_t s);
   // block the host until the last exchange is complete (checks device-side timeouts)
   void sync_exchange();
   hipStream_t comm_stream(size_t di) const;
@@ -163,6 +175,7 @@ private:
   std::vector<DType> dtypes_;
   MethodFlags flags_ = MethodFlags::All;
   PlacementStrategy strategy_ = PlacementStrategy::NodeAware;
+  Dim3 axisCost_{1, 1, 1};
   Backend backend_ = Backend::Device;
   bool backendSet_ = false;
   bool realized_ = false;
@@ -171,6 +184,7 @@ private:
   std::unique_ptr<Placement> placement_;
   std::vector<LocalDomain> domains_;
   std::vector<ExchangePlanEntry> plan_;
+  std::vector<std::array<uint8_t, 27>> remoteHalo_; // per local domain, per halo side: filled by a non-Kernel method
   std::array<uint64_t, 5> bytesPerMethod_{}; // indexed by log2(method)
   std::unique_ptr<Impl> impl_;
 };

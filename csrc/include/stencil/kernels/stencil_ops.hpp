@@ -49,6 +49,14 @@ struct StencilTune {
   // fused-pair kernel (stencil7x2): waves per block (8/12/16, one src row each, NW-4 output rows) and planes of
   // z lookahead (2/3/4)
   int x2nw = 16, x2pf = 2;
+  // fused-pair work split: 1 (default) = one block per resident slot, each taking an equal share of the
+  // (column, plane) space (one or two z segments): no partly empty last round and the fewest warm-up planes;
+  // 0 = fixed z-chunks per block column (zchunk / auto)
+  int x2sched = 1;
+  // CUs an overlapped fused-pair interior sweep leaves free for the exchange kernels of the comm stream (balanced
+  // segment mode: the grid is that many blocks short of the resident slots); reserveCUs is what one launch uses
+  int x2reserve = 8;
+  int reserveCUs = 0;
   bool xcdRemap = true;
   bool nontemporal = true;
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous

@@ -25,6 +25,10 @@ struct StencilModelConfig {
   bool fp64 = false;
   MethodFlags methods = MethodFlags::All;
   PlacementStrategy placement = PlacementStrategy::NodeAware;
+  // NodeAware cut costs (DistributedDomain::set_axis_cost): x faces count double, so weak-scaled cubes are cut
+  // along z and y first (8 GPUs: 1x2x4 instead of 2x2x2, the same 3 x 4 MiB of face traffic per GPU for 512^3
+  // per GPU, but row-contiguous faces whose exchange the fused pairs can overlap)
+  Dim3 axisCost{2, 1, 1};
   std::vector<int> gpus;       // empty = automatic
   bool overlap = true;
   // when every halo comes from this GPU (periodic self-wrap / co-resident sub-domains) the exchange is a local
@@ -77,7 +81,8 @@ private:
   std::unique_ptr<DistributedDomain> dd_;
   std::vector<Stream> compute_;
   std::vector<Event> exteriorDone_;
-  std::vector<Rect3> interiors_;
+  std::vector<Rect3> interiors_;     // single steps (get_interior)
+  std::vector<Rect3> pairInteriors_; // overlapped fused pairs (get_local_interior, see init)
   std::vector<std::vector<Rect3>> exteriors_;
   Spheres sph_;
   bool overlap_ = true;

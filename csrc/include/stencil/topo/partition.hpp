@@ -95,10 +95,12 @@ class NodePartition : public GridPartition {
   Dim3 sysDim_{1, 1, 1};
   Dim3 nodeDim_{1, 1, 1};
 
+  Dim3 cost_{1, 1, 1};
+
   void split(Dim3 &d, int64_t amt, const Radius &radius) {
-    const int64_t xIface = size_.y * size_.z * (radius.dir(1, 0, 0) + radius.dir(-1, 0, 0));
-    const int64_t yIface = size_.x * size_.z * (radius.dir(0, 1, 0) + radius.dir(0, -1, 0));
-    const int64_t zIface = size_.x * size_.y * (radius.dir(0, 0, 1) + radius.dir(0, 0, -1));
+    const int64_t xIface = cost_.x * size_.y * size_.z * (radius.dir(1, 0, 0) + radius.dir(-1, 0, 0));
+    const int64_t yIface = cost_.y * size_.x * size_.z * (radius.dir(0, 1, 0) + radius.dir(0, -1, 0));
+    const int64_t zIface = cost_.z * size_.x * size_.y * (radius.dir(0, 0, 1) + radius.dir(0, 0, -1));
     // minimum radius-weighted interface; ties go to z, then y, then x (the reference prefers x,
     // partition.hpp:224-237). On MI355X a z-face is one contiguous plane (full-rate 16-B copies) while an x-face is a
     // strided column touching one 128-B line per 4-B element, so remote faces are cheapest along z.
@@ -116,8 +118,13 @@ class NodePartition : public GridPartition {
 
 public:
   NodePartition() = default;
-  NodePartition(const Dim3 &size, const Radius &radius, int64_t nodes, int64_t gpus) {
+  // axisCost: relative cost per interface cell of a cut normal to x / y / z (default 1,1,1: the reference's plain
+  // radius-weighted interface). StencilModel uses (2,1,1): an x face is a strided column (one 128-B line per row
+  // for a 2-cell halo, packed and unpacked by gathers) while y/z faces are contiguous rows, and a domain without x
+  // cuts can overlap its exchange with row-contiguous exterior slabs only.
+  NodePartition(const Dim3 &size, const Radius &radius, int64_t nodes, int64_t gpus, const Dim3 &axisCost = Dim3(1, 1, 1)) {
     size_ = size;
+    cost_ = axisCost;
     for (int64_t amt : prime_factors_desc(nodes)) split(sysDim_, amt, radius);
     for (int64_t amt : prime_factors_desc(gpus)) split(nodeDim_, amt, radius);
     dim_ = sysDim_ * nodeDim_;

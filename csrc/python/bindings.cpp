@@ -284,7 +284,8 @@ PYBIND11_MODULE(_C, m) {
       .def("linearize", &RankPartition::linearize)
       .def("dimensionize", &RankPartition::dimensionize);
   py::class_<NodePartition>(m, "NodePartition")
-      .def(py::init<const Dim3 &, const Radius &, int64_t, int64_t>())
+      .def(py::init<const Dim3 &, const Radius &, int64_t, int64_t, const Dim3 &>(), py::arg("size"), py::arg("radius"),
+           py::arg("nodes"), py::arg("gpus"), py::arg("axis_cost") = Dim3(1, 1, 1))
       .def("dim", &NodePartition::dim)
       .def("sys_dim", &NodePartition::sys_dim)
       .def("node_dim", &NodePartition::node_dim)
@@ -458,6 +459,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_methods", &DistributedDomain::set_methods)
       .def("methods", &DistributedDomain::methods)
       .def("set_placement", &DistributedDomain::set_placement)
+      .def("set_axis_cost", &DistributedDomain::set_axis_cost)
       .def("set_gpus", &DistributedDomain::set_gpus)
       .def("gpus", &DistributedDomain::gpus)
       .def("set_backend", &DistributedDomain::set_backend)
@@ -475,6 +477,7 @@ PYBIND11_MODULE(_C, m) {
       .def("get_origin", &DistributedDomain::get_origin)
       .def("get_compute_region", &DistributedDomain::get_compute_region)
       .def("get_interior", &DistributedDomain::get_interior)
+      .def("get_local_interior", &DistributedDomain::get_local_interior, py::arg("reach") = 2)
       .def("get_exterior", &DistributedDomain::get_exterior)
       .def("subdomain_idx", &DistributedDomain::subdomain_idx)
       .def("placement_dim", [](DistributedDomain &d) { return d.placement().dim(); })
@@ -540,7 +543,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("alternate_z", &StencilTune::alternateZ)
       .def_readwrite("nw", &StencilTune::nw)
       .def_readwrite("x2pf", &StencilTune::x2pf)
-      .def_readwrite("x2nw", &StencilTune::x2nw);
+      .def_readwrite("x2nw", &StencilTune::x2nw)
+      .def_readwrite("x2sched", &StencilTune::x2sched)
+      .def_readwrite("x2reserve", &StencilTune::x2reserve);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())
       .def_readwrite("size", &StencilModelConfig::size)
@@ -551,6 +556,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fp64", &StencilModelConfig::fp64)
       .def_readwrite("methods", &StencilModelConfig::methods)
       .def_readwrite("placement", &StencilModelConfig::placement)
+      .def_readwrite("axis_cost", &StencilModelConfig::axisCost)
       .def_readwrite("gpus", &StencilModelConfig::gpus)
       .def_readwrite("overlap", &StencilModelConfig::overlap)
       .def_readwrite("auto_overlap", &StencilModelConfig::autoOverlap)

@@ -263,7 +263,7 @@ void DistributedDomain::realize() {
     if (strategy_ == PlacementStrategy::NodeAware) {
       BandwidthFn bw = dev ? BandwidthFn([](int a, int b) { return gpu_topo::bandwidth(a, b); })
                            : BandwidthFn([](int a, int b) { return a == b ? 10.0 : 1.0; });
-      placement_.reset(new NodeAwarePlacement(size_, pg, radius_, gpus_, bw));
+      placement_.reset(new NodeAwarePlacement(size_, pg, radius_, gpus_, bw, axisCost_));
     } else {
       placement_.reset(new TrivialPlacement(size_, pg, gpus_));
     }
@@ -372,6 +372,7 @@ void DistributedDomain::realize() {
   std::map<std::tuple<int, int, int64_t>, int> sendKey, recvKey;
   std::vector<std::tuple<int, int, Dim3>> localTranslates; // (srcDom, dstDom, dir)
   plan_.clear();
+  remoteHalo_.assign(domains_.size(), std::array<uint8_t, 27>{});
   for (size_t di = 0; di < domains_.size(); ++di) {
     const Dim3 myIdx = placement_->get_idx(myRank, int(di));
     const int myDev = placement_->get_device(myIdx);
@@ -425,6 +426,8 @@ void DistributedDomain::realize() {
                   srcDev = placement_->get_device(srcIdx);
         const MethodFlags m = choose(srcRank, srcDev, myRank, myDev);
         if (m == MethodFlags::None) LOG_FATAL("no method available to recv " << srcIdx << " -> " << myIdx);
+        // the halo on side -dir is valid after the same-device translate only for Kernel messages
+        if (m != MethodFlags::Kernel) remoteHalo_[di][size_t(dir_index(-dir))] = 1;
         if (m == MethodFlags::Kernel || m == MethodFlags::PeerCopy) continue; // written by the sender directly
         const auto key = std::make_tuple(int(m), int(di), linearize(srcIdx, gdim));
         auto it = recvKey.find(key);
@@ -731,6 +734,49 @@ std::vector<Rect3> DistributedDomain::get_interior() const {
   return ret;
 }
 
+std::vector<Rect3> DistributedDomain::get_local_interior(int reach) const {
+  STENCIL_REQUIRE(realized_, "get_local_interior before realize()");
+  std::vector<Rect3> ret(domains_.size());
+  for (size_t di = 0; di < domains_.size(); ++di) {
+    const Rect3 com = domains_[di].get_compute_region();
+    const auto &rh = remoteHalo_[di];
+    // shrink[axis][side]: cells to drop at the low (0) / high (1) face of each axis
+    int64_t sh[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+    auto comp = [](const Dim3 &d, int a) { return a == 0 ? d.x : (a == 1 ? d.y : d.z); };
+    // remote faces: the stencil reaches `reach` cells along an axis
+    for (int i = 0; i < 27; ++i) {
+      const Dim3 d = dir_from_index(i);
+      const int nz = (d.x != 0) + (d.y != 0) + (d.z != 0);
+      if (nz != 1 || !rh[size_t(i)]) continue;
+      for (int a = 0; a < 3; ++a)
+        if (comp(d, a) != 0) sh[a][comp(d, a) > 0] = std::max<int64_t>(sh[a][comp(d, a) > 0], std::min<int64_t>(reach, radius_.dir(d)));
+    }
+    // remote edges / corners: a cell reads them only when it is within reach of all their faces at once, so one
+    // shrunk face among them covers the rest; with none, drop every face of the direction (conservative)
+    for (int i = 0; i < 27; ++i) {
+      const Dim3 d = dir_from_index(i);
+      const int nz = (d.x != 0) + (d.y != 0) + (d.z != 0);
+      if (nz < 2 || !rh[size_t(i)] || radius_.dir(d) == 0) continue;
+      bool covered = false;
+      for (int a = 0; a < 3; ++a)
+        if (comp(d, a) != 0 && sh[a][comp(d, a) > 0] > 0) covered = true;
+      if (covered) continue;
+      for (int a = 0; a < 3; ++a)
+        if (comp(d, a) != 0) sh[a][comp(d, a) > 0] = std::max<int64_t>(sh[a][comp(d, a) > 0], 1);
+    }
+    Rect3 in = com;
+    in.lo.x += sh[0][0];
+    in.hi.x -= sh[0][1];
+    in.lo.y += sh[1][0];
+    in.hi.y -= sh[1][1];
+    in.lo.z += sh[2][0];
+    in.hi.z -= sh[2][1];
+    if (in.hi.x < in.lo.x || in.hi.y < in.lo.y || in.hi.z < in.lo.z) in = Rect3(com.lo, com.lo);
+    ret[di] = in;
+  }
+  return ret;
+}
+
 std::vector<std::vector<Rect3>> DistributedDomain::get_exterior() const {
   std::vector<std::vector<Rect3>> ret(domains_.size());
   const auto ins = get_interior();
@@ -773,6 +819,12 @@ void DistributedDomain::record_ready(size_t di, hipStream_t s) {
   if (backend_ != Backend::Device) return;
   impl_->ready.at(di).record(s);
   impl_->readyPending[di] = true;
+}
+
+void DistributedDomain::wait_translated(size_t di, hipStream_t s) {
+  if (backend_ != Backend::Device) return;
+  const DevCtx &ctx = impl_->devs[impl_->devIndex.at(domains_.at(di).gpu())];
+  ctx.translated.wait_on(s);
 }
 
 void DistributedDomain::wait_exchange(size_t di, hipStream_t s) {

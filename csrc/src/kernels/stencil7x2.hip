@@ -121,24 +121,44 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
   __shared__ NV us[2][NW][64]; // u1 row of every wave, plane z+dz at publish (= z when read)
   __shared__ T ce[2][NW][2];   // src edge scalars of the published rows: [0] at x-1 (lane 0), [1] at x+V
 
-  const uint32_t nb = uint32_t(a.gx) * a.gy * a.gz;
+  const uint32_t nb = gridDim.x;
   const uint32_t lb = REMAP ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
-  const int bz = int(lb % uint32_t(a.gz));
-  const int by = int((lb / uint32_t(a.gz)) % uint32_t(a.gy));
-  const int bx = int(lb / (uint32_t(a.gz) * a.gy));
   const int lane = threadIdx.x;
   const int w = int(threadIdx.y);
+  // The block's work is a range [s, e) of the linear (column, plane) space, column = bx * gy + by (y-neighbour
+  // columns are adjacent, so with the XCD remap their shared halo rows meet in one L2). Chunk mode: one fixed
+  // z-chunk. Segment mode (a.seg): gridDim.x = the resident block slots, each takes an equal share, i.e. one or
+  // two z segments of about ncols * nz / slots planes: no partly empty last round of blocks, and the fewest
+  // 4-plane warm-ups per useful plane.
+  const int64_t nzt = a.hiz - a.loz;
+  int64_t s, e;
+  if (a.seg) {
+    const int64_t W = int64_t(a.gx) * a.gy * nzt;
+    s = int64_t(lb) * W / nb;
+    e = int64_t(lb + 1) * W / nb;
+  } else {
+    const int64_t col = lb / uint32_t(a.gz);
+    s = col * nzt + int64_t(lb % uint32_t(a.gz)) * a.zc;
+    e = min(s + a.zc, (col + 1) * nzt);
+  }
+  for (int seg = 0; s < e; ++seg) { // block-uniform
+  const int64_t col = s / nzt;
+  const int zo = int(s - col * nzt);
+  const int nzs = int(min<int64_t>(nzt - zo, e - s));
+  s += nzs;
+  const int bx = int(col / a.gy), by = int(col - int64_t(bx) * a.gy);
+  const int zs = a.loz + zo;
+  const int ze = zs + nzs;
+  // alternate the march direction between neighbouring pieces of a column, so the planes two pieces share are
+  // read by both at about the same time (warm-up of one, tail of the other)
+  const bool down = ((a.seg ? ((lb + uint32_t(seg)) & 1) : ((zo / a.zc) & 1)) != 0) != (a.flip != 0);
   const int c = bx * 64 + lane;
   const bool cvalid = c < a.nchunks;
   const int cl = cvalid ? c : a.nchunks - 1;
   const int xb = a.x0 + cl * V;
   const int yblk = a.loy + YO * by; // first output row of the block
   const int y = yblk - 2 + w;       // this wave's row
-  const int zs = a.loz + bz * a.zc;
-  const int ze = min(zs + a.zc, a.hiz);
-  if (yblk >= a.hiy || zs >= ze) return; // block-uniform
-  const bool down = ((bz & 1) != 0) != (a.flip != 0);
-  const int nzs = ze - zs;
+  if (yblk >= a.hiy) continue; // block-uniform
 
   const bool edgeL = lane == 0;
   const bool edgeR = lane == 63 || c + 1 >= a.nchunks;
@@ -296,6 +316,7 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
     march(std::true_type{});
   else
     march(std::false_type{});
+  } // segments
 }
 
 // S o S on a few small boxes (the exterior slabs of an overlapped step: interior sweep during the exchange, these
@@ -502,12 +523,27 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.gy = (ny + YO - 1) / YO;
   const void *kern = tune.xcdRemap ? (const void *)stencil7x2_kernel<T, NW, PF, KIND, true>
                                    : (const void *)stencil7x2_kernel<T, NW, PF, KIND, false>;
-  int zc = tune.zchunk;
-  if (zc <= 0) // each z-chunk re-reads 4 warm-up planes (2 src + 2 for u1)
-    zc = pick_zchunk(int64_t(a.gx) * a.gy, nz, x2_resident_blocks(kern, 64 * NW), 4, 16);
-  a.zc = zc;
-  a.gz = (nz + zc - 1) / zc;
-  const uint32_t blocks = uint32_t(a.gx) * a.gy * a.gz;
+  const int64_t cols = int64_t(a.gx) * a.gy;
+  const int64_t resident = x2_resident_blocks(kern, 64 * NW);
+  uint32_t blocks;
+  if (tune.x2sched != 0 && tune.zchunk <= 0) {
+    // one block per resident slot, but pieces of at least 16 planes (each piece re-reads 4 warm-up planes)
+    a.seg = 1;
+    a.zc = 1;
+    a.gz = 1;
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dom.gpu()) != hipSuccess) cus = 256;
+    const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
+    const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
+    blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 16)));
+  } else {
+    int zc = tune.zchunk;
+    if (zc <= 0) // each z-chunk re-reads 4 warm-up planes (2 src + 2 for u1)
+      zc = pick_zchunk(cols, nz, resident, 4, 16);
+    a.zc = zc;
+    a.gz = (nz + zc - 1) / zc;
+    blocks = uint32_t(cols * a.gz);
+  }
   dom.set_device();
   if (tune.xcdRemap)
     hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, true>), dim3(blocks), dim3(64, NW), 0, stream, a);

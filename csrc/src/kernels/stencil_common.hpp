@@ -47,6 +47,7 @@ template <typename T> struct StencilArgs {
   int rawZm1;                       // clamp for the deep z prefetch
   int zc;                           // planes per block
   int gx, gy, gz;                   // logical grid
+  int seg;                          // stencil7x2: 1 = balanced (column, plane) segments over gridDim.x blocks
   // spheres, raw coordinates
   int hx, hy, hz, cx, cy, cz;
   int r1sq; // (radius+1)^2, 0 = disabled

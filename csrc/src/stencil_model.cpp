@@ -28,6 +28,7 @@ StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::
   dd_->set_radius(r);
   dd_->set_methods(cfg.methods);
   dd_->set_placement(cfg.placement);
+  dd_->set_axis_cost(cfg.axisCost);
   if (!cfg.gpus.empty()) dd_->set_gpus(cfg.gpus);
   if (cfg.setBackend) dd_->set_backend(cfg.backend);
   for (int q = 0; q < cfg.quantities; ++q) {
@@ -76,14 +77,27 @@ void StencilModel::init() {
   pairs_ = cfg_.temporal >= 2 && !forward_ && !doms0.empty();
   for (const auto &d : doms0)
     for (int64_t q = 0; q < d.num_data() && pairs_; ++q) pairs_ = stencil7x2_supported(d, q);
-  // fused pairs overlap like single steps: S o S of the interior (2 cells from every face that receives a halo)
-  // during the depth-2 exchange, the exterior slabs after it; without a non-empty interior: exchange, then sweep
-  // Measured on one MI355X (512^3, bench_stencil --only ext): interior sweep 308 us + thin-slab exterior 64 us when
-  // run concurrently = 387 us vs 296 us for one whole sweep, i.e. the split costs ~90 us of the ~100 us of xGMI
-  // exchange it could hide. So `auto` keeps fused pairs un-overlapped; overlap=on (auto off) forces the split.
-  if (pairs_ && cfg_.autoOverlap) overlap_ = false;
-  if (pairs_ && overlap_)
-    for (const auto &r : dd_->get_interior()) overlap_ = overlap_ && !r.empty();
+  // Fused pairs overlap against the REMOTE part of the exchange only: the same-device translate (periodic
+  // self-wrap, co-resident sub-domains) runs first, then S o S of the local interior (the compute region shrunk
+  // only at faces whose halo arrives over IPC / RCCL / staged transports, get_local_interior) while those
+  // transports are in flight, then the thin slabs at the remote faces. Measured on one MI355X (512^3,
+  // bench_stencil --only ext): with all six faces shrunk the split costs ~90 us of the ~100 us it could hide
+  // (interior 308 us + x/y/z slabs 64 us concurrently = 387 us vs 296 us whole), dominated by the x slabs (lanes
+  // along strided rows); y/z slabs are row-contiguous. So `auto` overlaps pairs exactly when some halo is remote
+  // and no x face is: 2 GPUs (z split) and 4 GPUs (y, z split) of the weak-scaling ladder, not 2x2x2.
+  if (pairs_) {
+    const auto li = dd_->get_local_interior(2);
+    bool remote = false, xcut = false;
+    for (size_t di = 0; di < doms0.size(); ++di) {
+      const Rect3 c = doms0[di].get_compute_region();
+      remote = remote || !(li[di].lo == c.lo && li[di].hi == c.hi);
+      xcut = xcut || li[di].lo.x != c.lo.x || li[di].hi.x != c.hi.x;
+    }
+    if (cfg_.autoOverlap) overlap_ = overlap_ && remote && !xcut;
+    // forced overlap without remote halos (one GPU): the classic full split, exercises every slab kernel
+    pairInteriors_ = remote ? li : dd_->get_interior();
+    for (const auto &r : pairInteriors_) overlap_ = overlap_ && !r.empty();
+  }
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
@@ -195,14 +209,20 @@ void StencilModel::enqueue_step(int k) {
   if (k == 2 && overlap_) {
     // temporal blocking, overlapped: interior S o S on the compute stream while the depth-2 exchange runs on the
     // comm stream, then the exterior slabs on the comm stream behind it; the compute stream joins them
+    // the interior sweep leaves x2reserve CUs free, so the pack / flag / unpack kernels of the comm stream are
+    // not queued behind a grid that holds every CU until it retires
     dd_->exchange_async();
-    for (size_t di = 0; di < doms.size(); ++di)
+    StencilTune ti = cfg_.tune;
+    ti.reserveCUs = cfg_.tune.x2reserve;
+    for (size_t di = 0; di < doms.size(); ++di) {
+      dd_->wait_translated(di, compute_[di]);
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
-        stencil7x2_apply(doms[di], q, interiors_[di], cfg_.kind, sph_, compute_[di].get(), cfg_.tune);
+        stencil7x2_apply(doms[di], q, pairInteriors_[di], cfg_.kind, sph_, compute_[di].get(), ti);
+    }
     for (size_t di = 0; di < doms.size(); ++di) {
       hipStream_t s = dd_->comm_stream(di);
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
-        stencil7x2_apply_exterior(doms[di], q, interiors_[di], cfg_.kind, sph_, s, cfg_.tune);
+        stencil7x2_apply_exterior(doms[di], q, pairInteriors_[di], cfg_.kind, sph_, s, cfg_.tune);
       exteriorDone_[di].record(s);
       exteriorDone_[di].wait_on(compute_[di]);
     }

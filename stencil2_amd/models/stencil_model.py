@@ -22,7 +22,7 @@ class StencilModel:
                  quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
                  placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, auto_overlap: bool = True,
                  use_graph: bool = True, forward: bool = False, temporal: int = 1, backend=None,
-                 tune: _C.StencilTune | None = None, group=None):
+                 tune: _C.StencilTune | None = None, group=None, axis_cost=None):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
         cfg.kind = kind
@@ -43,6 +43,8 @@ class StencilModel:
             cfg.backend = backend
         if tune is not None:
             cfg.tune = tune
+        if axis_cost is not None:  # NodeAware cut costs per axis (default (2, 1, 1): x faces are strided)
+            cfg.axis_cost = _C.Dim3(*axis_cost)
         self.config = cfg
         self._m = _C.StencilModel(cfg, group if group is not None else get_group())
         self._dd = None

@@ -97,7 +97,39 @@ def scenario_jacobi(backend, methods, size):
         o, s = d.origin(), d.size()
         got = m.interior(di).cpu()
         bad += int((got != u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x]).sum())
-    print(f"rank {g.rank()} jacobi bad {bad}")
+    if os.environ.get("MP_EXPECT_OVERLAP") is not None:
+        bad += int(m.overlapping() != (os.environ["MP_EXPECT_OVERLAP"] == "1"))
+    print(f"rank {g.rank()} jacobi bad {bad} overlap {m.overlapping()} dim {m.domain.placement_dim()}")
+    return bad
+
+
+def scenario_localint(backend, methods, size):
+    """get_local_interior: shrunk by the stencil reach (2) exactly at the faces whose halo comes from another rank,
+    untouched along axes that wrap onto the same rank; always a superset of get_interior()."""
+    g = st.init_process_group()
+    r = st.Radius.constant(0)
+    r.set_face(2)
+    r.set_edge(1)
+    dd = st.DistributedDomain(*size, group=g)
+    dd.set_backend(backend)
+    dd.set_radius(r)
+    dd.set_methods(methods)
+    dd.add_data("d", torch.float32)
+    dd.realize()
+    bad = 0
+    li, full = dd.get_local_interior(2), dd.get_interior()
+    dim = dd.placement_dim()
+    for di in range(dd.num_domains()):
+        d = dd.domain(di)
+        o, s = d.origin(), d.size()
+        a, b = li[di], full[di]
+        for ax, n in (("x", dim.x), ("y", dim.y), ("z", dim.z)):
+            lo, hi = getattr(o, ax), getattr(o, ax) + getattr(s, ax)
+            want = (lo + 2, hi - 2) if n > 1 else (lo, hi)
+            got = (getattr(a.lo, ax), getattr(a.hi, ax))
+            bad += got != want
+            bad += not (getattr(a.lo, ax) <= getattr(b.lo, ax) and getattr(a.hi, ax) >= getattr(b.hi, ax))
+    print(f"rank {g.rank()} dim {dim} localint bad {bad}")
     return bad
 
 
@@ -111,6 +143,8 @@ def main():
         bad = scenario_exchange(backend, methods, sys.argv[2], tuple(int(v) for v in sys.argv[3].split(",")))
     elif sc == "canary":
         bad = scenario_canary(backend, methods, sys.argv[2], tuple(int(v) for v in sys.argv[3].split(",")))
+    elif sc == "localint":
+        bad = scenario_localint(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "jacobi":
         bad = scenario_jacobi(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     else:

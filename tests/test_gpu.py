@@ -157,12 +157,13 @@ def test_astaroth_forwarding_26dirs(st, gpus):
 @pytest.mark.parametrize("size", [(32, 32, 32), (67, 45, 33), (130, 64, 40)])
 @pytest.mark.parametrize("gpus", [[0], [0, 0], [0, 0, 0, 0]])
 @pytest.mark.parametrize("fp64", [False, True])
-@pytest.mark.parametrize("shape", [(16, 3), (16, 1), (8, 2), (12, 1)])
+@pytest.mark.parametrize("shape", [(16, 3, 1), (16, 1, 1), (8, 2, 1), (12, 1, 0), (16, 2, 0)])
 def test_jacobi_temporal2_matches_oracle(st, size, gpus, fp64, shape):
     """Temporal blocking (stencil7x2: S o S per sweep, one depth-2 exchange per pair) is bitwise equal to single
-    steps; run(5) = two fused pairs + one single step, run(16) = one captured graph block (single sub-domain)."""
+    steps; run(5) = two fused pairs + one single step, run(16) = one captured graph block (single sub-domain).
+    shape = (waves per block, planes of lookahead, work split: 1 = balanced segments, 0 = fixed z-chunks)."""
     t = st.StencilTune()
-    t.x2nw, t.x2pf = shape
+    t.x2nw, t.x2pf, t.x2sched = shape
     m = st.Jacobi3D(size, gpus=gpus, fp64=fp64, temporal=2, tune=t)
     m.init()
     assert m.temporal_blocking()
@@ -331,11 +332,13 @@ def test_colocated_ipc_two_ranks_one_gpu(radius):
         assert rc == 0, out[-3000:]
 
 
-@pytest.mark.parametrize("temporal", ["1", "2"])
-def test_colocated_ipc_jacobi_two_ranks(temporal):
-    outs = run_ranks(2, WORKER, ["jacobi", "40,24,20"],
+@pytest.mark.parametrize("temporal,ranks", [("1", 2), ("2", 2), ("2", 4), ("2", 8)])
+def test_colocated_ipc_jacobi_two_ranks(temporal, ranks):
+    """Jacobi over HIP IPC between ranks sharing one GPU. Fused pairs overlap automatically here (the split axes
+    are y/z): S o S of the local interior runs while the remote halos are in flight."""
+    outs = run_ranks(ranks, WORKER, ["jacobi", "48,48,48"],  # a cube: cut along z, then y (8 ranks: 1x2x4)
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
-                                "MP_TEMPORAL": temporal})
+                                "MP_TEMPORAL": temporal, "MP_EXPECT_OVERLAP": "1"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 

@@ -35,3 +35,9 @@ def test_jacobi_ranks_match_oracle():
 def test_race_canary_staged(n, radius):
     """NaN-poisoned halos, iteration-tagged interiors, back-to-back exchanges with random transport jitter."""
     _ok(run_ranks(n, WORKER, ["canary", radius, "14,10,9"], env_extra={"STENCIL_JITTER_US": "300"}))
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_local_interior_ranks(n):
+    """the overlap interior of fused pairs: shrunk only at faces whose halo crosses ranks"""
+    _ok(run_ranks(n, WORKER, ["localint", "24,20,18"]))

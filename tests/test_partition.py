@@ -44,6 +44,13 @@ def test_node_partition_min_interface(st):
     rx.set_dir(-1, 0, 0, 4)
     p = st.NodePartition(D(100, 100, 100), rx, 2, 2)
     assert p.dim().x == 1
+    # the models' MI355X cut costs (x faces count double): weak-scaled cubes are never cut along x up to 8 GPUs,
+    # with the same face bytes per GPU (1x2x4 of 1024^3: 3 links x 4 MiB, like 2x2x2)
+    c = D(2, 1, 1)
+    assert st.NodePartition(D(1024, 1024, 1024), r, 1, 8, c).dim() == D(1, 2, 4)
+    assert st.NodePartition(D(813, 813, 813), r, 1, 4, c).dim() == D(1, 2, 2)
+    assert st.NodePartition(D(645, 645, 645), r, 1, 2, c).dim() == D(1, 1, 2)
+    assert st.NodePartition(D(1024, 1024, 1024), r, 1, 8, D(1, 1, 1)).dim() == D(2, 2, 2)
 
 
 @settings(max_examples=60, deadline=None)
