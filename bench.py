@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--x2nw", type=int, default=16, help="waves per block of the fused two-step kernel (8/12/16)")
     ap.add_argument("--x2pf", type=int, default=2, help="planes of z lookahead of the fused two-step kernel (2/3/4)")
     ap.add_argument("--zchunk", type=int, default=0, help="z planes per block (0 = auto)")
+    ap.add_argument("--x2sched", type=int, default=1,
+                    help="fused-pair work split: 1 = balanced segments over the resident blocks, 0 = fixed z-chunks")
     ap.add_argument("--temporal", type=int, default=2,
                     help="steps fused per sweep: 2 = temporal blocking (one depth-2 halo exchange + one fused "
                          "S(S(u)) sweep per two steps, bitwise equal to single steps), 1 = one exchange + sweep per step")
@@ -138,6 +140,7 @@ def main():
     tune.x2nw = args.x2nw
     tune.x2pf = args.x2pf
     tune.zchunk = args.zchunk
+    tune.x2sched = args.x2sched
     overlap = not args.no_overlap and args.overlap != "off"
     model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=overlap,
                         auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
@@ -197,7 +200,7 @@ def main():
                                                                    model.domain.placement_dim().y,
                                                                    model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
                        "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
-                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1},
+                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2sched": args.x2sched, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
                       "gcells_per_gpu": round(gcells / n, 3)},

@@ -60,6 +60,7 @@ int main(int argc, char **argv) {
       .option(&reps, "--reps", "repetitions of the whole sweep (interleaved)")
       .option(&only, "--only", "run only 'lds', 'reg' or 'copy'");
   if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
+  std::setvbuf(stdout, nullptr, _IOLBF, 0); // progress lines reach a redirected log as they are printed
   LocalDomain ld(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
   ld.set_radius(1);
   ld.add_data<float>("d");
@@ -226,6 +227,109 @@ int main(int argc, char **argv) {
     std::printf("x2_whole,0,0,0,%.2f,0,0\nx2_interior,0,0,0,%.2f,0,0\nx2_exterior,0,0,0,%.2f,0,0\nx2_int+ext_concurrent,0,0,0,%.2f,0,0\n",
                 whole, inner, outer, both);
     }
+  }
+  for (int rep = 0; rep < reps; ++rep)
+  if (only == "ovl") {
+    // Remote-halo overlap of a fused pair on ONE GPU, the off-GPU link emulated by host-pinned memory (PCIe, about
+    // as slow as one xGMI link): the z faces are "packed" into a pinned buffer, "unpacked" from a device buffer,
+    // then the z slabs are computed. seq = pack + unpack + whole sweep on one stream (no overlap); ovl = pack ->
+    // unpack -> z slabs on a high-priority stream while the z-shrunk interior sweep runs (reserve r CUs).
+    // (CU-masked streams were tried as well: no faster, and one masked configuration hung the run.)
+    LocalDomain l2(Dim3(n, n, n), Dim3(0, 0, 0), 0, Backend::Device);
+    l2.set_radius(Radius::face_edge_corner(2, 1, 0));
+    l2.add_data<float>("d");
+    l2.realize();
+    jacobi_init(l2, 0, l2.get_full_region(), s);
+    s.sync();
+    const Rect3 c = l2.get_compute_region();
+    const Rect3 in(c.lo + Dim3(0, 0, 2), c.hi - Dim3(0, 0, 2));
+    const Dim3 pch = l2.pitch(0);
+    const int64_t faceBytes = 2 * pch.x * pch.y * 4; // two planes
+    char *hostBuf = nullptr, *devBuf = nullptr;
+    HIP_CHECK(hipHostMalloc((void **)&hostBuf, 2 * faceBytes, hipHostMallocDefault));
+    HIP_CHECK(hipMalloc((void **)&devBuf, 2 * faceBytes));
+    std::vector<CopySeg> packSegs, unpackSegs;
+    char *cur = static_cast<char *>(l2.curr_data(0));
+    const int64_t zlo = l2.radius().z(-1), nz = l2.size().z;
+    for (int k = 0; k < 2; ++k) {
+      const int64_t zs = k == 0 ? zlo : zlo + nz - 2;  // interior planes sent
+      const int64_t zh = k == 0 ? zlo + nz : zlo - 2;  // halo planes received (periodic self)
+      const Dim3 ext(faceBytes / 4, 1, 1);
+      packSegs.push_back(make_copy_seg(StridedBox{cur + zs * pch.x * pch.y * 4, 0, 0},
+                                       StridedBox{hostBuf + k * faceBytes, 0, 0}, ext, 4));
+      unpackSegs.push_back(make_copy_seg(StridedBox{devBuf + k * faceBytes, 0, 0},
+                                         StridedBox{cur + zh * pch.x * pch.y * 4, 0, 0}, ext, 4));
+    }
+    finalize_segs(packSegs);
+    finalize_segs(unpackSegs);
+    CopyPlan pk = make_copy_plan(packSegs, 0), up = make_copy_plan(unpackSegs, 0);
+    StencilTune t;
+    Stream hi(0, Priority::HIGH);
+    Event e(0), e2(0);
+    const double sweep = timeit([&] { stencil7x2_apply(l2, 0, c, StencilKind::Jacobi, sph, s, t); });
+    const double packOnly = timeit([&] { copy_plan_device(pk, s); });
+    const double seq = timeit([&] {
+      copy_plan_device(pk, s);
+      copy_plan_device(up, s);
+      stencil7x2_apply(l2, 0, c, StencilKind::Jacobi, sph, s, t);
+    });
+    std::printf("ovl_sweep,0,0,0,%.2f,0,0\novl_pack_pinned,0,0,0,%.2f,0,0\novl_seq,0,0,0,%.2f,0,0\n", sweep, packOnly, seq);
+    const double ext = timeit([&] { stencil7x2_apply_exterior(l2, 0, in, StencilKind::Jacobi, sph, s, t); });
+    std::printf("ovl_zslabs_alone,0,0,0,%.2f,0,0\n", ext);
+    // extAfter: the slabs run on the compute stream after the interior sweep (whole GPU) instead of on the comm
+    // stream behind the unpack (few CUs while the sweep holds the rest)
+    auto overlapped = [&](hipStream_t cs, hipStream_t ms, int reserve, bool extAfter = false, int lim = 0) {
+      StencilTune ti = t;
+      ti.reserveCUs = reserve;
+      return timeit([&] {
+        e.record(s);
+        e.wait_on(ms);
+        e.wait_on(cs);
+        copy_plan_device(pk, ms, lim);
+        copy_plan_device(up, ms, lim);
+        if (!extAfter) stencil7x2_apply_exterior(l2, 0, in, StencilKind::Jacobi, sph, ms, t);
+        stencil7x2_apply(l2, 0, in, StencilKind::Jacobi, sph, cs, ti);
+        e2.record(ms);
+        e2.wait_on(extAfter ? cs : s);
+        if (extAfter) stencil7x2_apply_exterior(l2, 0, in, StencilKind::Jacobi, sph, cs, t);
+        e.record(cs);
+        e.wait_on(s);
+      });
+    };
+    for (int r : {0, 8, 16})
+      std::printf("ovl_reserve%d,0,0,0,%.2f,0,0\n", r, overlapped(s, hi, r));
+    for (int r : {0, 4, 8, 16})
+      std::printf("ovl_extafter_reserve%d,0,0,0,%.2f,0,0\n", r, overlapped(s, hi, r, true));
+    // comm kernels confined to `lim` CUs (copy_plan_device maxBlocks) beside a sweep that leaves `r` CUs free
+    for (int lim : {4, 8, 16})
+      for (int r : {4, 8, 16}) {
+        if (r < lim) continue;
+        std::printf("ovl_lim%d_reserve%d,0,0,0,%.2f,0,0\n", lim, r, overlapped(s, hi, r, true, lim));
+        std::printf("ovl_lim%d_reserve%d_extcomm,0,0,0,%.2f,0,0\n", lim, r, overlapped(s, hi, r, false, lim));
+      }
+    {
+      const double p8 = timeit([&] { copy_plan_device(pk, s, 8); });
+      std::printf("ovl_pack_pinned_lim8,0,0,0,%.2f,0,0\n", p8);
+    }
+    {
+      StencilTune tc = t;
+      tc.x2sched = 0; // fixed z-chunks (several rounds of blocks) instead of balanced segments
+      const double ch = timeit([&] {
+        e.record(s);
+        e.wait_on(hi);
+        copy_plan_device(pk, hi);
+        copy_plan_device(up, hi);
+        stencil7x2_apply(l2, 0, in, StencilKind::Jacobi, sph, s, tc);
+        e2.record(hi);
+        e2.wait_on(s);
+        stencil7x2_apply_exterior(l2, 0, in, StencilKind::Jacobi, sph, s, t);
+      });
+      std::printf("ovl_extafter_chunks,0,0,0,%.2f,0,0\n", ch);
+    }
+    free_copy_plan(pk);
+    free_copy_plan(up);
+    HIP_CHECK(hipHostFree(hostBuf));
+    HIP_CHECK(hipFree(devBuf));
   }
   for (int rep = 0; rep < reps; ++rep)
   if (only == "x2pp") {

@@ -145,6 +145,12 @@ public:
   // block the host until the last exchange is complete (checks device-side timeouts)
   void sync_exchange();
   hipStream_t comm_stream(size_t di) const;
+  // confine the pack / unpack kernels of the off-GPU transports (not the same-device translate) to at most n
+  // 1024-thread blocks, i.e. n CUs (0 = one block per work item, the whole GPU). Used while an overlapped compute
+  // grid holds every other CU: measured on one MI355X (bench_stencil --only ovl) a 4 MiB pack beside the interior
+  // sweep costs the pair ~80 us unconfined (its blocks land on CUs the sweep's blocks then wait for) and ~25 us
+  // confined to 8 CUs beside a sweep that leaves 8 free.
+  void set_comm_max_blocks(int n) { commBlocks_ = n; }
   void swap();
 
   // ---- output ----
@@ -176,6 +182,7 @@ private:
   MethodFlags flags_ = MethodFlags::All;
   PlacementStrategy strategy_ = PlacementStrategy::NodeAware;
   Dim3 axisCost_{1, 1, 1};
+  int commBlocks_ = 0;
   Backend backend_ = Backend::Device;
   bool backendSet_ = false;
   bool realized_ = false;

@@ -72,7 +72,8 @@ struct CopyPlan {
 // build + upload (device must be current). Segments must be finalized.
 CopyPlan make_copy_plan(const std::vector<CopySeg> &segs, int device);
 void free_copy_plan(CopyPlan &p);
-void copy_plan_device(const CopyPlan &p, hipStream_t stream);
+// maxBlocks > 0: at most that many 1024-thread blocks (one CU each) walk the work table (see copy.hip)
+void copy_plan_device(const CopyPlan &p, hipStream_t stream, int maxBlocks = 0);
 // one-shot helper (allocates a temporary plan, synchronous)
 void copy_segs_device_sync(std::vector<CopySeg> segs, int device);
 

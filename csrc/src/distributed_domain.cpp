@@ -80,7 +80,7 @@ struct SegList {
       }
     }
   }
-  void run_device(int v, hipStream_t s) const { copy_plan_device(plan[v], s); }
+  void run_device(int v, hipStream_t s, int maxBlocks = 0) const { copy_plan_device(plan[v], s, maxBlocks); }
   void run_host(int v) const { copy_segs_host(host[v]); }
   void release() {
     for (auto &p : plan) free_copy_plan(p);
@@ -943,7 +943,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
       for (int ci : ctx.coloSend) credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownBlock));
       wait_flags_device(credits, I.epoch - 2, I.errDev, 1, I.waitTimeout, S(ctx));
     }
-    ctx.coloPack.run_device(cv, S(ctx));
+    ctx.coloPack.run_device(cv, S(ctx), commBlocks_);
     std::vector<uint64_t *> arrived;
     for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
     signal_flags_device(arrived, I.epoch, S(ctx));
@@ -956,7 +956,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
     for (auto &ctx : I.devs) {
       if (ctx.rcclSend.empty()) continue;
       HIP_CHECK(hipSetDevice(ctx.dev));
-      ctx.rcclPack.run_device(parity, S(ctx));
+      ctx.rcclPack.run_device(parity, S(ctx), commBlocks_);
     }
     NCCL_CHECK(ncclGroupStart());
     for (auto &ctx : I.devs) {
@@ -971,7 +971,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
     for (auto &ctx : I.devs) {
       if (ctx.rcclRecv.empty()) continue;
       HIP_CHECK(hipSetDevice(ctx.dev));
-      ctx.rcclUnpack.run_device(parity, S(ctx));
+      ctx.rcclUnpack.run_device(parity, S(ctx), commBlocks_);
     }
   }
 
@@ -984,7 +984,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
       for (auto &ctx : I.devs) {
         if (ctx.stagedSend.empty()) continue;
         HIP_CHECK(hipSetDevice(ctx.dev));
-        ctx.stagedPack.run_device(parity, S(ctx));
+        ctx.stagedPack.run_device(parity, S(ctx), commBlocks_);
         for (int ci : ctx.stagedSend)
           HIP_CHECK(hipMemcpyAsync(I.chans[ci].hbuf, I.chans[ci].dbuf, size_t(I.chans[ci].bytes), hipMemcpyDeviceToHost,
                                    S(ctx)));
@@ -1003,7 +1003,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
           HIP_CHECK(hipMemcpyAsync(I.chans[ci].dbuf, I.chans[ci].hbuf, size_t(I.chans[ci].bytes), hipMemcpyHostToDevice,
                                    S(ctx)));
         }
-        ctx.stagedUnpack.run_device(parity, S(ctx));
+        ctx.stagedUnpack.run_device(parity, S(ctx), commBlocks_);
       }
     }
   }
@@ -1020,7 +1020,7 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
       credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
     }
     wait_flags_device(arrived, I.epoch, I.errDev, 2, I.waitTimeout, S(ctx));
-    ctx.coloUnpack.run_device(cv, S(ctx));
+    ctx.coloUnpack.run_device(cv, S(ctx), commBlocks_);
     signal_flags_device(credits, I.epoch, S(ctx));
   }
 

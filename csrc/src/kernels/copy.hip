@@ -74,12 +74,12 @@ template <> struct VecOf<1> { using T = uint8_t; };
 constexpr uint32_t kItems = 4;
 
 template <uint32_t V, uint32_t MAXN>
-__device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w) {
+__device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w, uint32_t tid) {
   using T = typename VecOf<V>::T;
   const uint32_t ru = s.row_units, ny = s.ny;
   const int64_t sys = s.src_ystride, szs = s.src_zstride, dys = s.dst_ystride, dzs = s.dst_zstride;
   const uint32_t n = w.rows ? ru : 1;
-  for (uint32_t base = threadIdx.x; base < w.count; base += 256 * kItems) {
+  for (uint32_t base = tid; base < w.count; base += 256 * kItems) {
     T v[kItems][MAXN];
     char *dps[kItems];
 #pragma unroll
@@ -115,26 +115,42 @@ __device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w) 
   }
 }
 
+__device__ __forceinline__ void copy_work(const CopySeg &s, const CopyWork &w, uint32_t tid) {
+  switch (s.vec) {
+  case 16:
+    copy_items<16, 4>(s, w, tid);
+    break;
+  case 8:
+    copy_items<8, 4>(s, w, tid);
+    break;
+  case 4:
+    copy_items<4, 4>(s, w, tid);
+    break;
+  case 2:
+    copy_items<2, 4>(s, w, tid);
+    break;
+  default:
+    copy_items<1, 4>(s, w, tid);
+    break;
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_plan_kernel(const CopySeg *__restrict__ segs,
                                                         const CopyWork *__restrict__ work) {
   const CopyWork w = work[blockIdx.x];
-  const CopySeg s = segs[w.seg];
-  switch (s.vec) {
-  case 16:
-    copy_items<16, 4>(s, w);
-    break;
-  case 8:
-    copy_items<8, 4>(s, w);
-    break;
-  case 4:
-    copy_items<4, 4>(s, w);
-    break;
-  case 2:
-    copy_items<2, 4>(s, w);
-    break;
-  default:
-    copy_items<1, 4>(s, w);
-    break;
+  copy_work(segs[w.seg], w, threadIdx.x);
+}
+
+// Few-CU form (copy_plan_device with maxBlocks): 1024-thread blocks of four independent 256-thread groups, each
+// walking the work table with a grid stride. A launch of B blocks then occupies at most B CUs for its whole
+// duration, so it can run beside a grid that holds every other CU (an overlapped interior sweep) without taking
+// the CUs that grid's blocks need.
+__global__ __launch_bounds__(1024) void copy_plan_kernel_narrow(const CopySeg *__restrict__ segs,
+                                                                const CopyWork *__restrict__ work, uint32_t nwork) {
+  const uint32_t g = threadIdx.x >> 8; // wave-uniform (a group is 4 whole waves)
+  for (uint32_t wi = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + g); wi < nwork; wi += gridDim.x * 4) {
+    const CopyWork w = work[wi];
+    copy_work(segs[w.seg], w, threadIdx.x & 255);
   }
 }
 
@@ -171,9 +187,15 @@ void free_copy_plan(CopyPlan &p) {
   p.nwork = 0;
 }
 
-void copy_plan_device(const CopyPlan &p, hipStream_t stream) {
+void copy_plan_device(const CopyPlan &p, hipStream_t stream, int maxBlocks) {
   if (!p.nwork) return;
-  hipLaunchKernelGGL(copy_plan_kernel, dim3(p.nwork), dim3(256), 0, stream, p.dsegs, p.dwork);
+  if (maxBlocks > 0) {
+    const int blocks = std::min(maxBlocks, (p.nwork + 3) / 4);
+    hipLaunchKernelGGL(copy_plan_kernel_narrow, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dwork,
+                       uint32_t(p.nwork));
+  } else {
+    hipLaunchKernelGGL(copy_plan_kernel, dim3(p.nwork), dim3(256), 0, stream, p.dsegs, p.dwork);
+  }
   HIP_CHECK(hipGetLastError());
 }
 

@@ -97,6 +97,8 @@ void StencilModel::init() {
     // forced overlap without remote halos (one GPU): the classic full split, exercises every slab kernel
     pairInteriors_ = remote ? li : dd_->get_interior();
     for (const auto &r : pairInteriors_) overlap_ = overlap_ && !r.empty();
+    // the sweep leaves x2reserve CUs free and the transports' pack/unpack kernels stay on that many CUs
+    if (overlap_) dd_->set_comm_max_blocks(cfg_.tune.x2reserve);
   }
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
