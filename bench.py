@@ -35,8 +35,8 @@ def main():
     ap.add_argument("--variant", type=int, default=2,
                     help="single-step kernel variant (2: VALU LDS z-march, 8: MFMA x-line update; needs --temporal 1)")
     ap.add_argument("--nw", type=int, default=8, help="waves per block of the stencil kernel")
-    ap.add_argument("--x2nw", type=int, default=16, help="waves per block of the fused two-step kernel (8/12/16)")
-    ap.add_argument("--x2pf", type=int, default=2, help="planes of z lookahead of the fused two-step kernel (2/3/4)")
+    ap.add_argument("--x2nw", type=int, default=12, help="waves per block of the fused two-step kernel (8/12/16)")
+    ap.add_argument("--x2pf", type=int, default=3, help="planes of z lookahead of the fused two-step kernel (1/2/3)")
     ap.add_argument("--zchunk", type=int, default=0, help="z planes per block (0 = auto)")
     ap.add_argument("--x2sched", type=int, default=1,
                     help="fused-pair work split: 1 = balanced segments over the resident blocks, 0 = fixed z-chunks")

@@ -47,8 +47,9 @@ struct StencilTune {
   int zchunk = 0; // planes per block (0 = auto: exactly one round of resident blocks)
   int nw = 8;     // waves per block stacked in y (deep-lookahead variants: 4/8/16)
   // fused-pair kernel (stencil7x2): waves per block (8/12/16, one src row each, NW-4 output rows) and planes of
-  // z lookahead (2/3/4)
-  int x2nw = 16, x2pf = 2;
+  // z lookahead (1/2/3). 12 waves get 3 waves/SIMD and up to 168 VGPRs (no spills at any lookahead, fp32 or fp64);
+  // one MI355X, 512^3, bench.py: 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s
+  int x2nw = 12, x2pf = 3;
   // fused-pair work split: 1 (default) = one block per resident slot, each taking an equal share of the
   // (column, plane) space (one or two z segments): no partly empty last round and the fewest warm-up planes;
   // 0 = fixed z-chunks per block column (zchunk / auto)

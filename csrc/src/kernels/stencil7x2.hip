@@ -110,7 +110,8 @@ template <typename F, int... I> __device__ __forceinline__ bool run_phases(F &f,
 // steps before it is consumed. The march direction is a template argument of the loop body (DOWN), so selecting
 // the +z / -z neighbour costs nothing.
 template <typename T, int NW, int PF, int KIND, bool REMAP>
-__global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a) {
+// 12 waves: 3 per SIMD, so the register budget is 168 VGPRs (4 waves/SIMD for 8 and 16: 128)
+__global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel(StencilArgs<T> a) {
   using NV = typename Vec16<T>::native;
   using P2 = typename Pk<T>::t;
   constexpr int V = Vec16<T>::N;
@@ -130,28 +131,32 @@ __global__ __launch_bounds__(64 * NW, 4) void stencil7x2_kernel(StencilArgs<T> a
   // z-chunk. Segment mode (a.seg): gridDim.x = the resident block slots, each takes an equal share, i.e. one or
   // two z segments of about ncols * nz / slots planes: no partly empty last round of blocks, and the fewest
   // 4-plane warm-ups per useful plane.
-  const int64_t nzt = a.hiz - a.loz;
-  int64_t s, e;
+  // 32-bit block-uniform bookkeeping (the host guarantees ncols * nz < 2^32): every extra live register of the
+  // loop around the march would be spilled from the march's hot loop, which uses all 128 VGPRs
+  const uint32_t nzt = uint32_t(a.hiz - a.loz);
+  uint32_t s, e;
   if (a.seg) {
-    const int64_t W = int64_t(a.gx) * a.gy * nzt;
-    s = int64_t(lb) * W / nb;
-    e = int64_t(lb + 1) * W / nb;
+    const uint64_t W = uint64_t(uint32_t(a.gx) * uint32_t(a.gy)) * nzt;
+    s = uint32_t(uint64_t(lb) * W / nb);
+    e = uint32_t(uint64_t(lb + 1) * W / nb);
   } else {
-    const int64_t col = lb / uint32_t(a.gz);
-    s = col * nzt + int64_t(lb % uint32_t(a.gz)) * a.zc;
-    e = min(s + a.zc, (col + 1) * nzt);
+    const uint32_t col = lb / uint32_t(a.gz);
+    s = col * nzt + (lb % uint32_t(a.gz)) * uint32_t(a.zc);
+    e = min(s + uint32_t(a.zc), (col + 1) * nzt);
   }
-  for (int seg = 0; s < e; ++seg) { // block-uniform
-  const int64_t col = s / nzt;
-  const int zo = int(s - col * nzt);
-  const int nzs = int(min<int64_t>(nzt - zo, e - s));
-  s += nzs;
-  const int bx = int(col / a.gy), by = int(col - int64_t(bx) * a.gy);
-  const int zs = a.loz + zo;
-  const int ze = zs + nzs;
   // alternate the march direction between neighbouring pieces of a column, so the planes two pieces share are
   // read by both at about the same time (warm-up of one, tail of the other)
-  const bool down = ((a.seg ? ((lb + uint32_t(seg)) & 1) : ((zo / a.zc) & 1)) != 0) != (a.flip != 0);
+  bool odd = a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0;
+  while (s < e) { // block-uniform
+  const uint32_t col = s / nzt;
+  const int zo = int(s - col * nzt);
+  const int nzs = int(min(nzt - uint32_t(zo), e - s));
+  s += uint32_t(nzs);
+  const int bx = int(col / uint32_t(a.gy)), by = int(col - uint32_t(bx) * uint32_t(a.gy));
+  const int zs = a.loz + zo;
+  const int ze = zs + nzs;
+  const bool down = odd != (a.flip != 0);
+  odd = !odd;
   const int c = bx * 64 + lane;
   const bool cvalid = c < a.nchunks;
   const int cl = cvalid ? c : a.nchunks - 1;

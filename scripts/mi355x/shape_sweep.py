@@ -1,0 +1,34 @@
+"""Per-GPU throughput of the Jacobi3D step at the sub-domain shapes of the weak-scaling ladder, on ONE GPU (all
+halos periodic self-copies): 512^3 (N=1), 645x645x323 (N=2), 813x407x407 (N=4), 1024x512x256 (N=8, 1x2x4) and
+512^3 (N=8, 2x2x2). Separates the compute-shape cost from the communication cost of the multi-GPU runs."""
+import argparse
+import json
+import time
+
+import torch
+
+import stencil2_amd as st
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, default=32)
+ap.add_argument("--shapes", default="512x512x512,645x645x323,813x407x407,1024x512x256")
+ap.add_argument("--x2sched", default="1")
+args = ap.parse_args()
+for sched in (int(v) for v in args.x2sched.split(",")):
+    for sh in args.shapes.split(","):
+        L = tuple(int(v) for v in sh.split("x"))
+        t = st.StencilTune()
+        t.x2sched = sched
+        m = st.Jacobi3D(L, gpus=[0], temporal=2, tune=t)
+        m.init()
+        m.run(8)
+        m.synchronize()
+        t0 = time.perf_counter()
+        m.run(args.steps)
+        m.synchronize()
+        dt = time.perf_counter() - t0
+        cells = L[0] * L[1] * L[2]
+        print(json.dumps({"shape": sh, "x2sched": sched, "us_per_step": round(dt / args.steps * 1e6, 1),
+                          "gcells": round(cells * args.steps / dt / 1e9, 1)}), flush=True)
+        del m
+        torch.cuda.empty_cache()
