@@ -165,6 +165,7 @@ def main():
 
     # exchange-only loop on the same decomposition (halo-exchange GB/s, bench_exchange definition)
     dd = model.domain
+    dd.set_comm_max_blocks(0)  # the exchange alone may use the whole GPU (the overlapped steps confine it to 8 CUs)
     xbytes = dd.exchange_bytes_for_method(st.MethodFlags.All)
     barrier()
     t1 = time.perf_counter()

@@ -41,6 +41,10 @@ struct CopySeg {
   uint32_t pad_;
   uint64_t unit_begin; // exclusive prefix sum of units over previous segments
   uint64_t units;      // row_units * ny * nz
+  // device plans only: a second copy of the same shape and strides done by the same items (make_copy_plan pairs
+  // narrow-row segments, e.g. the +x and -x faces of a periodic self-wrap, whose rows share cache lines)
+  char *src2;
+  char *dst2;
 };
 
 // Build a segment copying a box of extent `ext` elements of `elemSize` bytes.

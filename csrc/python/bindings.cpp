@@ -460,6 +460,7 @@ PYBIND11_MODULE(_C, m) {
       .def("methods", &DistributedDomain::methods)
       .def("set_placement", &DistributedDomain::set_placement)
       .def("set_axis_cost", &DistributedDomain::set_axis_cost)
+      .def("set_comm_max_blocks", &DistributedDomain::set_comm_max_blocks)
       .def("set_gpus", &DistributedDomain::set_gpus)
       .def("gpus", &DistributedDomain::gpus)
       .def("set_backend", &DistributedDomain::set_backend)

@@ -73,15 +73,16 @@ template <> struct VecOf<1> { using T = uint8_t; };
 // flight together instead of one round trip per item.
 constexpr uint32_t kItems = 4;
 
-template <uint32_t V, uint32_t MAXN>
+template <uint32_t V, uint32_t MAXN, bool PAIR>
 __device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w, uint32_t tid) {
   using T = typename VecOf<V>::T;
   const uint32_t ru = s.row_units, ny = s.ny;
   const int64_t sys = s.src_ystride, szs = s.src_zstride, dys = s.dst_ystride, dzs = s.dst_zstride;
   const uint32_t n = w.rows ? ru : 1;
   for (uint32_t base = tid; base < w.count; base += 256 * kItems) {
-    T v[kItems][MAXN];
+    T v[kItems][MAXN], v2[kItems][PAIR ? MAXN : 1];
     char *dps[kItems];
+    int64_t doff[kItems];
 #pragma unroll
     for (uint32_t k = 0; k < kItems; ++k) {
       const uint32_t it = base + k * 256;
@@ -97,11 +98,19 @@ __device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w, 
           c = item - r * ru;
         }
         const uint32_t y = r % ny, z = r / ny;
-        const T *sp = reinterpret_cast<const T *>(s.src + int64_t(z) * szs + int64_t(y) * sys + uint64_t(c) * V);
-        dps[k] = s.dst + int64_t(z) * dzs + int64_t(y) * dys + uint64_t(c) * V;
+        const int64_t soff = int64_t(z) * szs + int64_t(y) * sys + int64_t(c) * V;
+        doff[k] = int64_t(z) * dzs + int64_t(y) * dys + int64_t(c) * V;
+        const T *sp = reinterpret_cast<const T *>(s.src + soff);
+        dps[k] = s.dst + doff[k];
 #pragma unroll
         for (uint32_t u = 0; u < MAXN; ++u)
           if (u < n) v[k][u] = sp[u];
+        if constexpr (PAIR) {
+          const T *sp2 = reinterpret_cast<const T *>(s.src2 + soff);
+#pragma unroll
+          for (uint32_t u = 0; u < MAXN; ++u)
+            if (u < n) v2[k][u] = sp2[u];
+        }
       }
     }
 #pragma unroll
@@ -111,28 +120,41 @@ __device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w, 
 #pragma unroll
         for (uint32_t u = 0; u < MAXN; ++u)
           if (u < n) dp[u] = v[k][u];
+        if constexpr (PAIR) {
+          T *dp2 = reinterpret_cast<T *>(s.dst2 + doff[k]);
+#pragma unroll
+          for (uint32_t u = 0; u < MAXN; ++u)
+            if (u < n) dp2[u] = v2[k][u];
+        }
       }
   }
 }
 
-__device__ __forceinline__ void copy_work(const CopySeg &s, const CopyWork &w, uint32_t tid) {
+template <bool PAIR> __device__ __forceinline__ void copy_work_t(const CopySeg &s, const CopyWork &w, uint32_t tid) {
   switch (s.vec) {
   case 16:
-    copy_items<16, 4>(s, w, tid);
+    copy_items<16, 4, PAIR>(s, w, tid);
     break;
   case 8:
-    copy_items<8, 4>(s, w, tid);
+    copy_items<8, 4, PAIR>(s, w, tid);
     break;
   case 4:
-    copy_items<4, 4>(s, w, tid);
+    copy_items<4, 4, PAIR>(s, w, tid);
     break;
   case 2:
-    copy_items<2, 4>(s, w, tid);
+    copy_items<2, 4, PAIR>(s, w, tid);
     break;
   default:
-    copy_items<1, 4>(s, w, tid);
+    copy_items<1, 4, PAIR>(s, w, tid);
     break;
   }
+}
+
+__device__ __forceinline__ void copy_work(const CopySeg &s, const CopyWork &w, uint32_t tid) {
+  if (s.src2)
+    copy_work_t<true>(s, w, tid);
+  else
+    copy_work_t<false>(s, w, tid);
 }
 
 __global__ __launch_bounds__(256) void copy_plan_kernel(const CopySeg *__restrict__ segs,
@@ -154,15 +176,45 @@ __global__ __launch_bounds__(1024) void copy_plan_kernel_narrow(const CopySeg *_
   }
 }
 
-CopyPlan make_copy_plan(const std::vector<CopySeg> &segs, int device) {
+// Pair narrow-row segments of identical shape and strides: one item then copies the same row of both (the +x and
+// -x faces of a periodic self-wrap read and write the first and last line of every row: paired, each line is
+// fetched once). Copies in one plan are independent (one launch runs them concurrently anyway), so any pairing
+// is valid; the first compatible partner is taken.
+static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
+  std::vector<CopySeg> out;
+  std::vector<bool> used(in.size(), false);
+  auto narrow = [](const CopySeg &s) { return s.units && s.row_units <= 4 && !s.src2; };
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (used[i]) continue;
+    CopySeg a = in[i];
+    if (narrow(a))
+      for (size_t j = i + 1; j < in.size(); ++j) {
+        const CopySeg &b = in[j];
+        if (used[j] || !narrow(b) || b.vec != a.vec || b.row_units != a.row_units || b.ny != a.ny ||
+            b.units != a.units || b.src_ystride != a.src_ystride || b.src_zstride != a.src_zstride ||
+            b.dst_ystride != a.dst_ystride || b.dst_zstride != a.dst_zstride)
+          continue;
+        a.src2 = b.src;
+        a.dst2 = b.dst;
+        used[j] = true;
+        break;
+      }
+    out.push_back(a);
+  }
+  return out;
+}
+
+CopyPlan make_copy_plan(const std::vector<CopySeg> &segsIn, int device) {
   CopyPlan p;
   p.device = device;
+  std::vector<CopySeg> segs = pair_narrow_segs(segsIn);
+  finalize_segs(segs);
   std::vector<CopyWork> work;
   const uint32_t perBlockUnits = 256 * 4; // items per block
   for (uint32_t si = 0; si < segs.size(); ++si) {
     const CopySeg &s = segs[si];
     if (!s.units) continue;
-    p.bytes += s.units * s.vec;
+    p.bytes += s.units * s.vec * (s.src2 ? 2 : 1);
     const bool rows = s.row_units <= 4;
     const uint64_t items = rows ? s.units / s.row_units : s.units;
     STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
