@@ -134,7 +134,14 @@ public:
   void exchange();       // blocking: returns when every halo of every local domain is valid
   // enqueue on the comm streams; only the staged (host) path blocks the caller. With a single local device a
   // caller stream may be given: the exchange is then enqueued on it (no cross-stream events).
-  void exchange_async(hipStream_t stream = nullptr);
+  // skipAxes (prepared by prepare_skip_wrapped): leave out the same-process copies of every direction crossing
+  // those axes; their halos are then stale and only kernels that wrap in-kernel may run on the result
+  void exchange_async(hipStream_t stream = nullptr, int skipAxes = 0);
+  // axes (1 = x, 2 = y, 4 = z) along which the decomposition has one sub-domain and the grid is periodic: every
+  // sub-domain is its own neighbour there, so a kernel can read the periodic image instead of a copied halo
+  int self_wrap_axes() const;
+  // build the same-process copy plan used by exchange_async(.., axes) (a subset of self_wrap_axes())
+  void prepare_skip_wrapped(int axes);
   // make the next exchange wait for the work currently enqueued on `s` (which touches domain di)
   void record_ready(size_t di, hipStream_t s);
   // make `s` wait until the halos of domain di from the last exchange are written

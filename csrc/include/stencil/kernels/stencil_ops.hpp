@@ -63,7 +63,15 @@ struct StencilTune {
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous
   // step wrote last, which are still in the MALL / L2
   bool alternateZ = true;
+  // fused pairs only: bitmask of axes (1 = x, 2 = y, 4 = z) along which the sub-domain is its own periodic
+  // neighbour and the kernels read the periodic image in place of the halo (StencilModel sets it together with
+  // DistributedDomain::exchange_async(.., skipWrapped), which then skips those same-GPU self copies). Needs the
+  // region to span the whole compute region along wrapped axes, and for x an extent that is a multiple of the
+  // 16-B chunk (>= 2 chunks). 0 = read halos.
+  int wrap = 0;
 };
+// axes (mask as StencilTune::wrap) the fused-pair kernels can wrap in-kernel for this quantity's layout
+int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi);
 
 // Halo forwarding: the producer writes its neighbours' halos. For every direction whose receiving halo lives in a
 // sub-domain this process can store into directly (same GPU, or a P2P-mapped peer GPU over xGMI), the stencil
@@ -122,7 +130,7 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
                       hipStream_t stream, const StencilTune &tune = StencilTune());
 // S o S on several small regions (the exterior slabs of an overlapped fused pair), one thread per cell
 void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
-                              const Spheres &sph, hipStream_t stream);
+                              const Spheres &sph, hipStream_t stream, int wrap = 0);
 // S o S on the compute region minus `interior` (the exterior of an overlapped fused pair): z slabs and y slabs by
 // the sweep kernel (6 waves per block for 2-row slabs), thin x slabs by a lanes-on-rows kernel
 void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &interior, StencilKind kind,

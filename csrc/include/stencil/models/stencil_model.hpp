@@ -47,6 +47,11 @@ struct StencilModelConfig {
   // per two steps, bitwise equal to two single steps); 1 = one exchange + one sweep per step. run(n) advances in
   // fused pairs (a trailing odd step is a single step); step() is always one step.
   int temporal = 1;
+  // fused pairs: along axes where the decomposition has one sub-domain (periodic self-neighbour,
+  // DistributedDomain::self_wrap_axes) the pair kernels read the periodic image in place of the halo, and the
+  // pair's exchange skips those same-GPU copies (on one MI355X at 512^3 the depth-2 self-copy is ~34 us of a ~300 us
+  // pair, mostly the strided x faces). Single steps keep the full exchange. Off: every halo is copied.
+  bool wrapSelf = true;
   bool setBackend = false;
   Backend backend = Backend::Device;
   StencilTune tune;
@@ -75,6 +80,7 @@ public:
   bool overlapping() const { return overlap_; }
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }
+  int wrap_axes() const { return pairTune_.wrap; } // axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
 
 private:
   StencilModelConfig cfg_;
@@ -89,6 +95,7 @@ private:
   bool graphs_ = false;
   bool forward_ = false;
   bool pairs_ = false; // temporal blocking active
+  StencilTune pairTune_; // cfg_.tune + the in-kernel wrap axes of the fused pairs
   std::vector<std::vector<std::unique_ptr<HaloForwarder>>> fwd_; // [domain][quantity]
   std::vector<Event> stepDone_;                                    // forwarding with several sub-domains
   hipGraphExec_t graphExec_[2] = {nullptr, nullptr};

@@ -487,8 +487,10 @@ PYBIND11_MODULE(_C, m) {
       .def("plan_summary", &DistributedDomain::plan_summary)
       .def("exchange", &DistributedDomain::exchange, py::call_guard<py::gil_scoped_release>())
       .def("exchange_async",
-           [](DistributedDomain &d, uintptr_t s) { d.exchange_async(reinterpret_cast<hipStream_t>(s)); },
-           py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
+           [](DistributedDomain &d, uintptr_t s, int skip) { d.exchange_async(reinterpret_cast<hipStream_t>(s), skip); },
+           py::arg("stream") = 0, py::arg("skip_axes") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("self_wrap_axes", &DistributedDomain::self_wrap_axes)
+      .def("prepare_skip_wrapped", &DistributedDomain::prepare_skip_wrapped)
       .def("sync_exchange", &DistributedDomain::sync_exchange, py::call_guard<py::gil_scoped_release>())
       .def("record_ready",
            [](DistributedDomain &d, size_t di, uintptr_t s) { d.record_ready(di, reinterpret_cast<hipStream_t>(s)); })
@@ -546,7 +548,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("x2pf", &StencilTune::x2pf)
       .def_readwrite("x2nw", &StencilTune::x2nw)
       .def_readwrite("x2sched", &StencilTune::x2sched)
-      .def_readwrite("x2reserve", &StencilTune::x2reserve);
+      .def_readwrite("x2reserve", &StencilTune::x2reserve)
+      .def_readwrite("wrap", &StencilTune::wrap);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())
       .def_readwrite("size", &StencilModelConfig::size)
@@ -564,6 +567,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("use_graph", &StencilModelConfig::useGraph)
       .def_readwrite("forward", &StencilModelConfig::forward)
       .def_readwrite("temporal", &StencilModelConfig::temporal)
+      .def_readwrite("wrap_self", &StencilModelConfig::wrapSelf)
       .def_property(
           "backend", [](const StencilModelConfig &c) { return c.backend; },
           [](StencilModelConfig &c, Backend b) {
@@ -588,6 +592,7 @@ PYBIND11_MODULE(_C, m) {
       .def("overlapping", &StencilModel::overlapping)
       .def("forwarding", &StencilModel::forwarding)
       .def("temporal_blocking", &StencilModel::temporal_blocking)
+      .def("wrap_axes", &StencilModel::wrap_axes)
       .def("compute_stream", [](StencilModel &mdl, size_t di) { return reinterpret_cast<uintptr_t>(mdl.compute_stream(di)); })
       .def("domain",
            [](std::shared_ptr<StencilModel> mdl) {

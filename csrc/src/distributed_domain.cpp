@@ -119,6 +119,7 @@ struct DevCtx {
   Event done, translated;
   std::vector<int> doms;
   SegList translate;              // Kernel + PeerCopy originating here (variant = parity)
+  SegList translateSkip;          // same without the directions crossing Impl::skipAxes (prepare_skip_wrapped)
   std::set<int> peerWriters;      // devices whose translate writes into this device
   std::vector<int> coloSend, coloRecv, rcclSend, rcclRecv, stagedSend, stagedRecv;
   SegList coloPack, coloUnpack;   // variant = parity*2 + slot
@@ -140,6 +141,8 @@ struct DistributedDomain::Impl {
   // host backend
   SegList hostTranslate, hostStagedPack, hostStagedUnpack;
   bool rccl = false;
+  std::vector<std::tuple<int, int, Dim3>> localTranslates; // (srcDom, dstDom, dir) of the Kernel/PeerCopy messages
+  int skipAxes = 0;                                         // axes translateSkip leaves out (0 = not prepared)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -177,6 +180,7 @@ DistributedDomain::~DistributedDomain() {
     if (c.ownBlock) (void)hipFree(c.ownBlock);
   for (auto &d : impl_->devs) {
     d.translate.release();
+    d.translateSkip.release();
     d.coloPack.release();
     d.coloUnpack.release();
     d.rcclPack.release();
@@ -512,6 +516,7 @@ void DistributedDomain::realize() {
     HIP_CHECK(hipHostGetDevicePointer((void **)&I.errDev, I.errHost, 0));
 
     // same-process direct stores
+    I.localTranslates = localTranslates;
     for (const auto &t : localTranslates) {
       const LocalDomain &s = domains_[std::get<0>(t)], &d = domains_[std::get<1>(t)];
       DevCtx &ctx = I.devs[I.devIndex[s.gpu()]];
@@ -862,10 +867,47 @@ void DistributedDomain::exchange() {
   if (exchangeStats_) timeExchange_ += pg_->allreduce_max(now_s() - t0);
 }
 
-void DistributedDomain::exchange_async(hipStream_t stream) {
+int DistributedDomain::self_wrap_axes() const {
+  STENCIL_REQUIRE(realized_, "self_wrap_axes before realize");
+  const Dim3 gdim = placement_->dim();
+  const int64_t n[3] = {gdim.x, gdim.y, gdim.z};
+  int m = 0;
+  for (int ax = 0; ax < 3; ++ax) {
+    const int64_t d[3] = {ax == 0, ax == 1, ax == 2};
+    if (n[ax] == 1 && boundary_.face_periodic(int(d[0]), int(d[1]), int(d[2])) &&
+        boundary_.face_periodic(-int(d[0]), -int(d[1]), -int(d[2])))
+      m |= 1 << ax;
+  }
+  return m;
+}
+
+void DistributedDomain::prepare_skip_wrapped(int axes) {
+  STENCIL_REQUIRE(realized_, "prepare_skip_wrapped before realize");
+  STENCIL_REQUIRE((axes & ~self_wrap_axes()) == 0,
+                  "axes " << axes << " are not self-periodic (self_wrap_axes = " << self_wrap_axes() << ")");
+  Impl &I = *impl_;
+  if (axes == I.skipAxes || backend_ == Backend::Host) return;
+  for (auto &ctx : I.devs) {
+    ctx.translateSkip.release();
+    ctx.translateSkip = SegList();
+  }
+  for (const auto &t : I.localTranslates) {
+    const Dim3 dir = std::get<2>(t);
+    if (((axes & 1) && dir.x != 0) || ((axes & 2) && dir.y != 0) || ((axes & 4) && dir.z != 0)) continue;
+    const LocalDomain &sd = domains_[std::get<0>(t)], &dd = domains_[std::get<1>(t)];
+    DevCtx &ctx = I.devs[I.devIndex[sd.gpu()]];
+    for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p]);
+  }
+  for (auto &ctx : I.devs) ctx.translateSkip.upload(ctx.dev);
+  I.skipAxes = axes;
+}
+
+void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   STENCIL_REQUIRE(realized_, "exchange before realize");
   TraceRange tr("DD::exchange()");
   Impl &I = *impl_;
+  STENCIL_REQUIRE(skipAxes == 0 || backend_ == Backend::Host || skipAxes == I.skipAxes,
+                  "exchange_async(skipAxes=" << skipAxes << ") without prepare_skip_wrapped(" << skipAxes << ")");
   comm::ProcGroup &pg = *pg_;
   const int parity = domains_.empty() ? 0 : domains_[0].parity();
   for (auto &d : domains_) STENCIL_REQUIRE(d.parity() == parity, "local domains out of swap() lockstep");
@@ -927,7 +969,8 @@ void DistributedDomain::exchange_async(hipStream_t stream) {
   for (auto &ctx : I.devs) {
     HIP_CHECK(hipSetDevice(ctx.dev));
     TraceRange t("kernel/peer translate");
-    if (!ctx.translate.host[parity].empty()) ctx.translate.run_device(parity, S(ctx));
+    const SegList &tl = skipAxes != 0 ? ctx.translateSkip : ctx.translate;
+    if (!tl.host[parity].empty()) tl.run_device(parity, S(ctx));
     if (!over) ctx.translated.record(S(ctx)); // events only matter across streams
   }
 

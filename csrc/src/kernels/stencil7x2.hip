@@ -171,15 +171,31 @@ __global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy && cvalid;
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1; // outer waves: garbage u1, never consumed
 
-  const int yc = y < 0 ? 0 : (y > a.rawYm1 ? a.rawYm1 : y);
+  // y-wrapped rows read their periodic image (one conditional shift: rows reach 2 beyond the region, ny >= 2)
+  const int yw = (a.wrapm & 2) ? (y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y)) : y;
+  const int yc = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
   // addresses = wave-uniform plane base (SGPRs) + a 32-bit per-lane byte offset within the plane, so the loads and
   // stores use the saddr + voffset form and each lane holds one offset VGPR instead of 64-bit pointers
   const uint32_t rowoff = uint32_t((yc * int64_t(a.px) + xb) * int64_t(sizeof(T)));
   const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
-  auto zcl = [&](int zz) { return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz); };
-  auto rowp = [&](int zz) -> const T * {
-    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy) + rowoff);
+  // x wrap: the first interior chunk reads its left edge cells (x-1, x-2) at x-1+nx, x-2+nx, the last one its right
+  // edge cells at x+V-nx, x+V+1-nx (the other edge pair of such a lane is never consumed and stays in the row,
+  // stencil7x2_wrappable_axes); every other lane reads the edge cells beside its chunk
+  int xdelta = 0;
+  if (a.wrapm & 1) xdelta = xb == a.wlo[0] ? a.wn[0] : (xb + V == a.wlo[0] + a.wn[0] ? -a.wn[0] : 0);
+  // byte offset of the edge pointer from (plane base - 64 B): a right-wrap lane's pointer can sit up to 2 cells
+  // before raw x = 0 (inside the row's front padding), so on raw row 0 the offset from the plane base is negative;
+  // the 64-B bias keeps the unsigned 32-bit offset >= 0 (the front padding is < 64 B)
+  const uint32_t edgeoff = uint32_t(int(rowoff) + 64 + xdelta * int(sizeof(T)));
+  // z wrap (block-uniform): consumed planes reach 2 beyond the region (one conditional shift, nz >= 2); deeper
+  // lookahead planes are never consumed and only need a valid address (the clamp)
+  const int zwn = (a.wrapm & 4) ? a.wn[2] : 0, zwlo = a.wlo[2], zwhi = a.wlo[2] + zwn;
+  auto zcl = [&](int zz) { // branch-free (zwn = 0: identity shifts), so the unrolled march stays one basic block
+    zz += zz < zwlo ? zwn : 0;
+    zz -= zz >= zwhi ? zwn : 0;
+    return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
   };
+  auto planep = [&](int zz) -> const char * { return reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy); };
   // sphere membership of the row at plane P: y/z part once per row, per-cell test only for the few hit rows
   struct RowSph {
     int dh, dc;
@@ -233,15 +249,17 @@ __global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel
     NV Ub, Uc, Ua;        // u1 planes z-dz, z, z+dz
     P2 UcE, UaE;          // u1 at (x-1, x+V), planes z and z+dz
     auto load_row = [&](int zz, int k) {
-      const T *p = rowp(zz);
+      const char *b = planep(zz);
+      const T *p = reinterpret_cast<const T *>(b + rowoff);
+      const T *pe = reinterpret_cast<const T *>((b - 64) + edgeoff);
       // every lane loads the edge scalars (in-row addresses, same cache lines as the chunk; only the edge lanes
       // use them): masked loads would sit behind exec branches, and the waitcnt pass, counting the path that skips
       // them, would then wait on this step's own loads and void the lookahead
       C[k] = *reinterpret_cast<const NV *>(p);
-      CL[k] = p[-1];
-      CR[k] = p[V];
-      LL[k] = p[-2];
-      RR[k] = p[V + 1];
+      CL[k] = pe[-1];
+      CR[k] = pe[V];
+      LL[k] = pe[-2];
+      RR[k] = pe[V + 1];
     };
 
     // warm-up: the loop starts two planes early (t = -2: u1 only), window planes z0-2dz .. z0+(NC-2)dz
@@ -340,9 +358,18 @@ template <typename T, int KIND>
 __global__ __launch_bounds__(256) void stencil7x2_regions_kernel(StencilArgs<T> a, X2Regions rt) {
   const int64_t total = rt.begin[rt.n];
   const int64_t px = a.px, pxy = a.pxy;
+  auto ld = [&](int x, int y, int z) -> T {
+    return a.src[int64_t(wrap_coord(a, z, 2)) * pxy + int64_t(wrap_coord(a, y, 1)) * px + wrap_coord(a, x, 0)];
+  };
   auto u1 = [&](int x, int y, int z) -> T {
-    const T *p = a.src + int64_t(z) * pxy + int64_t(y) * px + x;
-    const T v = sum6<T, KIND>(p[1], p[-1], p[px], p[-px], p[pxy], p[-pxy]); // sum6 includes the exact /6
+    T v;
+    if (a.wrapm == 0) {
+      const T *p = a.src + int64_t(z) * pxy + int64_t(y) * px + x;
+      v = sum6<T, KIND>(p[1], p[-1], p[px], p[-px], p[pxy], p[-pxy]); // sum6 includes the exact /6
+    } else {
+      v = sum6<T, KIND>(ld(x + 1, y, z), ld(x - 1, y, z), ld(x, y + 1, z), ld(x, y - 1, z), ld(x, y, z + 1),
+                        ld(x, y, z - 1));
+    }
     return KIND == 0 ? sphere_fix(a, x, y, z, v) : v;
   };
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
@@ -399,7 +426,10 @@ __global__ __launch_bounds__(256) void stencil7x2_thin_kernel(StencilArgs<T> a, 
   const int cl = tb.lo[k][LANE] - 2 + 60 * g + lane;
   const int64_t st[3] = {1, a.px, a.pxy};
   const int rawm1[3] = {int(a.px) - 1, a.rawYm1, a.rawZm1};
-  auto clampc = [&](int c, int ax) { return c < 0 ? 0 : (c > rawm1[ax] ? rawm1[ax] : c); };
+  auto clampc = [&](int c, int ax) {
+    c = wrap_coord(a, c, ax); // wrapped axes: the periodic image (never the THIN axis of an x slab, see the host)
+    return c < 0 ? 0 : (c > rawm1[ax] ? rawm1[ax] : c);
+  };
   const T *lp = a.src + int64_t(clampc(cl, LANE)) * st[LANE];
   T v[NTV][NB];
   if constexpr (THIN == 0) {
@@ -512,6 +542,32 @@ bool stencil7x2_supported(const LocalDomain &dom, int64_t qi) {
   return aligned && lox - 2 + dom.pad_x(qi) >= 0 && lox + nchunks * V + 1 < p.x - dom.pad_x(qi);
 }
 
+int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi) {
+  if (!stencil7x2_supported(dom, qi)) return 0;
+  const int64_t es = dom.elem_size(qi), V = 16 / es;
+  const int64_t lox = dom.radius().x(-1), nx = dom.size().x, px = dom.pitch(qi).x, pad = dom.pad_x(qi);
+  // x: whole chunks only (the chunk grid starts at the 16-B aligned lox), at least two, and the last chunk not on
+  // lane 0 of its column (a wrap lane shifts both of its edge pairs: its other edge must be the unused one, never a
+  // column boundary); the unused edge pair of a wrap lane (x-2 .. x+V+1 shifted by +-nx) must stay in the row
+  const bool x = nx % V == 0 && nx >= 2 * V && (nx / V) % 64 != 1 && lox - V - 2 + pad >= 0 &&
+                 lox + nx + V + 1 < px - pad;
+  // y / z: one conditional shift maps the 2 cells beyond a face onto the grid
+  return (x ? 1 : 0) | (dom.size().y >= 2 ? 2 : 0) | (dom.size().z >= 2 ? 4 : 0);
+}
+
+// along wrapped axes the region must be the whole compute region (the kernels wrap at its faces)
+static void check_wrap(const LocalDomain &dom, int64_t qi, const Rect3 &region, int wrap) {
+  if (wrap == 0) return;
+  STENCIL_REQUIRE((wrap & ~stencil7x2_wrappable_axes(dom, qi)) == 0,
+                  "in-kernel wrap " << wrap << " not supported by this layout (" << stencil7x2_wrappable_axes(dom, qi) << ")");
+  const Rect3 cr = dom.get_compute_region();
+  const int64_t lo[3] = {region.lo.x, region.lo.y, region.lo.z}, hi[3] = {region.hi.x, region.hi.y, region.hi.z};
+  const int64_t clo[3] = {cr.lo.x, cr.lo.y, cr.lo.z}, chi[3] = {cr.hi.x, cr.hi.y, cr.hi.z};
+  for (int ax = 0; ax < 3; ++ax)
+    STENCIL_REQUIRE(!((wrap >> ax) & 1) || (lo[ax] == clo[ax] && hi[ax] == chi[ax]),
+                    "region " << region << " does not span wrapped axis " << ax << " of " << cr);
+}
+
 template <typename T, int KIND, int NW, int PF>
 static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
                        const StencilTune &tune) {
@@ -519,6 +575,7 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
+  a.wrapm = tune.wrap;
   const int rxm = int(dom.radius().x(-1));
   const int off = ((a.lox - rxm) % V + V) % V;
   a.x0 = a.lox - off;
@@ -565,6 +622,7 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   const Rect3 cr = dom.get_compute_region();
   STENCIL_REQUIRE(cr.contains(region.lo) && region.hi.x <= cr.hi.x && region.hi.y <= cr.hi.y && region.hi.z <= cr.hi.z,
                   "stencil region " << region << " outside compute region " << cr);
+  check_wrap(dom, qi, region, tune.wrap);
   const bool f32 = dom.elem_size(qi) == 4;
   const bool jac = kind == StencilKind::Jacobi;
   // shapes (rows per lane, waves per block, min waves/SIMD): 1x8 keeps everything in registers at 6 waves/SIMD;
@@ -601,9 +659,10 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
 
 template <typename T, int KIND>
 static void apply_x2_regions_t(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &rs, const Spheres &sph,
-                               hipStream_t stream) {
+                               hipStream_t stream, int wrap) {
   StencilArgs<T> a = make_args<T>(dom, qi, dom.get_compute_region(), KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth,
                                   sph);
+  a.wrapm = wrap;
   const Dim3 org = dom.accessor_origin();
   for (size_t k0 = 0; k0 < rs.size(); k0 += kMaxX2Regions) {
     X2Regions rt{};
@@ -628,7 +687,7 @@ static void apply_x2_regions_t(const LocalDomain &dom, int64_t qi, const std::ve
 }
 
 void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
-                              const Spheres &sph, hipStream_t stream) {
+                              const Spheres &sph, hipStream_t stream, int wrap) {
   STENCIL_REQUIRE(stencil7x2_supported(dom, qi), "two-step stencil needs a device fp32/fp64 quantity with depth-2 halos");
   const Rect3 cr = dom.get_compute_region();
   std::vector<Rect3> rs;
@@ -641,17 +700,18 @@ void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vec
   if (rs.empty()) return;
   dom.set_device();
   const bool f32 = dom.elem_size(qi) == 4;
+  STENCIL_REQUIRE((wrap & ~stencil7x2_wrappable_axes(dom, qi)) == 0, "in-kernel wrap " << wrap << " not supported");
   if (f32)
-    kind == StencilKind::Jacobi ? apply_x2_regions_t<float, 0>(dom, qi, rs, sph, stream)
-                                : apply_x2_regions_t<float, 1>(dom, qi, rs, sph, stream);
+    kind == StencilKind::Jacobi ? apply_x2_regions_t<float, 0>(dom, qi, rs, sph, stream, wrap)
+                                : apply_x2_regions_t<float, 1>(dom, qi, rs, sph, stream, wrap);
   else
-    kind == StencilKind::Jacobi ? apply_x2_regions_t<double, 0>(dom, qi, rs, sph, stream)
-                                : apply_x2_regions_t<double, 1>(dom, qi, rs, sph, stream);
+    kind == StencilKind::Jacobi ? apply_x2_regions_t<double, 0>(dom, qi, rs, sph, stream, wrap)
+                                : apply_x2_regions_t<double, 1>(dom, qi, rs, sph, stream, wrap);
 }
 
 template <typename T, int KIND, int THIN, int LANE, int MARCH>
 static void launch_thin(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &slabs, const Spheres &sph,
-                        hipStream_t stream) {
+                        hipStream_t stream, int wrap) {
   if (slabs.empty()) return;
   const Dim3 org = dom.accessor_origin();
   ThinTable tb{};
@@ -672,6 +732,7 @@ static void launch_thin(const LocalDomain &dom, int64_t qi, const std::vector<Re
   StencilArgs<T> a = make_args<T>(dom, qi, dom.get_compute_region(), KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth,
                                   sph);
   a.x0 = int(dom.radius().x(-1)); // raw x of the first interior cell: 16-B aligned (stencil7x2_supported)
+  a.wrapm = wrap;
   const uint32_t blocks = uint32_t((tb.wbegin[tb.n] + 3) / 4);
   if (maxT <= 2)
     hipLaunchKernelGGL((stencil7x2_thin_kernel<T, KIND, THIN, LANE, MARCH, 2>), dim3(blocks), dim3(256), 0, stream, a, tb);
@@ -682,7 +743,7 @@ static void launch_thin(const LocalDomain &dom, int64_t qi, const std::vector<Re
 
 template <typename T, int KIND>
 static void apply_exterior_t(const LocalDomain &dom, int64_t qi, const Rect3 &c, const Rect3 &in, const Spheres &sph,
-                             hipStream_t stream) {
+                             hipStream_t stream, int wrap) {
   auto nonempty = [](std::initializer_list<Rect3> l) {
     std::vector<Rect3> v;
     for (const Rect3 &r : l)
@@ -696,9 +757,9 @@ static void apply_exterior_t(const LocalDomain &dom, int64_t qi, const Rect3 &c,
                             Rect3(Dim3(c.lo.x, in.hi.y, in.lo.z), Dim3(c.hi.x, c.hi.y, in.hi.z))});
   const auto xs = nonempty({Rect3(Dim3(c.lo.x, in.lo.y, in.lo.z), Dim3(in.lo.x, in.hi.y, in.hi.z)),
                             Rect3(Dim3(in.hi.x, in.lo.y, in.lo.z), Dim3(c.hi.x, in.hi.y, in.hi.z))});
-  launch_thin<T, KIND, 2, 0, 1>(dom, qi, zs, sph, stream);
-  launch_thin<T, KIND, 1, 0, 2>(dom, qi, ys, sph, stream);
-  launch_thin<T, KIND, 0, 1, 2>(dom, qi, xs, sph, stream);
+  launch_thin<T, KIND, 2, 0, 1>(dom, qi, zs, sph, stream, wrap);
+  launch_thin<T, KIND, 1, 0, 2>(dom, qi, ys, sph, stream, wrap);
+  launch_thin<T, KIND, 0, 1, 2>(dom, qi, xs, sph, stream, wrap);
 }
 
 void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &interior, StencilKind kind,
@@ -712,6 +773,8 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
   STENCIL_REQUIRE(stencil7x2_supported(dom, qi), "two-step stencil needs a device fp32/fp64 quantity with depth-2 halos");
   STENCIL_REQUIRE(c.contains(in.lo) && in.hi.x <= c.hi.x && in.hi.y <= c.hi.y && in.hi.z <= c.hi.z,
                   "interior " << in << " outside compute region " << c);
+  // a wrapped axis is never cut by the interior: no slab is thin along it (x slabs load unwrapped row windows)
+  check_wrap(dom, qi, in, tune.wrap);
   const Dim3 lo = in.lo - c.lo, hi = c.hi - in.hi;
   if (std::max({lo.x, lo.y, lo.z, hi.x, hi.y, hi.z}) > 4) {
     // thick shells: the thread-per-cell kernel
@@ -720,16 +783,17 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
                               Rect3(Dim3(c.lo.x, in.hi.y, in.lo.z), Dim3(c.hi.x, c.hi.y, in.hi.z)),
                               Rect3(Dim3(c.lo.x, in.lo.y, in.lo.z), Dim3(in.lo.x, in.hi.y, in.hi.z)),
                               Rect3(Dim3(in.hi.x, in.lo.y, in.lo.z), Dim3(c.hi.x, in.hi.y, in.hi.z))};
-    stencil7x2_apply_regions(dom, qi, ext, kind, sph, stream);
+    stencil7x2_apply_regions(dom, qi, ext, kind, sph, stream, tune.wrap);
     return;
   }
   dom.set_device();
   const bool f32 = dom.elem_size(qi) == 4, jac = kind == StencilKind::Jacobi;
   if (f32)
-    jac ? apply_exterior_t<float, 0>(dom, qi, c, in, sph, stream) : apply_exterior_t<float, 1>(dom, qi, c, in, sph, stream);
+    jac ? apply_exterior_t<float, 0>(dom, qi, c, in, sph, stream, tune.wrap)
+        : apply_exterior_t<float, 1>(dom, qi, c, in, sph, stream, tune.wrap);
   else
-    jac ? apply_exterior_t<double, 0>(dom, qi, c, in, sph, stream)
-        : apply_exterior_t<double, 1>(dom, qi, c, in, sph, stream);
+    jac ? apply_exterior_t<double, 0>(dom, qi, c, in, sph, stream, tune.wrap)
+        : apply_exterior_t<double, 1>(dom, qi, c, in, sph, stream, tune.wrap);
 }
 
 } // namespace stencil

@@ -59,7 +59,20 @@ template <typename T> struct StencilArgs {
   int fwm[3], fwp[3];
   uint32_t fmask;
   int64_t fd[27];
+  // in-kernel periodic wrap (fused pairs, StencilTune::wrap): along every axis set in wrapm the sub-domain is its
+  // own neighbour, so a cell outside [wlo, wlo + wn) is read at its periodic image inside instead of from a halo
+  // the exchange would have to copy first (raw coordinates)
+  int wrapm;
+  int wlo[3], wn[3];
 };
+
+// periodic image of raw coordinate c along axis ax (identity unless the axis wraps)
+template <typename T> __device__ __forceinline__ int wrap_coord(const StencilArgs<T> &a, int c, int ax) {
+  if (!((a.wrapm >> ax) & 1)) return c;
+  int d = (c - a.wlo[ax]) % a.wn[ax];
+  if (d < 0) d += a.wn[ax];
+  return a.wlo[ax] + d;
+}
 
 
 // bijective XCD-aware remap: consecutive logical ids land on the same XCD (blocks b, b+8, ... share one)
@@ -101,6 +114,14 @@ inline StencilArgs<T> make_args(const LocalDomain &dom, int64_t qi, const Rect3 
   a.hiz = int(r.hi.z);
   a.rawYm1 = int(dom.raw_size().y - 1);
   a.rawZm1 = int(dom.raw_size().z - 1);
+  const Rect3 cr = dom.get_compute_region();
+  const Dim3 ce = cr.extent();
+  a.wlo[0] = int(cr.lo.x - org.x);
+  a.wlo[1] = int(cr.lo.y - org.y);
+  a.wlo[2] = int(cr.lo.z - org.z);
+  a.wn[0] = int(ce.x);
+  a.wn[1] = int(ce.y);
+  a.wn[2] = int(ce.z);
   if (kind == StencilKind::Jacobi && sph.enabled) {
     a.hx = int(sph.hot.x - org.x);
     a.hy = int(sph.hot.y - org.y);

@@ -75,6 +75,19 @@ void StencilModel::init() {
     for (int64_t q = 0; q < d.num_data() && forward_; ++q) forward_ = HaloForwarder::supported(d, q);
   if (forward_) overlap_ = false; // the halos travel inside the stencil kernel
   pairs_ = cfg_.temporal >= 2 && !forward_ && !doms0.empty();
+  // a fused pair computes the intermediate step on the halo ring too, with the sphere test at the halo cell's
+  // unwrapped coordinate: across the global periodic boundary that is -1 / L instead of L-1 / 0. The two agree
+  // unless a sphere reaches the first or last plane of an axis (only on grids much thinner in y/z than x/10):
+  // then run single steps.
+  if (pairs_ && sph_.enabled) {
+    const Dim3 L = cfg_.size;
+    for (const Dim3 &c : {sph_.hot, sph_.cold}) {
+      const int64_t cc[3] = {c.x, c.y, c.z}, ll[3] = {L.x, L.y, L.z};
+      for (int a = 0; a < 3; ++a)
+        if (cc[a] - sph_.radius < 1 || cc[a] + sph_.radius > ll[a] - 2) pairs_ = false;
+    }
+    if (!pairs_) LOG_WARN("Jacobi spheres reach a periodic face of " << L << ": temporal blocking off");
+  }
   for (const auto &d : doms0)
     for (int64_t q = 0; q < d.num_data() && pairs_; ++q) pairs_ = stencil7x2_supported(d, q);
   // Fused pairs overlap against the REMOTE part of the exchange only: the same-device translate (periodic
@@ -99,6 +112,23 @@ void StencilModel::init() {
     for (const auto &r : pairInteriors_) overlap_ = overlap_ && !r.empty();
     // the sweep leaves x2reserve CUs free and the transports' pack/unpack kernels stay on that many CUs
     if (overlap_) dd_->set_comm_max_blocks(cfg_.tune.x2reserve);
+  }
+  pairTune_ = cfg_.tune;
+  pairTune_.wrap = 0;
+  if (pairs_ && cfg_.wrapSelf && std::getenv("STENCIL_NO_WRAP") == nullptr) {
+    int w = dd_->self_wrap_axes();
+    for (size_t di = 0; di < doms0.size(); ++di) {
+      const auto &d = doms0[di];
+      for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7x2_wrappable_axes(d, q);
+      // the swept regions must span every wrapped axis (a forced full split cuts all of them)
+      const Rect3 c = d.get_compute_region();
+      const Rect3 r = overlap_ ? pairInteriors_[di] : c;
+      if (r.lo.x != c.lo.x || r.hi.x != c.hi.x) w &= ~1;
+      if (r.lo.y != c.lo.y || r.hi.y != c.hi.y) w &= ~2;
+      if (r.lo.z != c.lo.z || r.hi.z != c.hi.z) w &= ~4;
+    }
+    pairTune_.wrap = w;
+    if (w != 0) dd_->prepare_skip_wrapped(w);
   }
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
@@ -213,8 +243,8 @@ void StencilModel::enqueue_step(int k) {
     // comm stream, then the exterior slabs on the comm stream behind it; the compute stream joins them
     // the interior sweep leaves x2reserve CUs free, so the pack / flag / unpack kernels of the comm stream are
     // not queued behind a grid that holds every CU until it retires
-    dd_->exchange_async();
-    StencilTune ti = cfg_.tune;
+    dd_->exchange_async(nullptr, pairTune_.wrap);
+    StencilTune ti = pairTune_;
     ti.reserveCUs = cfg_.tune.x2reserve;
     for (size_t di = 0; di < doms.size(); ++di) {
       dd_->wait_translated(di, compute_[di]);
@@ -224,7 +254,7 @@ void StencilModel::enqueue_step(int k) {
     for (size_t di = 0; di < doms.size(); ++di) {
       hipStream_t s = dd_->comm_stream(di);
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
-        stencil7x2_apply_exterior(doms[di], q, pairInteriors_[di], cfg_.kind, sph_, s, cfg_.tune);
+        stencil7x2_apply_exterior(doms[di], q, pairInteriors_[di], cfg_.kind, sph_, s, pairTune_);
       exteriorDone_[di].record(s);
       exteriorDone_[di].wait_on(compute_[di]);
     }
@@ -233,12 +263,12 @@ void StencilModel::enqueue_step(int k) {
   if (k == 2) {
     // temporal blocking: one depth-2 exchange, then S o S on every sub-domain
     const bool single = device && doms.size() == 1;
-    dd_->exchange_async(single ? compute_[0].get() : nullptr);
+    dd_->exchange_async(single ? compute_[0].get() : nullptr, pairTune_.wrap);
     for (size_t di = 0; di < doms.size(); ++di) {
       hipStream_t s = device ? compute_[di].get() : nullptr;
       if (!single) dd_->wait_exchange(di, s);
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
-        stencil7x2_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, cfg_.tune);
+        stencil7x2_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, pairTune_);
     }
     return;
   }

@@ -22,7 +22,7 @@ class StencilModel:
                  quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
                  placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, auto_overlap: bool = True,
                  use_graph: bool = True, forward: bool = False, temporal: int = 1, backend=None,
-                 tune: _C.StencilTune | None = None, group=None, axis_cost=None):
+                 tune: _C.StencilTune | None = None, group=None, axis_cost=None, wrap_self: bool = True):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
         cfg.kind = kind
@@ -39,6 +39,7 @@ class StencilModel:
         cfg.use_graph = use_graph
         cfg.forward = forward
         cfg.temporal = temporal
+        cfg.wrap_self = wrap_self
         if backend is not None:
             cfg.backend = backend
         if tune is not None:
@@ -73,6 +74,10 @@ class StencilModel:
     def temporal_blocking(self) -> bool:
         """True when run() advances in fused pairs of steps (stencil7x2, one depth-2 exchange per pair)."""
         return self._m.temporal_blocking()
+
+    def wrap_axes(self) -> int:
+        """Axes (mask 1=x, 2=y, 4=z) the fused pairs read periodically in-kernel instead of from copied halos."""
+        return self._m.wrap_axes()
 
     def forwarding(self) -> bool:
         """True when the stencil kernels write the neighbours' halos directly (in-process exchanges only)."""

@@ -148,3 +148,28 @@ def test_native_ctest_cpu():
         pytest.skip("native tests not built")
     r = subprocess.run([exe, "--cpu"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("gpus", [[0], [0, 0], [0, 0, 0, 0]])
+@pytest.mark.parametrize("axes", [(True, True, True), (False, True, True), (True, True, False)])
+def test_self_wrap_axes(st, gpus, axes):
+    """self_wrap_axes: exactly the periodic axes the decomposition leaves whole (each sub-domain its own neighbour
+    there) -- the axes StencilModel's fused pairs read periodically in-kernel instead of copying halos."""
+    dd = st.DistributedDomain(24, 20, 16, group=st.make_single_group())
+    dd.set_backend(st.Backend.Host)
+    dd.set_radius(2)
+    dd.set_boundary(st.Boundary.axes(*axes))
+    dd.set_gpus(gpus)
+    q = dd.add_data("q", torch.int64)
+    dd.realize()
+    pd = dd.placement_dim()
+    want = sum(1 << a for a, (n, p) in enumerate(zip((pd.x, pd.y, pd.z), axes)) if n == 1 and p)
+    assert dd.self_wrap_axes() == want
+    dd.prepare_skip_wrapped(want)  # host backend: the full exchange runs (nothing to skip on the host path)
+    fill_coords(dd, q)
+    dd.exchange_async(0, want)
+    r = st.Radius.constant(2)
+    assert check_exchange(dd, q, r, boundary=st.Boundary.axes(*axes)) == 0
+    if want != 7:
+        with pytest.raises(Exception):
+            dd.prepare_skip_wrapped(7 & ~want)

@@ -176,6 +176,54 @@ def test_jacobi_temporal2_matches_oracle(st, size, gpus, fp64, shape):
         assert torch.equal(_gather(m), u), f"after run({n})"
 
 
+@pytest.mark.parametrize("size,fp64", [((64, 40, 36), False), ((67, 45, 33), False), ((34, 30, 28), True),
+                                       ((8, 12, 10), False), ((260, 64, 60), False), ((264, 64, 60), False),
+                                       ((130, 40, 36), True)])
+@pytest.mark.parametrize("gpus", [[0], [0, 0], [0, 0, 0, 0]])
+@pytest.mark.parametrize("kind", ["jacobi", "astaroth"])
+def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
+    """Fused pairs with in-kernel periodic wrap along the axes the decomposition leaves whole (the pair's exchange
+    skips those self copies): bitwise equal to single steps, and to the same model with wrap_self=False. x wraps only
+    for whole 16-B chunks (64, 8 fp32 and 34 fp64 do, 67 does not); run(5) ends on a single step, which refreshes
+    every halo with the full exchange."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    ms = [cls(size, gpus=gpus, fp64=fp64, temporal=2, wrap_self=w, **kw) for w in (True, False)]
+    for m in ms:
+        m.init()
+        assert m.temporal_blocking()
+    pd = ms[0].domain.placement_dim()
+    whole = sum(1 << a for a, n in enumerate((pd.x, pd.y, pd.z)) if n == 1)
+    assert ms[1].wrap_axes() == 0
+    assert ms[0].wrap_axes() & ~whole == 0 and ms[0].wrap_axes() & 6 == whole & 6
+    V = 2 if fp64 else 4
+    assert ms[0].wrap_axes() & 1 == (whole & 1 if size[0] % V == 0 and (size[0] // V) % 64 != 1 else 0)
+    u = _gather(ms[0])
+    for n in (5, 16, 2):
+        for m in ms:
+            m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        for m in ms:
+            m.synchronize()
+            assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
+
+
+def test_temporal2_spheres_at_periodic_face_fall_back(st):
+    """Spheres that reach a periodic face (radius x/10 on a thin y/z grid) make the fused pair's halo-ring step
+    differ from the neighbour's: the model runs single steps there, still equal to the oracle."""
+    m = st.Jacobi3D((260, 20, 18), gpus=[0], temporal=2)
+    m.init()
+    assert not m.temporal_blocking()
+    u = _gather(m)
+    m.run(4)
+    for _ in range(4):
+        u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
 @pytest.mark.parametrize("size", [(32, 32, 32), (67, 45, 33), (130, 70, 20)])
 @pytest.mark.parametrize("gpus", [[0], [0, 0]])
 def test_jacobi_mfma_variant_matches_oracle(st, size, gpus):
