@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--temporal", type=int, default=2,
                     help="steps fused per sweep: 2 = temporal blocking (one depth-2 halo exchange + one fused "
                          "S(S(u)) sweep per two steps, bitwise equal to single steps), 1 = one exchange + sweep per step")
+    ap.add_argument("--x2xfast", type=int, default=0, help="fused-pair column order: 1 x-major, 0 y-major")
     ap.add_argument("--wrap", type=int, default=1,
                     help="fused pairs read the periodic image along axes the decomposition leaves whole (no self-copy "
                          "of those halos); 0 = copy every halo")
@@ -144,6 +145,7 @@ def main():
     tune.x2pf = args.x2pf
     tune.zchunk = args.zchunk
     tune.x2sched = args.x2sched
+    tune.x2xfast = args.x2xfast
     overlap = not args.no_overlap and args.overlap != "off"
     model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=overlap,
                         auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
@@ -204,7 +206,7 @@ def main():
                                                                    model.domain.placement_dim().y,
                                                                    model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
                        "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
-                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2sched": args.x2sched, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
+                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
                        "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none"},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),

@@ -54,6 +54,9 @@ struct StencilTune {
   // (column, plane) space (one or two z segments): no partly empty last round and the fewest warm-up planes;
   // 0 = fixed z-chunks per block column (zchunk / auto)
   int x2sched = 1;
+  // fused-pair column order: 1 = x-major (x-adjacent columns of a y range on one XCD), 0 = y-major. One MI355X:
+  // 512^3 equal within noise (944-965 Gcells/s either way); 645/813/1024-wide shapes 2-3 % faster y-major
+  int x2xfast = 0;
   // CUs an overlapped fused-pair interior sweep leaves free for the exchange kernels of the comm stream (balanced
   // segment mode: the grid is that many blocks short of the resident slots); reserveCUs is what one launch uses
   int x2reserve = 8;

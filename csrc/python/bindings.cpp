@@ -549,7 +549,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("x2nw", &StencilTune::x2nw)
       .def_readwrite("x2sched", &StencilTune::x2sched)
       .def_readwrite("x2reserve", &StencilTune::x2reserve)
-      .def_readwrite("wrap", &StencilTune::wrap);
+      .def_readwrite("wrap", &StencilTune::wrap)
+      .def_readwrite("x2xfast", &StencilTune::x2xfast);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())
       .def_readwrite("size", &StencilModelConfig::size)

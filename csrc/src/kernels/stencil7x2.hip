@@ -109,9 +109,13 @@ template <typename F, int... I> __device__ __forceinline__ bool run_phases(F &f,
 // z: the src window holds planes z .. z+(2+PF)dz; the last PF planes are in flight, so a row load is issued PF
 // steps before it is consumed. The march direction is a template argument of the loop body (DOWN), so selecting
 // the +z / -z neighbour costs nothing.
-template <typename T, int NW, int PF, int KIND, bool REMAP>
+// WRAP (in-kernel periodic wrap, StencilTune::wrap): 0 none, 1 y/z only, 2 x too. A template value so that only
+// the x-wrap instance pays for separate edge loads (3 loads per row instead of the 2 overlapping 16-B loads the
+// compiler forms around the chunk when the edge cells are adjacent to it)
+template <typename T, int NW, int PF, int KIND, int WRAP>
 // 12 waves: 3 per SIMD, so the register budget is 168 VGPRs (4 waves/SIMD for 8 and 16: 128)
-__global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel(StencilArgs<T> a) {
+__global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4))
+__attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void stencil7x2_kernel(StencilArgs<T> a) {
   using NV = typename Vec16<T>::native;
   using P2 = typename Pk<T>::t;
   constexpr int V = Vec16<T>::N;
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel
   __shared__ T ce[2][NW][2];   // src edge scalars of the published rows: [0] at x-1 (lane 0), [1] at x+V
 
   const uint32_t nb = gridDim.x;
-  const uint32_t lb = REMAP ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
+  const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
   const int lane = threadIdx.x;
   const int w = int(threadIdx.y);
   // The block's work is a range [s, e) of the linear (column, plane) space, column = bx * gy + by (y-neighbour
@@ -152,7 +156,17 @@ __global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel
   const int zo = int(s - col * nzt);
   const int nzs = int(min(nzt - uint32_t(zo), e - s));
   s += uint32_t(nzs);
-  const int bx = int(col / uint32_t(a.gy)), by = int(col - uint32_t(bx) * uint32_t(a.gy));
+  // column order: y-major (y-neighbour columns adjacent: their shared halo rows meet in one L2) or x-major (the
+  // x-neighbour columns of a row range adjacent: the cells one column's edge lanes read from the next, and with x
+  // wrap the far row end, are read by a block of the same XCD at the same time)
+  int bx, by;
+  if (a.xfast) {
+    by = int(col / uint32_t(a.gx));
+    bx = int(col - uint32_t(by) * uint32_t(a.gx));
+  } else {
+    bx = int(col / uint32_t(a.gy));
+    by = int(col - uint32_t(bx) * uint32_t(a.gy));
+  }
   const int zs = a.loz + zo;
   const int ze = zs + nzs;
   const bool down = odd != (a.flip != 0);
@@ -172,7 +186,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1; // outer waves: garbage u1, never consumed
 
   // y-wrapped rows read their periodic image (one conditional shift: rows reach 2 beyond the region, ny >= 2)
-  const int yw = (a.wrapm & 2) ? (y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y)) : y;
+  const int yw =
+      (WRAP >= 1 && (a.wrapm & 2)) ? (y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y)) : y;
   const int yc = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
   // addresses = wave-uniform plane base (SGPRs) + a 32-bit per-lane byte offset within the plane, so the loads and
   // stores use the saddr + voffset form and each lane holds one offset VGPR instead of 64-bit pointers
@@ -182,17 +197,19 @@ __global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel
   // edge cells at x+V-nx, x+V+1-nx (the other edge pair of such a lane is never consumed and stays in the row,
   // stencil7x2_wrappable_axes); every other lane reads the edge cells beside its chunk
   int xdelta = 0;
-  if (a.wrapm & 1) xdelta = xb == a.wlo[0] ? a.wn[0] : (xb + V == a.wlo[0] + a.wn[0] ? -a.wn[0] : 0);
+  if (WRAP == 2 && (a.wrapm & 1)) xdelta = xb == a.wlo[0] ? a.wn[0] : (xb + V == a.wlo[0] + a.wn[0] ? -a.wn[0] : 0);
   // byte offset of the edge pointer from (plane base - 64 B): a right-wrap lane's pointer can sit up to 2 cells
   // before raw x = 0 (inside the row's front padding), so on raw row 0 the offset from the plane base is negative;
   // the 64-B bias keeps the unsigned 32-bit offset >= 0 (the front padding is < 64 B)
   const uint32_t edgeoff = uint32_t(int(rowoff) + 64 + xdelta * int(sizeof(T)));
   // z wrap (block-uniform): consumed planes reach 2 beyond the region (one conditional shift, nz >= 2); deeper
   // lookahead planes are never consumed and only need a valid address (the clamp)
-  const int zwn = (a.wrapm & 4) ? a.wn[2] : 0, zwlo = a.wlo[2], zwhi = a.wlo[2] + zwn;
+  const int zwn = (WRAP >= 1 && (a.wrapm & 4)) ? a.wn[2] : 0, zwlo = a.wlo[2], zwhi = a.wlo[2] + zwn;
   auto zcl = [&](int zz) { // branch-free (zwn = 0: identity shifts), so the unrolled march stays one basic block
-    zz += zz < zwlo ? zwn : 0;
-    zz -= zz >= zwhi ? zwn : 0;
+    if constexpr (WRAP >= 1) {
+      zz += zz < zwlo ? zwn : 0;
+      zz -= zz >= zwhi ? zwn : 0;
+    }
     return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
   };
   auto planep = [&](int zz) -> const char * { return reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy); };
@@ -251,7 +268,9 @@ __global__ __launch_bounds__(64 * NW, (NW == 12 ? 3 : 4)) void stencil7x2_kernel
     auto load_row = [&](int zz, int k) {
       const char *b = planep(zz);
       const T *p = reinterpret_cast<const T *>(b + rowoff);
-      const T *pe = reinterpret_cast<const T *>((b - 64) + edgeoff);
+      // 16-B aligned (rowoff, the bias and the +-nx shift of whole chunks are): the edge pairs then load as the
+      // aligned 16-B vectors around the chunk, as in the copy-halo instance
+      const T *pe = WRAP == 2 ? static_cast<const T *>(__builtin_assume_aligned((b - 64) + edgeoff, 16)) : p;
       // every lane loads the edge scalars (in-row addresses, same cache lines as the chunk; only the edge lanes
       // use them): masked loads would sit behind exec branches, and the waitcnt pass, counting the path that skips
       // them, would then wait on this step's own loads and void the lookahead
@@ -576,6 +595,7 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
   a.wrapm = tune.wrap;
+  a.xfast = tune.x2xfast;
   const int rxm = int(dom.radius().x(-1));
   const int off = ((a.lox - rxm) % V + V) % V;
   a.x0 = a.lox - off;
@@ -583,8 +603,8 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = (a.nchunks + 63) / 64;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = tune.xcdRemap ? (const void *)stencil7x2_kernel<T, NW, PF, KIND, true>
-                                   : (const void *)stencil7x2_kernel<T, NW, PF, KIND, false>;
+  a.remap = tune.xcdRemap ? 1 : 0;
+  const void *kern = (const void *)stencil7x2_kernel<T, NW, PF, KIND, 0>;
   const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x2_resident_blocks(kern, 64 * NW);
   uint32_t blocks;
@@ -607,10 +627,12 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     blocks = uint32_t(cols * a.gz);
   }
   dom.set_device();
-  if (tune.xcdRemap)
-    hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, true>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  if (a.wrapm & 1)
+    hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, 2>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  else if (a.wrapm)
+    hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, 1>), dim3(blocks), dim3(64, NW), 0, stream, a);
   else
-    hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, false>), dim3(blocks), dim3(64, NW), 0, stream, a);
+    hipLaunchKernelGGL((stencil7x2_kernel<T, NW, PF, KIND, 0>), dim3(blocks), dim3(64, NW), 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -48,6 +48,8 @@ template <typename T> struct StencilArgs {
   int zc;                           // planes per block
   int gx, gy, gz;                   // logical grid
   int seg;                          // stencil7x2: 1 = balanced (column, plane) segments over gridDim.x blocks
+  int xfast;                        // stencil7x2: 1 = column index x-major (x-adjacent columns on one XCD)
+  int remap;                        // stencil7x2: 1 = XCD-aware block remap
   // spheres, raw coordinates
   int hx, hy, hz, cx, cy, cz;
   int r1sq; // (radius+1)^2, 0 = disabled

@@ -127,6 +127,7 @@ void StencilModel::init() {
       if (r.lo.y != c.lo.y || r.hi.y != c.hi.y) w &= ~2;
       if (r.lo.z != c.lo.z || r.hi.z != c.hi.z) w &= ~4;
     }
+    if (const char *e = std::getenv("STENCIL_WRAP_AXES")) w &= std::atoi(e); // restrict (experiments)
     pairTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
