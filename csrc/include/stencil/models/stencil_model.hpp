@@ -26,9 +26,11 @@ struct StencilModelConfig {
   MethodFlags methods = MethodFlags::All;
   PlacementStrategy placement = PlacementStrategy::NodeAware;
   // NodeAware cut costs (DistributedDomain::set_axis_cost): x faces count double, so weak-scaled cubes are cut
-  // along z and y first (8 GPUs: 1x2x4 instead of 2x2x2, the same 3 x 4 MiB of face traffic per GPU for 512^3
-  // per GPU, but row-contiguous faces whose exchange the fused pairs can overlap)
-  Dim3 axisCost{2, 1, 1};
+  // along y and z only (8 GPUs: 1x4x2 instead of 2x2x2, the same face bytes per GPU for 512^3 per GPU, but
+  // row-contiguous faces whose exchange the fused pairs can overlap); y cuts cost less than z cuts so sub-domains
+  // keep long z columns for the z-marching sweeps (one MI355X, fused pairs: 1024x256x512 885 vs 1024x512x256
+  // 708-767 Gcells/s; 645x323x645 731 vs 645x645x323 704)
+  Dim3 axisCost{4, 2, 3};
   std::vector<int> gpus;       // empty = automatic
   bool overlap = true;
   // when every halo comes from this GPU (periodic self-wrap / co-resident sub-domains) the exchange is a local

@@ -1,5 +1,5 @@
 """Per-GPU throughput of the Jacobi3D step at the sub-domain shapes of the weak-scaling ladder, on ONE GPU (all
-halos periodic self-copies): 512^3 (N=1), 645x645x323 (N=2), 813x407x407 (N=4), 1024x512x256 (N=8, 1x2x4) and
+halos periodic self-copies): 512^3 (N=1), 645x323x645 (N=2), 813x407x407 (N=4), 1024x256x512 (N=8, 1x4x2) and
 512^3 (N=8, 2x2x2). Separates the compute-shape cost from the communication cost of the multi-GPU runs."""
 import argparse
 import json
@@ -11,7 +11,7 @@ import stencil2_amd as st
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=32)
-ap.add_argument("--shapes", default="512x512x512,645x645x323,813x407x407,1024x512x256")
+ap.add_argument("--shapes", default="512x512x512,645x323x645,813x407x407,1024x256x512")
 ap.add_argument("--x2sched", default="1")
 args = ap.parse_args()
 for sched in (int(v) for v in args.x2sched.split(",")):

@@ -384,7 +384,7 @@ def test_colocated_ipc_two_ranks_one_gpu(radius):
 def test_colocated_ipc_jacobi_two_ranks(temporal, ranks):
     """Jacobi over HIP IPC between ranks sharing one GPU. Fused pairs overlap automatically here (the split axes
     are y/z): S o S of the local interior runs while the remote halos are in flight."""
-    outs = run_ranks(ranks, WORKER, ["jacobi", "48,48,48"],  # a cube: cut along z, then y (8 ranks: 1x2x4)
+    outs = run_ranks(ranks, WORKER, ["jacobi", "48,48,48"],  # a cube: cut along y, then z (8 ranks: 1x4x2)
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
                                 "MP_TEMPORAL": temporal, "MP_EXPECT_OVERLAP": "1"})
     for rc, out in outs:
