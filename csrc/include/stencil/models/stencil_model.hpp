@@ -72,6 +72,7 @@ public:
   void run(int iters);
   static constexpr int kGraphSteps = 16; // even: the block starts and ends on the same buffer parity
   void synchronize();           // wait for all enqueued work (and check exchange errors)
+  void prepare();               // instantiate run()'s hipGraph blocks for both buffer parities (no work is run)
   DistributedDomain &domain() { return *dd_; }
   const StencilModelConfig &config() const { return cfg_; }
   int64_t cells() const { return cfg_.size.flatten(); } // global cells updated per step
@@ -103,6 +104,7 @@ private:
   hipGraphExec_t graphExec_[2] = {nullptr, nullptr};
   hipGraphExec_t graphBlock_[2] = {nullptr, nullptr}; // kGraphSteps steps starting at parity p
   void enqueue_step(int k = 1); // k = 1: one step; k = 2: a fused pair (temporal blocking)
+  void capture_block();         // graphBlock_[current parity] (no work is run)
   bool pair_ok() const { return pairs_; }
   int64_t steps_ = 0;
 };

@@ -62,6 +62,10 @@ class StencilModel:
     def run(self, iters: int):
         self._m.run(iters)
 
+    def prepare(self):
+        """Instantiate run()'s hipGraph blocks for both buffer parities (records work, runs nothing)."""
+        self._m.prepare()
+
     def synchronize(self):
         self._m.synchronize()
 

@@ -210,6 +210,24 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
+@pytest.mark.parametrize("temporal", [1, 2])
+def test_prepare_graph_blocks(st, temporal):
+    """prepare() records run()'s hipGraph blocks for both buffer parities without running anything: the field is
+    unchanged by it, and later runs of either parity (odd step counts in between) match the oracle."""
+    m = st.Jacobi3D((48, 40, 36), gpus=[0], temporal=temporal)
+    m.init()
+    u = _gather(m)
+    m.prepare()
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+    for n in (16, 3, 16, 1, 32):
+        m.run(n)
+        for _ in range(n):
+            u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
 def test_temporal2_spheres_at_periodic_face_fall_back(st):
     """Spheres that reach a periodic face (radius x/10 on a thin y/z grid) make the fused pair's halo-ring step
     differ from the neighbour's: the model runs single steps there, still equal to the oracle."""
