@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <set>
 #include <sstream>
 #include <thread>
@@ -296,48 +297,66 @@ void DistributedDomain::realize() {
   if (dev && any_methods(MethodFlags::Colocated) && pg.size() > 1 && pg.colocated_size() > 1 &&
       std::getenv("STENCIL_SKIP_IPC_PROBE") == nullptr) {
     TraceRange trp("ipc probe");
-    int ok = 1;
-    char *blk = nullptr;
-    HIP_CHECK(hipSetDevice(gpus_[0]));
-    if (hipExtMallocWithFlags((void **)&blk, 256, hipDeviceMallocUncached) != hipSuccess) {
-      (void)hipGetLastError();
-      ok = 0;
-    }
-    hipIpcMemHandle_t mine{};
-    if (ok && hipIpcGetMemHandle(&mine, blk) != hipSuccess) {
-      (void)hipGetLastError();
-      ok = 0;
-    }
-    if (ok) {
-      const uint64_t tag = 0x57e9c11000000000ull + uint64_t(myRank);
-      HIP_CHECK(hipMemcpy(blk, &tag, sizeof(tag), hipMemcpyHostToDevice));
-    }
-    std::vector<hipIpcMemHandle_t> all(pg.size());
-    pg.allgather(&mine, sizeof(mine), all.data());
-    std::vector<int> oks(pg.size());
-    pg.allgather(&ok, sizeof(int), oks.data());
-    for (int r = 0; r < pg.size() && ok; ++r) {
-      if (r == myRank || !pg.colocated(r) || !oks[r]) continue;
-      char *peer = nullptr;
-      if (hipIpcOpenMemHandle((void **)&peer, all[r], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-        (void)hipGetLastError();
-        ok = 0;
-        break;
-      }
-      uint64_t got = 0;
-      if (hipMemcpy(&got, peer, sizeof(got), hipMemcpyDeviceToHost) != hipSuccess ||
-          got != 0x57e9c11000000000ull + uint64_t(r)) {
+    // up to 3 collective attempts: a transient open/map failure on a busy node must not cost the transport
+    bool allOk = false;
+    for (int attempt = 0; attempt < 3 && !allOk; ++attempt) {
+      int ok = 1;
+      char *blk = nullptr;
+      HIP_CHECK(hipSetDevice(gpus_[0]));
+      if (hipExtMallocWithFlags((void **)&blk, 256, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         ok = 0;
       }
-      (void)hipIpcCloseMemHandle(peer);
+      hipIpcMemHandle_t mine{};
+      if (ok && hipIpcGetMemHandle(&mine, blk) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = 0;
+      }
+      if (ok) {
+        const uint64_t tag = 0x57e9c11000000000ull + uint64_t(myRank);
+        HIP_CHECK(hipMemcpy(blk, &tag, sizeof(tag), hipMemcpyHostToDevice));
+      }
+      std::vector<hipIpcMemHandle_t> all(pg.size());
+      pg.allgather(&mine, sizeof(mine), all.data());
+      std::vector<int> oks(pg.size());
+      pg.allgather(&ok, sizeof(int), oks.data());
+      for (int r = 0; r < pg.size() && ok; ++r) {
+        if (r == myRank || !pg.colocated(r) || !oks[r]) continue;
+        char *peer = nullptr;
+        if (hipIpcOpenMemHandle((void **)&peer, all[r], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+          (void)hipGetLastError();
+          ok = 0;
+          break;
+        }
+        uint64_t got = 0;
+        if (hipMemcpy(&got, peer, sizeof(got), hipMemcpyDeviceToHost) != hipSuccess ||
+            got != 0x57e9c11000000000ull + uint64_t(r)) {
+          (void)hipGetLastError();
+          ok = 0;
+        }
+        (void)hipIpcCloseMemHandle(peer);
+      }
+      if (std::getenv("STENCIL_IPC_PROBE_FAIL")) ok = 0; // rehearses the fallback (tests)
+      allOk = pg.allreduce_min_i64(ok) == 1;
+      pg.barrier(); // peers are done with our block
+      if (blk) (void)hipFree(blk);
     }
-    const bool allOk = pg.allreduce_min_i64(ok) == 1;
-    pg.barrier(); // peers are done with our block
-    if (blk) (void)hipFree(blk);
     if (!allOk) {
       if (myRank == 0) LOG_WARN("HIP IPC between co-located ranks is unavailable; Colocated transport disabled");
       flags_ = MethodFlags(int(flags_) & ~int(MethodFlags::Colocated));
+      // RCCL refuses two ranks on one device: co-located ranks that share a GPU then fall back to host staging
+      // (device identity by PCI bus id: ranks may see different device numberings)
+      std::vector<uint64_t> devOf(pg.size());
+      char bus[64] = {0};
+      HIP_CHECK(hipDeviceGetPCIBusId(bus, sizeof(bus), gpus_[0]));
+      const uint64_t myDev = uint64_t(std::hash<std::string>()(std::string(bus)));
+      pg.allgather(&myDev, sizeof(myDev), devOf.data());
+      bool shared = false;
+      for (int r = 0; r < pg.size(); ++r) shared |= r != myRank && pg.colocated(r) && devOf[r] == myDev;
+      if (pg.allreduce_min_i64(shared ? 0 : 1) == 0 && any_methods(MethodFlags::Rccl)) {
+        if (myRank == 0) LOG_WARN("co-located ranks share a GPU: Rccl replaced by Staged");
+        flags_ = MethodFlags((int(flags_) & ~int(MethodFlags::Rccl)) | int(MethodFlags::Staged));
+      }
     }
   }
 

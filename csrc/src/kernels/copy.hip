@@ -60,8 +60,12 @@ void copy_segs_host(const std::vector<CopySeg> &segs) {
 }
 
 template <uint32_t V> struct VecOf;
-template <> struct VecOf<16> { using T = uint4; };
-template <> struct VecOf<8> { using T = uint2; };
+// clang vector types, not HIP's uint4/uint2 (union structs that SROA will not split: the item arrays below then
+// stay a private stack frame)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <> struct VecOf<16> { using T = u32x4; };
+template <> struct VecOf<8> { using T = u32x2; };
 template <> struct VecOf<4> { using T = uint32_t; };
 template <> struct VecOf<2> { using T = uint16_t; };
 template <> struct VecOf<1> { using T = uint8_t; };
@@ -71,81 +75,99 @@ template <> struct VecOf<1> { using T = uint8_t; };
 // instruction and the strided x-face rows are spread over every lane. Each thread owns up to kItems items
 // (stride 256) and issues all their loads before any store, so the scattered x-face accesses of a thread are in
 // flight together instead of one round trip per item.
-constexpr uint32_t kItems = 4;
+constexpr uint32_t kItemsMax = 4;
 
-template <uint32_t V, uint32_t MAXN, bool PAIR>
+// N = units per item (1 for wide rows, row_units for narrow rows) is a template value: the per-thread register
+// arrays are then indexed by constants only and live in VGPRs (with a runtime n guard they stayed a 528-B private
+// stack frame: scratch traffic and a scratch setup on every launch).
+template <uint32_t V, uint32_t N, bool PAIR>
 __device__ __forceinline__ void copy_items(const CopySeg &s, const CopyWork &w, uint32_t tid) {
   using T = typename VecOf<V>::T;
+  // items in flight per thread: kItems, fewer when one item's data takes over 16 VGPRs (wide narrow-row pairs),
+  // so the 1024-thread form stays within its 128-VGPR budget without spilling
+  constexpr uint32_t kRegs = (N * (V < 4 ? 4 : V) / 4) * (PAIR ? 2 : 1);
+  constexpr uint32_t kItems = kRegs > 16 ? (kRegs > 32 ? 1 : 2) : kItemsMax;
   const uint32_t ru = s.row_units, ny = s.ny;
   const int64_t sys = s.src_ystride, szs = s.src_zstride, dys = s.dst_ystride, dzs = s.dst_zstride;
-  const uint32_t n = w.rows ? ru : 1;
   for (uint32_t base = tid; base < w.count; base += 256 * kItems) {
-    T v[kItems][MAXN], v2[kItems][PAIR ? MAXN : 1];
-    char *dps[kItems];
+    T v[kItems][N], v2[kItems][PAIR ? N : 1];
     int64_t doff[kItems];
+    bool live[kItems];
 #pragma unroll
     for (uint32_t k = 0; k < kItems; ++k) {
       const uint32_t it = base + k * 256;
-      dps[k] = nullptr;
-      if (it < w.count) {
-        const uint32_t item = w.first + it;
-        uint32_t r, c;
-        if (w.rows) {
-          r = item;
-          c = 0;
-        } else {
-          r = item / ru;
-          c = item - r * ru;
-        }
-        const uint32_t y = r % ny, z = r / ny;
-        const int64_t soff = int64_t(z) * szs + int64_t(y) * sys + int64_t(c) * V;
-        doff[k] = int64_t(z) * dzs + int64_t(y) * dys + int64_t(c) * V;
+      live[k] = it < w.count;
+      const uint32_t item = w.first + (live[k] ? it : 0);
+      uint32_t r, c;
+      if (w.rows) {
+        r = item;
+        c = 0;
+      } else {
+        r = item / ru;
+        c = item - r * ru;
+      }
+      const uint32_t y = r % ny, z = r / ny;
+      const int64_t soff = int64_t(z) * szs + int64_t(y) * sys + int64_t(c) * V;
+      doff[k] = int64_t(z) * dzs + int64_t(y) * dys + int64_t(c) * V;
+      if (live[k]) {
         const T *sp = reinterpret_cast<const T *>(s.src + soff);
-        dps[k] = s.dst + doff[k];
 #pragma unroll
-        for (uint32_t u = 0; u < MAXN; ++u)
-          if (u < n) v[k][u] = sp[u];
+        for (uint32_t u = 0; u < N; ++u) v[k][u] = sp[u];
         if constexpr (PAIR) {
           const T *sp2 = reinterpret_cast<const T *>(s.src2 + soff);
 #pragma unroll
-          for (uint32_t u = 0; u < MAXN; ++u)
-            if (u < n) v2[k][u] = sp2[u];
+          for (uint32_t u = 0; u < N; ++u) v2[k][u] = sp2[u];
         }
       }
     }
 #pragma unroll
     for (uint32_t k = 0; k < kItems; ++k)
-      if (dps[k]) {
-        T *dp = reinterpret_cast<T *>(dps[k]);
+      if (live[k]) {
+        T *dp = reinterpret_cast<T *>(s.dst + doff[k]);
 #pragma unroll
-        for (uint32_t u = 0; u < MAXN; ++u)
-          if (u < n) dp[u] = v[k][u];
+        for (uint32_t u = 0; u < N; ++u) dp[u] = v[k][u];
         if constexpr (PAIR) {
           T *dp2 = reinterpret_cast<T *>(s.dst2 + doff[k]);
 #pragma unroll
-          for (uint32_t u = 0; u < MAXN; ++u)
-            if (u < n) dp2[u] = v2[k][u];
+          for (uint32_t u = 0; u < N; ++u) dp2[u] = v2[k][u];
         }
       }
+  }
+}
+
+template <uint32_t V, bool PAIR> __device__ __forceinline__ void copy_work_v(const CopySeg &s, const CopyWork &w, uint32_t tid) {
+  switch (w.rows ? s.row_units : 1u) {
+  case 1:
+    copy_items<V, 1, PAIR>(s, w, tid);
+    break;
+  case 2:
+    copy_items<V, 2, PAIR>(s, w, tid);
+    break;
+  case 3:
+    copy_items<V, 3, PAIR>(s, w, tid);
+    break;
+  default:
+    copy_items<V, 4, PAIR>(s, w, tid);
+    break;
   }
 }
 
 template <bool PAIR> __device__ __forceinline__ void copy_work_t(const CopySeg &s, const CopyWork &w, uint32_t tid) {
   switch (s.vec) {
   case 16:
-    copy_items<16, 4, PAIR>(s, w, tid);
+    copy_work_v<16, PAIR>(s, w, tid);
     break;
   case 8:
-    copy_items<8, 4, PAIR>(s, w, tid);
+    copy_work_v<8, PAIR>(s, w, tid);
     break;
   case 4:
-    copy_items<4, 4, PAIR>(s, w, tid);
+    copy_work_v<4, PAIR>(s, w, tid);
     break;
   case 2:
-    copy_items<2, 4, PAIR>(s, w, tid);
+    copy_work_v<2, PAIR>(s, w, tid);
     break;
   default:
-    copy_items<1, 4, PAIR>(s, w, tid);
+    copy_work_v<1, PAIR>(s, w, tid);
     break;
   }
 }

@@ -409,6 +409,17 @@ def test_colocated_ipc_jacobi_two_ranks(temporal, ranks):
         assert rc == 0, out[-3000:]
 
 
+def test_ipc_probe_failure_falls_back_on_shared_gpu():
+    """Co-located ranks on one GPU whose IPC pre-flight fails (forced) must not pick RCCL (it refuses two ranks on
+    one device): the runtime drops Colocated and Rccl and stages through the host; results stay exact."""
+    outs = run_ranks(2, WORKER, ["jacobi", "48,48,48"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": "2", "STENCIL_IPC_PROBE_FAIL": "1"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out
+
+
 @pytest.mark.parametrize("methods", ["Colocated|Kernel", "Staged|Kernel"])
 def test_race_canary_two_ranks_one_gpu(methods):
     """Race canary over HIP IPC (double-buffered inboxes + credits) and the staged path, with jitter."""
