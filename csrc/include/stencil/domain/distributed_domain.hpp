@@ -49,6 +49,22 @@ inline bool any(MethodFlags a) { return a != MethodFlags::None; }
 std::string to_string(MethodFlags m);
 
 
+// What the planner knows about one (sender, receiver) sub-domain pair when it picks a transport.
+struct PairInfo {
+  bool device = true;     // device backend (false: host backend, only Kernel/PeerCopy-as-host-copy and Staged)
+  bool sameRank = false;  // both sub-domains in this process
+  bool sameDevice = false; // same device ordinal (meaningful within one rank)
+  bool peer = false;      // same rank, P2P access between the two devices (gpu_topo::peer)
+  bool sameHost = false;  // co-located ranks
+  bool canAccess = false; // co-located ranks whose devices can map each other's memory (HIP IPC over xGMI)
+  bool sharedGpu = false; // different ranks, and an endpoint's GPU is driven by two ranks (RCCL refuses that GPU)
+};
+// First enabled method whose predicate holds, in the reference's priority order (src/stencil.cu:163-194):
+// Kernel > PeerCopy > Colocated > Rccl > Staged. A pair touching a GPU shared by two ranks skips Rccl and takes the
+// host-staged path even when Staged is not among `flags` (it is the fallback RCCL itself would need). None = no
+// transport (the planner treats that as fatal).
+MethodFlags select_method(MethodFlags flags, const PairInfo &p);
+
 struct ExchangePlanEntry {
   MethodFlags method;
   Dim3 srcIdx, dstIdx;
@@ -133,7 +149,10 @@ public:
   // ---- exchange ----
   void exchange();       // blocking: returns when every halo of every local domain is valid
   // enqueue on the comm streams; only the staged (host) path blocks the caller. With a single local device a
-  // caller stream may be given: the exchange is then enqueued on it (no cross-stream events).
+  // caller stream may be given: the exchange is then enqueued on it. Caller-stream and comm-stream exchanges are
+  // ordered against each other by events (the last one of the other kind is waited for), and sync_exchange()
+  // also waits for the last caller-stream exchange (except exchanges captured into a hipGraph: the caller orders
+  // those by its stream).
   // skipAxes (prepared by prepare_skip_wrapped): leave out the same-process copies of every direction crossing
   // those axes; their halos are then stale and only kernels that wrap in-kernel may run on the result
   void exchange_async(hipStream_t stream = nullptr, int skipAxes = 0);

@@ -59,6 +59,9 @@ void copy_segs_host(const std::vector<CopySeg> &segs);
 // Device execution plan: the segment list plus a per-block work table built on the host, so every block reads
 // its (segment, first item, count) with scalar loads and never searches. Items are whole rows for narrow rows
 // (x-faces: <= 4 units per row) and single vector units otherwise.
+// Rows of at most this many vector units are copied one row per item (narrow rows, e.g. x faces); wider rows one
+// unit per item. make_copy_plan and the kernel's per-row template dispatch share this bound.
+constexpr uint32_t kNarrowMaxUnits = 4;
 struct CopyWork {
   uint32_t seg;
   uint32_t first;

@@ -210,6 +210,23 @@ PYBIND11_MODULE(_C, m) {
       .def("__or__", [](MethodFlags a, MethodFlags b) { return a | b; })
       .def("__and__", [](MethodFlags a, MethodFlags b) { return a & b; });
   m.def("methods_to_string", [](MethodFlags f) { return to_string(f); });
+  m.def(
+      "select_method",
+      [](MethodFlags flags, bool device, bool same_rank, bool same_device, bool peer, bool same_host, bool can_access,
+         bool shared_gpu) {
+        PairInfo p;
+        p.device = device;
+        p.sameRank = same_rank;
+        p.sameDevice = same_device;
+        p.peer = peer;
+        p.sameHost = same_host;
+        p.canAccess = can_access;
+        p.sharedGpu = shared_gpu;
+        return select_method(flags, p);
+      },
+      py::arg("flags"), py::arg("device") = true, py::arg("same_rank") = false, py::arg("same_device") = false,
+      py::arg("peer") = false, py::arg("same_host") = false, py::arg("can_access") = false,
+      py::arg("shared_gpu") = false);
   py::enum_<PlacementStrategy>(m, "PlacementStrategy")
       .value("NodeAware", PlacementStrategy::NodeAware)
       .value("Trivial", PlacementStrategy::Trivial);

@@ -42,6 +42,22 @@ std::string to_string(MethodFlags m) {
   return s.empty() ? "none" : s;
 }
 
+MethodFlags select_method(MethodFlags flags, const PairInfo &p) {
+  auto on = [&](MethodFlags m) { return (int(flags) & int(m)) != 0; };
+  if (!p.device) {
+    if (p.sameRank && (on(MethodFlags::Kernel) || on(MethodFlags::PeerCopy)))
+      return p.sameDevice && on(MethodFlags::Kernel) ? MethodFlags::Kernel : MethodFlags::PeerCopy;
+    return on(MethodFlags::Staged) ? MethodFlags::Staged : MethodFlags::None;
+  }
+  if (on(MethodFlags::Kernel) && p.sameRank && p.sameDevice) return MethodFlags::Kernel;
+  if (on(MethodFlags::PeerCopy) && p.sameRank && p.peer) return MethodFlags::PeerCopy;
+  if (on(MethodFlags::Colocated) && !p.sameRank && p.sameHost && p.canAccess) return MethodFlags::Colocated;
+  if (on(MethodFlags::Rccl) && !p.sharedGpu) return MethodFlags::Rccl;
+  if (on(MethodFlags::Staged)) return MethodFlags::Staged;
+  if (on(MethodFlags::Rccl) && p.sharedGpu) return MethodFlags::Staged;
+  return MethodFlags::None;
+}
+
 static int method_slot(MethodFlags m) {
   switch (m) {
   case MethodFlags::Staged:
@@ -144,6 +160,12 @@ struct DistributedDomain::Impl {
   bool rccl = false;
   std::vector<std::tuple<int, int, Dim3>> localTranslates; // (srcDom, dstDom, dir) of the Kernel/PeerCopy messages
   int skipAxes = 0;                                         // axes translateSkip leaves out (0 = not prepared)
+  // exchanges enqueued on a caller stream (single device) vs on the comm stream: each kind waits for the last
+  // exchange of the other kind, so the two never race on the IPC inbox slots / flags, and sync_exchange() also
+  // waits for (and then checks the timeout word of) the last caller-stream exchange
+  Event callerDone;
+  bool callerPending = false; // callerDone marks a caller-stream exchange not yet joined by sync_exchange
+  bool commPending = false;   // the comm stream holds an exchange (devs[0].done) a caller stream has not waited for
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -297,20 +319,26 @@ void DistributedDomain::realize() {
   if (dev && any_methods(MethodFlags::Colocated) && pg.size() > 1 && pg.colocated_size() > 1 &&
       std::getenv("STENCIL_SKIP_IPC_PROBE") == nullptr) {
     TraceRange trp("ipc probe");
-    // up to 3 collective attempts: a transient open/map failure on a busy node must not cost the transport
+    // up to 3 collective attempts with a growing pause between them (50, 200 ms): a transient open/map failure on a
+    // busy node must not cost the transport. Every failed attempt logs the call that failed on this rank.
     bool allOk = false;
     for (int attempt = 0; attempt < 3 && !allOk; ++attempt) {
+      if (attempt > 0) std::this_thread::sleep_for(std::chrono::milliseconds(50 * (1 << (2 * (attempt - 1)))));
       int ok = 1;
+      const char *failed = "";
+      int failedPeer = -1;
       char *blk = nullptr;
       HIP_CHECK(hipSetDevice(gpus_[0]));
       if (hipExtMallocWithFlags((void **)&blk, 256, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         ok = 0;
+        failed = "hipExtMallocWithFlags(uncached)";
       }
       hipIpcMemHandle_t mine{};
       if (ok && hipIpcGetMemHandle(&mine, blk) != hipSuccess) {
         (void)hipGetLastError();
         ok = 0;
+        failed = "hipIpcGetMemHandle";
       }
       if (ok) {
         const uint64_t tag = 0x57e9c11000000000ull + uint64_t(myRank);
@@ -326,6 +354,8 @@ void DistributedDomain::realize() {
         if (hipIpcOpenMemHandle((void **)&peer, all[r], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
           (void)hipGetLastError();
           ok = 0;
+          failed = "hipIpcOpenMemHandle";
+          failedPeer = r;
           break;
         }
         uint64_t got = 0;
@@ -333,10 +363,18 @@ void DistributedDomain::realize() {
             got != 0x57e9c11000000000ull + uint64_t(r)) {
           (void)hipGetLastError();
           ok = 0;
+          failed = "readback of the mapped block";
+          failedPeer = r;
         }
         (void)hipIpcCloseMemHandle(peer);
       }
-      if (std::getenv("STENCIL_IPC_PROBE_FAIL")) ok = 0; // rehearses the fallback (tests)
+      if (std::getenv("STENCIL_IPC_PROBE_FAIL")) { // rehearses the fallback (tests)
+        ok = 0;
+        failed = "STENCIL_IPC_PROBE_FAIL";
+      }
+      if (!ok)
+        LOG_INFO("IPC pre-flight attempt " << attempt + 1 << "/3 failed on rank " << myRank << ": " << failed
+                                           << (failedPeer >= 0 ? " (peer rank " + std::to_string(failedPeer) + ")" : ""));
       allOk = pg.allreduce_min_i64(ok) == 1;
       pg.barrier(); // peers are done with our block
       if (blk) (void)hipFree(blk);
@@ -344,21 +382,44 @@ void DistributedDomain::realize() {
     if (!allOk) {
       if (myRank == 0) LOG_WARN("HIP IPC between co-located ranks is unavailable; Colocated transport disabled");
       flags_ = MethodFlags(int(flags_) & ~int(MethodFlags::Colocated));
-      // RCCL refuses two ranks on one device: co-located ranks that share a GPU then fall back to host staging
-      // (device identity by PCI bus id: ranks may see different device numberings)
-      std::vector<uint64_t> devOf(pg.size());
-      char bus[64] = {0};
-      HIP_CHECK(hipDeviceGetPCIBusId(bus, sizeof(bus), gpus_[0]));
-      const uint64_t myDev = uint64_t(std::hash<std::string>()(std::string(bus)));
-      pg.allgather(&myDev, sizeof(myDev), devOf.data());
-      bool shared = false;
-      for (int r = 0; r < pg.size(); ++r) shared |= r != myRank && pg.colocated(r) && devOf[r] == myDev;
-      if (pg.allreduce_min_i64(shared ? 0 : 1) == 0 && any_methods(MethodFlags::Rccl)) {
-        if (myRank == 0) LOG_WARN("co-located ranks share a GPU: Rccl replaced by Staged");
-        flags_ = MethodFlags((int(flags_) & ~int(MethodFlags::Rccl)) | int(MethodFlags::Staged));
-      }
     }
   }
+
+  // ---- physical device identity of every (rank, device ordinal): ranks may number devices differently, and RCCL
+  // refuses a communicator in which two ranks drive one GPU. Pairs with an endpoint on a GPU that another rank of
+  // the same host also drives never use RCCL (select_method); everything else keeps its transport. ----
+  std::map<std::pair<int, int>, bool> sharedDev; // (rank, ordinal) -> GPU driven by another rank too
+  if (dev && pg.size() > 1) {
+    int nmine = int(gpus_.size()), maxN = 0;
+    std::vector<int> counts(pg.size());
+    pg.allgather(&nmine, sizeof(int), counts.data());
+    for (int c : counts) maxN = std::max(maxN, c);
+    struct DevId {
+      int64_t ordinal;
+      uint64_t bus;
+    };
+    std::vector<DevId> mine(size_t(maxN), DevId{-1, 0}), all(size_t(maxN) * pg.size());
+    for (int k = 0; k < nmine; ++k) {
+      char bus[64] = {0};
+      HIP_CHECK(hipDeviceGetPCIBusId(bus, sizeof(bus), gpus_[size_t(k)]));
+      mine[size_t(k)] = DevId{gpus_[size_t(k)], uint64_t(std::hash<std::string>()(std::string(bus)))};
+    }
+    pg.allgather(mine.data(), sizeof(DevId) * size_t(maxN), all.data());
+    for (int r = 0; r < pg.size(); ++r)
+      for (int k = 0; k < counts[r]; ++k) {
+        const DevId &a = all[size_t(r) * maxN + k];
+        bool sh = false;
+        for (int r2 = 0; r2 < pg.size() && !sh; ++r2) {
+          if (r2 == r || pg.hostname(r2) != pg.hostname(r)) continue;
+          for (int k2 = 0; k2 < counts[r2]; ++k2) sh |= all[size_t(r2) * maxN + k2].bus == a.bus;
+        }
+        sharedDev[{r, int(a.ordinal)}] = sh;
+      }
+  }
+  auto shared_dev = [&](int r, int ordinal) {
+    auto it = sharedDev.find({r, ordinal});
+    return it != sharedDev.end() && it->second;
+  };
 
   // ---- plan messages (reference src/stencil.cu:132-239) ----
   t0 = now_s();
@@ -373,22 +434,26 @@ void DistributedDomain::realize() {
     }
     return can != 0;
   };
+  bool warnedShared = false;
   auto choose = [&](int srcRank, int srcDev, int dstRank, int dstDev) -> MethodFlags {
     const bool sameRank = srcRank == dstRank;
-    if (!dev) {
-      if (sameRank && (any_methods(MethodFlags::Kernel) || any_methods(MethodFlags::PeerCopy)))
-        return srcDev == dstDev && any_methods(MethodFlags::Kernel) ? MethodFlags::Kernel : MethodFlags::PeerCopy;
-      if (any_methods(MethodFlags::Staged)) return MethodFlags::Staged;
-      return MethodFlags::None;
+    PairInfo pi;
+    pi.device = dev;
+    pi.sameRank = sameRank;
+    pi.sameDevice = srcDev == dstDev;
+    pi.sameHost = pg.hostname(srcRank) == pg.hostname(dstRank);
+    if (dev) {
+      pi.peer = sameRank && gpu_topo::peer(srcDev, dstDev);
+      pi.canAccess = !sameRank && pi.sameHost && (any_methods(MethodFlags::Colocated)) && can_access(srcDev, dstDev);
+      pi.sharedGpu = !sameRank && (shared_dev(srcRank, srcDev) || shared_dev(dstRank, dstDev));
     }
-    if (any_methods(MethodFlags::Kernel) && sameRank && srcDev == dstDev) return MethodFlags::Kernel;
-    if (any_methods(MethodFlags::PeerCopy) && sameRank && gpu_topo::peer(srcDev, dstDev)) return MethodFlags::PeerCopy;
-    if (any_methods(MethodFlags::Colocated) && !sameRank && pg.hostname(srcRank) == pg.hostname(dstRank) &&
-        can_access(srcDev, dstDev))
-      return MethodFlags::Colocated;
-    if (any_methods(MethodFlags::Rccl)) return MethodFlags::Rccl;
-    if (any_methods(MethodFlags::Staged)) return MethodFlags::Staged;
-    return MethodFlags::None;
+    const MethodFlags m = select_method(flags_, pi);
+    if (m == MethodFlags::Staged && pi.sharedGpu && any_methods(MethodFlags::Rccl) && !warnedShared) {
+      warnedShared = true;
+      LOG_WARN("rank " << srcRank << " dev " << srcDev << " -> rank " << dstRank << " dev " << dstDev
+                       << ": a GPU driven by two ranks cannot use RCCL; host-staged for such pairs");
+    }
+    return m;
   };
 
   // channel maps: (method, localDom, remoteLinear) -> channel index
@@ -525,6 +590,7 @@ void DistributedDomain::realize() {
         c.comm = Stream(d, Priority::HIGH);
         c.done = Event(d);
         c.translated = Event(d);
+        if (!I.callerDone) I.callerDone = Event(d);
       }
       I.devs[I.devIndex[d]].doms.push_back(int(di));
       I.ready.emplace_back(d);
@@ -640,41 +706,46 @@ void DistributedDomain::realize() {
     for (auto &c : I.chans) rcclChans += c.method == MethodFlags::Rccl;
     if (pg.allreduce_sum_u64(uint64_t(rcclChans)) > 0) {
       TraceRange trr("rccl init");
+      // members: every (rank, device) whose GPU no other rank drives (pairs touching a shared GPU are staged)
       const int nLocal = int(I.devs.size());
       std::vector<int> counts(pg.size());
       pg.allgather(&nLocal, sizeof(int), counts.data());
-      int first = 0, total = 0;
-      for (int r = 0; r < pg.size(); ++r) {
-        if (r < myRank) first += counts[r];
-        total += counts[r];
-      }
-      // device slot of every rank's devices, for peer rank lookup
-      std::vector<int> myDevs;
-      for (auto &d : I.devs) myDevs.push_back(d.dev);
       int maxN = 0;
       for (int c : counts) maxN = std::max(maxN, c);
-      std::vector<int> padded(maxN, -1), allDevs(size_t(maxN) * pg.size());
-      std::copy(myDevs.begin(), myDevs.end(), padded.begin());
-      pg.allgather(padded.data(), sizeof(int) * maxN, allDevs.data());
+      std::vector<int> padded(size_t(maxN), -1), allDevs(size_t(maxN) * pg.size());
+      for (int k = 0; k < nLocal; ++k)
+        if (!shared_dev(myRank, I.devs[size_t(k)].dev)) padded[size_t(k)] = I.devs[size_t(k)].dev;
+      pg.allgather(padded.data(), sizeof(int) * size_t(maxN), allDevs.data());
+      // RCCL rank of (rank r, slot k) = number of members before it
+      std::vector<int> ncclRankOf(allDevs.size(), -1);
+      int total = 0, root = -1;
+      for (int r = 0; r < pg.size(); ++r)
+        for (int k = 0; k < maxN; ++k)
+          if (allDevs[size_t(r) * maxN + k] >= 0) {
+            ncclRankOf[size_t(r) * maxN + k] = total++;
+            if (root < 0) root = r;
+          }
+      STENCIL_REQUIRE(root >= 0, "RCCL channels planned but no rank owns an exclusive GPU");
       ncclUniqueId id;
-      if (myRank == 0) NCCL_CHECK(ncclGetUniqueId(&id));
-      pg.bcast(&id, sizeof(id), 0);
+      if (myRank == root) NCCL_CHECK(ncclGetUniqueId(&id));
+      pg.bcast(&id, sizeof(id), root);
       NCCL_CHECK(ncclGroupStart());
       for (int k = 0; k < nLocal; ++k) {
-        HIP_CHECK(hipSetDevice(I.devs[k].dev));
-        NCCL_CHECK(ncclCommInitRank(&I.devs[k].nccl, total, id, first + k));
+        const int nr = ncclRankOf[size_t(myRank) * maxN + k];
+        if (nr < 0) continue;
+        HIP_CHECK(hipSetDevice(I.devs[size_t(k)].dev));
+        NCCL_CHECK(ncclCommInitRank(&I.devs[size_t(k)].nccl, total, id, nr));
       }
       NCCL_CHECK(ncclGroupEnd());
       // translate remote (rank, device) into RCCL ranks
-      std::vector<int> firstOf(pg.size(), 0);
-      for (int r = 1; r < pg.size(); ++r) firstOf[r] = firstOf[r - 1] + counts[r - 1];
       for (auto &c : I.chans) {
         if (c.method != MethodFlags::Rccl) continue;
-        int slot = -1;
-        for (int k = 0; k < counts[c.remoteRank]; ++k)
-          if (allDevs[size_t(c.remoteRank) * maxN + k] == c.remoteDev) slot = k;
-        STENCIL_REQUIRE(slot >= 0, "RCCL peer device not found");
-        c.ncclPeer = firstOf[c.remoteRank] + slot;
+        int peer = -1;
+        for (int k = 0; k < maxN; ++k)
+          if (allDevs[size_t(c.remoteRank) * maxN + k] == c.remoteDev) peer = ncclRankOf[size_t(c.remoteRank) * maxN + k];
+        STENCIL_REQUIRE(peer >= 0, "RCCL peer device not found");
+        STENCIL_REQUIRE(I.devs[size_t(I.devIndex[c.localDev])].nccl != nullptr, "RCCL channel on a shared GPU");
+        c.ncclPeer = peer;
       }
       I.rccl = true;
     }
@@ -868,6 +939,10 @@ void DistributedDomain::sync_exchange() {
     HIP_CHECK(hipSetDevice(d.dev));
     HIP_CHECK(hipStreamSynchronize(d.comm));
   }
+  if (impl_->callerPending) {
+    impl_->callerDone.sync();
+    impl_->callerPending = false;
+  }
   if (*impl_->errHost) {
     const int code = *impl_->errHost;
     LOG_FATAL("halo exchange timed out waiting for a colocated peer (code " << code << ", epoch " << impl_->epoch
@@ -951,6 +1026,22 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   // stream alone, with no cross-stream events
   const bool over = stream != nullptr && I.devs.size() == 1;
   auto S = [&](DevCtx &c) -> hipStream_t { return over ? stream : c.comm.get(); };
+  // hand-offs between caller-stream and comm-stream exchanges (events are not used while `stream` is being
+  // captured into a hipGraph: the graph is ordered by that stream alone)
+  bool capturing = false;
+  if (over) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+    capturing = cs != hipStreamCaptureStatusNone;
+  }
+  if (over && !capturing) {
+    HIP_CHECK(hipSetDevice(I.devs[0].dev));
+    if (I.commPending) I.devs[0].done.wait_on(stream);
+    I.commPending = false;
+  } else if (!over && I.callerPending) {
+    HIP_CHECK(hipSetDevice(I.devs[0].dev));
+    I.callerDone.wait_on(I.devs[0].comm);
+  }
 
   // (0) dependencies: the comm streams start after every local domain's producer work
   if (!over) {
@@ -1091,6 +1182,12 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     HIP_CHECK(hipSetDevice(ctx.dev));
     for (int src : ctx.peerWriters) I.devs[I.devIndex[src]].translated.wait_on(S(ctx));
     if (!over) ctx.done.record(S(ctx));
+  }
+  if (over && !capturing) {
+    I.callerDone.record(stream);
+    I.callerPending = true;
+  } else if (!over) {
+    I.commPending = true;
   }
 }
 

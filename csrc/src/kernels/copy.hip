@@ -146,10 +146,14 @@ template <uint32_t V, bool PAIR> __device__ __forceinline__ void copy_work_v(con
   case 3:
     copy_items<V, 3, PAIR>(s, w, tid);
     break;
-  default:
+  case 4:
     copy_items<V, 4, PAIR>(s, w, tid);
     break;
+  default:
+    // make_copy_plan marks a segment as rows only when row_units <= kNarrowMaxUnits: anything else is a planner bug
+    __builtin_trap();
   }
+  static_assert(kNarrowMaxUnits == 4, "copy_work_v dispatches row widths 1..4");
 }
 
 template <bool PAIR> __device__ __forceinline__ void copy_work_t(const CopySeg &s, const CopyWork &w, uint32_t tid) {
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(1024) void copy_plan_kernel_narrow(const CopySeg *_
 static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
   std::vector<CopySeg> out;
   std::vector<bool> used(in.size(), false);
-  auto narrow = [](const CopySeg &s) { return s.units && s.row_units <= 4 && !s.src2; };
+  auto narrow = [](const CopySeg &s) { return s.units && s.row_units <= kNarrowMaxUnits && !s.src2; };
   for (size_t i = 0; i < in.size(); ++i) {
     if (used[i]) continue;
     CopySeg a = in[i];
@@ -237,7 +241,7 @@ CopyPlan make_copy_plan(const std::vector<CopySeg> &segsIn, int device) {
     const CopySeg &s = segs[si];
     if (!s.units) continue;
     p.bytes += s.units * s.vec * (s.src2 ? 2 : 1);
-    const bool rows = s.row_units <= 4;
+    const bool rows = s.row_units <= kNarrowMaxUnits;
     const uint64_t items = rows ? s.units / s.row_units : s.units;
     STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
     for (uint64_t f = 0; f < items; f += perBlockUnits)
@@ -275,6 +279,10 @@ void copy_plan_device(const CopyPlan &p, hipStream_t stream, int maxBlocks) {
 
 void copy_segs_device_sync(std::vector<CopySeg> segs, int device) {
   finalize_segs(segs);
+  // the copy runs on the null stream, which does not order against the non-blocking compute/comm streams: wait for
+  // every kernel that may still write the source (e.g. a dump right after StencilModel::run() without synchronize())
+  HIP_CHECK(hipSetDevice(device));
+  HIP_CHECK(hipDeviceSynchronize());
   CopyPlan p = make_copy_plan(segs, device);
   copy_plan_device(p, nullptr);
   HIP_CHECK(hipDeviceSynchronize());

@@ -83,6 +83,22 @@ TEST(qap_reference_values, false) {
   CHECK(h[0] == 3 && h[1] == 1 && h[2] == 2 && h[3] == 0);
 }
 
+TEST(select_method_ladder, false) {
+  PairInfo p;
+  p.sameRank = true;
+  p.sameDevice = true;
+  CHECK(select_method(MethodFlags::All, p) == MethodFlags::Kernel);
+  p = PairInfo();
+  p.sameHost = true;
+  CHECK(select_method(MethodFlags::All, p) == MethodFlags::Rccl);
+  p.sharedGpu = true; // RCCL refuses a GPU two ranks drive: only such pairs are staged
+  CHECK(select_method(MethodFlags::All, p) == MethodFlags::Staged);
+  CHECK(select_method(MethodFlags::Rccl | MethodFlags::Kernel, p) == MethodFlags::Staged);
+  p.canAccess = true;
+  CHECK(select_method(MethodFlags::All, p) == MethodFlags::Colocated);
+  CHECK(select_method(MethodFlags::Kernel, PairInfo()) == MethodFlags::None);
+}
+
 TEST(statistics_trimean, false) {
   Statistics s;
   for (int i = 0; i < 8; ++i) s.insert(i);

@@ -99,7 +99,10 @@ def scenario_jacobi(backend, methods, size):
         bad += int((got != u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x]).sum())
     if os.environ.get("MP_EXPECT_OVERLAP") is not None:
         bad += int(m.overlapping() != (os.environ["MP_EXPECT_OVERLAP"] == "1"))
-    print(f"rank {g.rank()} jacobi bad {bad} overlap {m.overlapping()} dim {m.domain.placement_dim()}")
+    xb = {k: m.domain.exchange_bytes_for_method(getattr(st.MethodFlags, k))
+          for k in ("Staged", "Rccl", "Colocated", "PeerCopy", "Kernel")}
+    print(f"rank {g.rank()} jacobi bad {bad} overlap {m.overlapping()} dim {m.domain.placement_dim()} "
+          + " ".join(f"bytes_{k}={v}" for k, v in xb.items()))
     return bad
 
 

@@ -173,3 +173,26 @@ def test_self_wrap_axes(st, gpus, axes):
     if want != 7:
         with pytest.raises(Exception):
             dd.prepare_skip_wrapped(7 & ~want)
+
+
+def test_select_method_priority_and_shared_gpu(st):
+    """Transport ladder (reference src/stencil.cu:163-194) as a pure function, including the pair-scoped RCCL
+    fallback: only pairs with an endpoint on a GPU that two ranks drive leave RCCL (for the staged path)."""
+    M = st.MethodFlags
+    sel = st._C.select_method
+    assert sel(M.All, same_rank=True, same_device=True) == M.Kernel
+    assert sel(M.All, same_rank=True, peer=True) == M.PeerCopy
+    assert sel(M.All, same_host=True, can_access=True) == M.Colocated
+    assert sel(M.All, same_host=True, can_access=False) == M.Rccl
+    assert sel(M.All) == M.Rccl  # other host
+    # shared GPU: Colocated still wins when IPC works; otherwise staged, never RCCL
+    assert sel(M.All, same_host=True, can_access=True, shared_gpu=True) == M.Colocated
+    assert sel(M.All, same_host=True, shared_gpu=True) == M.Staged
+    assert sel(M.Rccl | M.Kernel, same_host=True, shared_gpu=True) == M.Staged
+    # a pair between two exclusive GPUs of the same job keeps RCCL
+    assert sel(M.Rccl | M.Kernel, same_host=True, shared_gpu=False) == M.Rccl
+    assert sel(M.Kernel) == M.None_
+    # host backend: translate within a process, staged across processes
+    assert sel(M.All, device=False, same_rank=True, same_device=True) == M.Kernel
+    assert sel(M.All, device=False) == M.Staged
+    assert sel(M.Kernel, device=False) == M.None_

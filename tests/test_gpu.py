@@ -418,6 +418,8 @@ def test_ipc_probe_failure_falls_back_on_shared_gpu():
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out
+        # only the pairs on the shared GPU are staged: here that is every cross-rank pair, none left on RCCL/IPC
+        assert "bytes_Rccl=0 " in out and "bytes_Colocated=0 " in out and "bytes_Staged=0 " not in out, out[-2000:]
 
 
 @pytest.mark.parametrize("methods", ["Colocated|Kernel", "Staged|Kernel"])
@@ -432,13 +434,14 @@ def test_race_canary_two_ranks_one_gpu(methods):
 
 @pytest.mark.parametrize("methods", ["Rccl|Kernel", "Staged|Kernel"])
 def test_jacobi_temporal2_two_ranks_other_transports(methods):
-    """fused pairs over the staged transport and (ranks sharing one GPU cannot use RCCL) its fallback"""
-    if methods.startswith("Rccl"):
-        pytest.skip("RCCL cannot put two ranks on one device; covered by the in-process RCCL tests")
+    """fused pairs over the staged transport, and over Rccl|Kernel between ranks that share one GPU: RCCL refuses a
+    GPU driven by two ranks, so exactly those pairs (here: all cross-rank pairs) are host-staged"""
     outs = run_ranks(2, WORKER, ["jacobi", "36,20,24"],
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20", "MP_TEMPORAL": "2"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out
+        assert "bytes_Rccl=0 " in out and "bytes_Staged=0 " not in out, out[-2000:]
 
 
 def test_staged_two_ranks_one_gpu():
