@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--nw", type=int, default=8, help="waves per block of the stencil kernel")
     ap.add_argument("--x2nw", type=int, default=12, help="waves per block of the fused two-step kernel (8/12/16)")
     ap.add_argument("--x2pf", type=int, default=3, help="planes of z lookahead of the fused two-step kernel (1/2/3)")
+    ap.add_argument("--x2row", type=int, default=1,
+                    help="fused pairs: one wave per whole 512-cell row when x wraps in-kernel (fp32); 0 = columns")
     ap.add_argument("--zchunk", type=int, default=0, help="z planes per block (0 = auto)")
     ap.add_argument("--x2sched", type=int, default=1,
                     help="fused-pair work split: 1 = balanced segments over the resident blocks, 0 = fixed z-chunks")
@@ -143,6 +145,7 @@ def main():
     tune.variant = args.variant
     tune.x2nw = args.x2nw
     tune.x2pf = args.x2pf
+    tune.x2row = args.x2row
     tune.zchunk = args.zchunk
     tune.x2sched = args.x2sched
     tune.x2xfast = args.x2xfast
@@ -210,7 +213,7 @@ def main():
                                                                    model.domain.placement_dim().y,
                                                                    model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
                        "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
-                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
+                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
                        "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none"},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),

@@ -564,6 +564,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("nw", &StencilTune::nw)
       .def_readwrite("x2pf", &StencilTune::x2pf)
       .def_readwrite("x2nw", &StencilTune::x2nw)
+      .def_readwrite("x2row", &StencilTune::x2row)
       .def_readwrite("x2sched", &StencilTune::x2sched)
       .def_readwrite("x2reserve", &StencilTune::x2reserve)
       .def_readwrite("wrap", &StencilTune::wrap)

@@ -361,6 +361,212 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
   } // segments
 }
 
+// Whole-row variant of the fused pair (fp32, x periodic and wrapped in-kernel, 512 interior cells per row, i.e. the
+// one-GPU 512^3 sweep). Each lane holds two 16-B chunks of its row, x = lox + 4*lane and x = lox + 256 + 4*lane, so
+// one wave covers the whole row and every x-neighbour - the periodic ones included - is a DPP lane rotate of the
+// wave's own registers:
+//   left of chunk h  = lane 0 ? (chunk h-1 of lane 63) : (chunk h of lane-1)   -> wave_ror:1 of the chunks' last cells
+//   right of chunk h = lane 63 ? (chunk h+1 of lane 0) : (chunk h of lane+1)   -> wave_rol:1 of their first cells
+// Against stencil7x2_kernel (one 16-B chunk per lane, two 256-cell columns per row) this drops, per row and plane:
+// the two edge-scalar loads (and their far-row-end sectors at the periodic faces: 6 % of the fetched bytes), the
+// edge-scalar LDS exchange, the u1 edge-pair computation, and half of the per-step fixed cost (plane addressing,
+// sphere tests, loop control, one barrier per 12 rows of 512 cells instead of 256). Each chunk load / store is one
+// fully coalesced 1 KB wave instruction. Block, z-march, LDS y-neighbours, summation order, exact /6 and spheres
+// are those of stencil7x2_kernel: S(S(src)) is bitwise equal to two single steps.
+__device__ __forceinline__ float rot_prev(float v) { // lane i <- lane i-1, lane 0 <- lane 63 (wave_ror:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x13C, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float rot_next(float v) { // lane i <- lane i+1, lane 63 <- lane 0 (wave_rol:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xf, 0xf, false));
+}
+
+template <int NW, int PF, int KIND>
+__global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void stencil7x2_row_kernel(
+    StencilArgs<float> a) {
+  using T = float;
+  using NV = nf4;
+  constexpr int V = 4, H = 2;   // chunks per lane
+  constexpr int HS = 64 * V;    // cells between a lane's chunks
+  constexpr int YO = NW - 4;
+  constexpr int NC = 3 + PF;
+  static_assert(NW == 12, "3 waves per SIMD: the 168-VGPR budget");
+  __shared__ NV cs[2][NW][H][64]; // src rows (plane z+2dz at publish)
+  __shared__ NV us[2][NW][H][64]; // u1 rows (plane z+dz at publish)
+
+  const uint32_t nb = gridDim.x;
+  const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
+  const int lane = threadIdx.x;
+  const int w = int(threadIdx.y);
+  const uint32_t nzt = uint32_t(a.hiz - a.loz);
+  uint32_t s, e;
+  if (a.seg) {
+    const uint64_t W = uint64_t(uint32_t(a.gy)) * nzt;
+    s = uint32_t(uint64_t(lb) * W / nb);
+    e = uint32_t(uint64_t(lb + 1) * W / nb);
+  } else {
+    const uint32_t col = lb / uint32_t(a.gz);
+    s = col * nzt + (lb % uint32_t(a.gz)) * uint32_t(a.zc);
+    e = min(s + uint32_t(a.zc), (col + 1) * nzt);
+  }
+  bool odd = a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0;
+  while (s < e) { // block-uniform
+  const uint32_t by = s / nzt; // one column per row range
+  const int zo = int(s - by * nzt);
+  const int nzs = int(min(nzt - uint32_t(zo), e - s));
+  s += uint32_t(nzs);
+  const int zs = a.loz + zo;
+  const int ze = zs + nzs;
+  const bool down = odd != (a.flip != 0);
+  odd = !odd;
+  const int xb = a.lox + lane * V; // chunk h at xb + h * HS
+  const int yblk = a.loy + YO * int(by);
+  const int y = yblk - 2 + w;
+  if (yblk >= a.hiy) continue;
+  const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy;
+  const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
+  const bool lane0 = lane == 0, lane63 = lane == 63;
+
+  const int yw = (a.wrapm & 2) ? (y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y)) : y;
+  const int yc = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
+  const uint32_t rowoff = uint32_t((yc * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+  const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+  const int zwn = (a.wrapm & 4) ? a.wn[2] : 0, zwlo = a.wlo[2], zwhi = a.wlo[2] + zwn;
+  auto zcl = [&](int zz) {
+    zz += zz < zwlo ? zwn : 0;
+    zz -= zz >= zwhi ? zwn : 0;
+    return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
+  };
+  auto planep = [&](int zz) -> const char * { return reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy); };
+  struct RowSph {
+    int dh, dc;
+    bool hit;
+  };
+  auto row_sph = [&](int P) -> RowSph {
+    RowSph r{0, 0, false};
+    if (KIND == 0 && a.r1sq > 0) {
+      r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
+      r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
+      r.hit = r.dh < a.r1sq || r.dc < a.r1sq;
+    }
+    return r;
+  };
+  auto fix = [&](const RowSph &rs, int x, T v) -> T {
+    const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
+    const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+    return hot ? T(1) : (cold ? T(0) : v);
+  };
+  // S of the wave's row (both chunks), x-neighbours by lane rotates
+  auto apply_row = [&](const NV (&cm)[H], const NV (&up)[H], const NV (&dn)[H], const NV (&zp)[H], const NV (&zm)[H],
+                       const RowSph &rs, NV (&o)[H]) {
+    T r3[H], l0[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      r3[h] = rot_prev(cm[h][V - 1]);
+      l0[h] = rot_next(cm[h][0]);
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const T left = lane0 ? r3[(h + H - 1) % H] : r3[h];
+      const T right = lane63 ? l0[(h + 1) % H] : l0[h];
+      NV vpx, vmx;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        vpx[k] = k < V - 1 ? cm[h][k + 1] : right;
+        vmx[k] = k > 0 ? cm[h][k - 1] : left;
+      }
+      o[h] = div6v<T, NV, V>(sum6v<T, KIND>(vpx, vmx, dn[h], up[h], zp[h], zm[h]));
+    }
+    if (KIND == 0 && rs.hit) {
+#pragma unroll
+      for (int h = 0; h < H; ++h)
+#pragma unroll
+        for (int k = 0; k < V; ++k) o[h][k] = fix(rs, xb + h * HS + k, o[h][k]);
+    }
+  };
+
+  auto march = [&](auto downTag) {
+    constexpr bool DOWN = decltype(downTag)::value;
+    constexpr int dz = DOWN ? -1 : 1;
+    const int z0 = DOWN ? ze - 1 : zs;
+    NV C[NC][H];
+    NV Ub[H], Uc[H], Ua[H];
+    auto load_row = [&](int zz, int k) {
+      const char *b = planep(zz) + rowoff;
+#pragma unroll
+      for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + h * HS * int(sizeof(T)));
+    };
+    {
+      const int zw = z0 - 2 * dz;
+#pragma unroll
+      for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, k);
+#pragma unroll
+      for (int h = 0; h < H; ++h) cs[0][w][h][lane] = C[1][h];
+      __syncthreads();
+    }
+    int buf = 0;
+    int t = -2;
+    auto step = [&](auto phase) -> bool {
+      constexpr int k = decltype(phase)::value;
+      constexpr int s0 = k % NC, s1 = (k + 1) % NC, s2 = (k + 2) % NC, sn = (k + NC - 1) % NC;
+      if (t >= nzs) return false;
+      const int z = z0 + t * dz;
+      const int P = z + dz;
+      load_row(z + (NC - 1) * dz, sn);
+      {
+        NV cA[H], cB[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          cA[h] = cs[buf][wA][h][lane];
+          cB[h] = cs[buf][wB][h][lane];
+        }
+        apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], row_sph(P), Ua);
+      }
+      if (t >= 0) {
+        NV uA[H], uB[H], o[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          uA[h] = us[buf][wA][h][lane];
+          uB[h] = us[buf][wB][h][lane];
+        }
+        apply_row(Uc, uA, uB, DOWN ? Ub : Ua, DOWN ? Ua : Ub, row_sph(z), o);
+        if (outRow) {
+          char *dp = reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff;
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            NV *q = reinterpret_cast<NV *>(dp + h * HS * int(sizeof(T)));
+            if (a.nt)
+              __builtin_nontemporal_store(o[h], q);
+            else
+              *q = o[h];
+          }
+        }
+      }
+      const int nbuf = buf ^ 1;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        cs[nbuf][w][h][lane] = C[s2][h];
+        us[nbuf][w][h][lane] = Ua[h];
+      }
+      __syncthreads();
+      buf = nbuf;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        Ub[h] = Uc[h];
+        Uc[h] = Ua[h];
+      }
+      ++t;
+      return true;
+    };
+    while (run_phases(step, std::make_integer_sequence<int, NC>{})) {
+    }
+  };
+  if (down)
+    march(std::true_type{});
+  else
+    march(std::false_type{});
+  } // segments
+}
+
 // S o S on a few small boxes (the exterior slabs of an overlapped step: interior sweep during the exchange, these
 // after it). One thread per output cell: u2 = S of the six u1 neighbours, each u1 = S of its six src neighbours,
 // in the single step's summation order with the exact /6 and the spheres, i.e. the same bits as the sweep kernel
@@ -636,6 +842,49 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   HIP_CHECK(hipGetLastError());
 }
 
+// whole-row kernel: fp32, x wrapped in-kernel, 512 interior cells per row starting on a 16-B chunk
+template <int KIND, int PF>
+static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
+                          const StencilTune &tune) {
+  constexpr int NW = 12, YO = NW - 4;
+  StencilArgs<float> a = make_args<float>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
+  const int rxm = int(dom.radius().x(-1));
+  if (!(tune.wrap & 1) || a.hix - a.lox != 512 || (a.lox - rxm) % 4 != 0) return false;
+  a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
+  a.nt = tune.nontemporal ? 1 : 0;
+  a.wrapm = tune.wrap;
+  a.x0 = a.lox;
+  a.nchunks = 128;
+  a.remap = tune.xcdRemap ? 1 : 0;
+  const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  a.gx = 1;
+  a.gy = (ny + YO - 1) / YO;
+  const void *kern = (const void *)stencil7x2_row_kernel<NW, PF, KIND>;
+  const int64_t cols = a.gy;
+  const int64_t resident = x2_resident_blocks(kern, 64 * NW);
+  uint32_t blocks;
+  if (tune.x2sched != 0 && tune.zchunk <= 0) {
+    a.seg = 1;
+    a.zc = 1;
+    a.gz = 1;
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dom.gpu()) != hipSuccess) cus = 256;
+    const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
+    const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
+    blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 16)));
+  } else {
+    int zc = tune.zchunk;
+    if (zc <= 0) zc = pick_zchunk(cols, nz, resident, 4, 16);
+    a.zc = zc;
+    a.gz = (nz + zc - 1) / zc;
+    blocks = uint32_t(cols * a.gz);
+  }
+  dom.set_device();
+  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  HIP_CHECK(hipGetLastError());
+  return true;
+}
+
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune) {
   if (region.empty()) return;
@@ -647,6 +896,19 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   check_wrap(dom, qi, region, tune.wrap);
   const bool f32 = dom.elem_size(qi) == 4;
   const bool jac = kind == StencilKind::Jacobi;
+  if (f32 && tune.x2row) { // whole rows of 512 cells in one wave (x wrapped in-kernel)
+    const int pf = tune.x2pf <= 1 ? 1 : (tune.x2pf == 2 ? 2 : 3);
+    bool done;
+    if (jac)
+      done = pf == 1 ? apply_x2row_t<0, 1>(dom, qi, region, sph, stream, tune)
+                     : (pf == 2 ? apply_x2row_t<0, 2>(dom, qi, region, sph, stream, tune)
+                                : apply_x2row_t<0, 3>(dom, qi, region, sph, stream, tune));
+    else
+      done = pf == 1 ? apply_x2row_t<1, 1>(dom, qi, region, sph, stream, tune)
+                     : (pf == 2 ? apply_x2row_t<1, 2>(dom, qi, region, sph, stream, tune)
+                                : apply_x2row_t<1, 3>(dom, qi, region, sph, stream, tune));
+    if (done) return;
+  }
   // shapes (rows per lane, waves per block, min waves/SIMD): 1x8 keeps everything in registers at 6 waves/SIMD;
   // 2x4 at 3 waves/SIMD; 2x8 at 4 (spills)
   // shape = waves per block (one src row each; NW-4 output rows) x planes of z lookahead

@@ -210,6 +210,36 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
+@pytest.mark.parametrize("kind,size,gpus", [("jacobi", (512, 120, 116), [0]), ("jacobi", (512, 300, 112), [0, 0]),
+                                            ("astaroth", (512, 36, 28), [0]), ("astaroth", (512, 520, 40), [0, 0, 0, 0])])
+@pytest.mark.parametrize("pf", [1, 2, 3])
+def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf):
+    """Fused pairs on 512-cell periodic rows take the whole-row kernel (one wave per row, x-neighbours by lane
+    rotates, StencilTune.x2row): bitwise equal to single steps, with the hot/cold spheres (Jacobi) inside the grid,
+    and to the column kernel (x2row = 0)."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    ms = []
+    for row in (1, 0):
+        t = st.StencilTune()
+        t.x2pf = pf
+        t.x2row = row
+        ms.append(cls(size, gpus=gpus, temporal=2, tune=t, axis_cost=(4, 2, 3), **kw))  # bench.py's cut: x stays whole
+    for m in ms:
+        m.init()
+        assert m.temporal_blocking() and m.wrap_axes() & 1
+    u = _gather(ms[0])
+    for n in (5, 16):
+        for m in ms:
+            m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        for m in ms:
+            m.synchronize()
+            assert torch.equal(_gather(m), u), f"x2row={1 - ms.index(m)} after run({n})"
+
+
 @pytest.mark.parametrize("temporal", [1, 2])
 def test_prepare_graph_blocks(st, temporal):
     """prepare() records run()'s hipGraph blocks for both buffer parities without running anything: the field is
@@ -281,13 +311,13 @@ def test_jacobi_mfma_variant_special_values(st):
     assert torch.equal(got.view(torch.int32), u.view(torch.int32)), int((got.view(torch.int32) != u.view(torch.int32)).sum())
 
 
-@pytest.mark.parametrize("temporal", [1, 2])
+@pytest.mark.parametrize("temporal,size", [(1, (72, 20, 18)), (2, (72, 20, 18)), (2, (512, 20, 18))])
 @pytest.mark.parametrize("kind", ["jacobi", "astaroth"])
-def test_stencil_special_values_bitwise(st, temporal, kind):
+def test_stencil_special_values_bitwise(st, temporal, size, kind):
     """Fields with signed zeros, values below 2^-100 (the exact-/6 slow path), subnormals and mixed signs: the packed
-    fp32 sums and the FMA division must stay bitwise equal to the torch oracle (0-started sums, IEEE division)."""
+    fp32 sums and the FMA division must stay bitwise equal to the torch oracle (0-started sums, IEEE division).
+    512-cell rows: the whole-row fused kernel (Jacobi there falls back to single steps: its spheres reach the faces)."""
     from stencil2_amd.ops import astaroth_step_reference
-    size = (72, 20, 18)
     if kind == "jacobi":
         m = st.Jacobi3D(size, gpus=[0, 0], temporal=temporal)
         ref = jacobi_step_reference
