@@ -1,7 +1,6 @@
 // Lab for the fused-pair sweep (one 512^3 fp32 Jacobi pair per launch, the bench.py layout, in-kernel x/y/z wrap).
-// Kernels come from gen.py: lab_base = stencil7x2_kernel with ablation bits (ABL: 1 no output stores, 2 no
-// lookahead loads), lab_var = the same with gen.py's experimental transform. Prints us per launch and checks that
-// lab_var writes the same bits as lab_base.
+// Kernels come from gen.py: lab_col = stencil7x2_kernel, lab_row = stencil7x2_row_kernel, each with ablation bits
+// (ABL: 1 no output stores, 2 no lookahead loads). Prints us per launch and checks that both write the same bits.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
@@ -19,8 +18,8 @@ namespace stencil {
 using namespace stencil;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 template <int ABL, int VAR> void launch(StencilArgs<float> a, int nb) {
-  if (VAR) hipLaunchKernelGGL((lab_var<float, 12, 3, 0, 2, ABL>), dim3(nb), dim3(64, 12), 0, 0, a);
-  else hipLaunchKernelGGL((lab_base<float, 12, 3, 0, 2, ABL>), dim3(nb), dim3(64, 12), 0, 0, a);
+  if (VAR) { a.gx = 1; hipLaunchKernelGGL((lab_row<12, 3, 0, ABL>), dim3(nb), dim3(64, 12), 0, 0, a); }
+  else hipLaunchKernelGGL((lab_col<float, 12, 3, 0, 2, ABL>), dim3(nb), dim3(64, 12), 0, 0, a);
 }
 template <int ABL, int VAR> float run(StencilArgs<float> a, float *b0, float *b1, int nb, int iters) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -49,21 +48,24 @@ int main() {
   a.gx = (a.nchunks + 63) / 64; a.gy = (n + 7) / 8; a.gz = 1; a.zc = 1; a.seg = 1; a.remap = 1; a.nt = 1;
   a.hx = 2 + n / 3; a.hy = 2 + n / 2; a.hz = 2 + n / 2; a.cx = 2 + 2 * n / 3; a.cy = a.hy; a.cz = a.hz; a.r1sq = (n / 10 + 1) * (n / 10 + 1);
   a.wrapm = 7; for (int d = 0; d < 3; ++d) { a.wlo[d] = 2; a.wn[d] = n; }
-  int per = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)lab_base<float, 12, 3, 0, 2, 0>, 768, 0));
+  int per = 0; CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)lab_col<float, 12, 3, 0, 2, 0>, 768, 0));
   const int nb = 256 * per;
   // bitwise check: one launch of each from the same source
   { StencilArgs<float> c = a; c.src = b0; c.dst = b1; launch<0, 0>(c, nb); c.dst = b2; launch<0, 1>(c, nb); CK(hipDeviceSynchronize());
     std::vector<float> o1(cnt), o2(cnt); CK(hipMemcpy(o1.data(), m1, cnt * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(o2.data(), m2, cnt * 4, hipMemcpyDeviceToHost));
-    printf("var bitwise equal to base: %s\n", memcmp(o1.data(), o2.data(), cnt * 4) == 0 ? "yes" : "NO"); }
+    printf("row kernel bitwise equal to column kernel: %s\n", memcmp(o1.data(), o2.data(), cnt * 4) == 0 ? "yes" : "NO"); }
   printf("blocks %d\n", nb);
   const int it = 20;
-  for (int rep = 0; rep < 3; ++rep) {
-    printf("base full      %7.1f us\n", run<0, 0>(a, b0, b1, nb, it));
-    printf("var  full      %7.1f us\n", run<0, 1>(a, b0, b1, nb, it));
+  for (int rep = 0; rep < 2; ++rep) {
+    printf("col full       %7.1f us\n", run<0, 0>(a, b0, b1, nb, it));
+    printf("row full       %7.1f us\n", run<0, 1>(a, b0, b1, nb, it));
   }
-  printf("base no stores %7.1f us\n", run<1, 0>(a, b0, b1, nb, it));
-  printf("base no loads  %7.1f us\n", run<2, 0>(a, b0, b1, nb, it));
-  printf("var  no stores %7.1f us\n", run<1, 1>(a, b0, b1, nb, it));
-  printf("var  no loads  %7.1f us\n", run<2, 1>(a, b0, b1, nb, it));
+  printf("row no stores  %7.1f us\n", run<1, 1>(a, b0, b1, nb, it));
+  printf("row no loads   %7.1f us\n", run<2, 1>(a, b0, b1, nb, it));
+  printf("row no ld/st   %7.1f us\n", run<3, 1>(a, b0, b1, nb, it));
+  a.r1sq = 0;
+  printf("row no sph     %7.1f us\n", run<0, 1>(a, b0, b1, nb, it));
+  printf("col no sph     %7.1f us\n", run<0, 0>(a, b0, b1, nb, it));
+  a.r1sq = (n / 10 + 1) * (n / 10 + 1);
   return 0;
 }
