@@ -13,12 +13,12 @@ using namespace stencil;
 int main(int argc, char **argv) {
   int64_t x = 512, y = 512, z = 512;
   int iters = 5, nq = 8;
-  bool noOverlap = false, weak = false;
+  bool noOverlap = false, weak = false, fp64 = false;
   app::MethodArgs ma;
   ArgParser p("Astaroth proxy (reference bin/astaroth_sim.cu)");
   p.option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z").option(&iters, "-n,--iters", "iterations")
       .option(&nq, "--q", "quantities").flag(&noOverlap, "--no-overlap", "no overlap")
-      .flag(&weak, "--weak", "treat x,y,z as per-GPU sizes");
+      .flag(&weak, "--weak", "treat x,y,z as per-GPU sizes").flag(&fp64, "--fp64", "fp64 quantities");
   ma.add(p);
   if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
   auto pg = comm::default_group();
@@ -33,6 +33,7 @@ int main(int argc, char **argv) {
   cfg.radius = 3;
   cfg.allDirections = true;
   cfg.quantities = nq;
+  cfg.fp64 = fp64;
   cfg.methods = ma.flags();
   cfg.placement = ma.placement();
   cfg.overlap = !noOverlap;

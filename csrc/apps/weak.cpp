@@ -11,11 +11,12 @@ using namespace stencil;
 int main(int argc, char **argv) {
   int64_t x = 512, y = 512, z = 512;
   int iters = 30, nq = 4, radius = 3;
-  bool strong = false;
+  bool strong = false, fp64 = false;
   app::MethodArgs ma;
   ArgParser p("weak/strong scaling exchange driver (reference bin/weak.cu, bin/strong.cu)");
   p.positional(&x, "x", "x").positional(&y, "y", "y").positional(&z, "z", "z").positional(&iters, "iters", "iterations")
-      .option(&nq, "--q", "quantities").option(&radius, "--radius", "radius").flag(&strong, "--strong", "strong scaling");
+      .option(&nq, "--q", "quantities").option(&radius, "--radius", "radius").flag(&strong, "--strong", "strong scaling")
+      .flag(&fp64, "--fp64", "fp64 quantities (BASELINE config: 1024^3/GPU fp64)");
   ma.add(p);
   if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
   auto pg = comm::default_group();
@@ -29,7 +30,12 @@ int main(int argc, char **argv) {
   dd.set_radius(radius);
   dd.set_methods(ma.flags());
   dd.set_placement(ma.placement());
-  for (int i = 0; i < nq; ++i) dd.add_data<float>("d" + std::to_string(i));
+  for (int i = 0; i < nq; ++i) {
+    if (fp64)
+      dd.add_data<double>("d" + std::to_string(i));
+    else
+      dd.add_data<float>("d" + std::to_string(i));
+  }
   dd.realize();
   for (int i = 0; i < iters; ++i) {
     dd.exchange();
