@@ -20,7 +20,7 @@ c = src.index("template <int NW, int PF, int KIND>\n__global__")
 d = src.index("// S o S on a few small boxes")
 rot = src[b:c]
 row = src[c:d].replace("template <int NW, int PF, int KIND>", "template <int NW, int PF, int KIND, int ABL>")
-row = ablate(row.replace("stencil7x2_row_kernel(StencilArgs", "lab_row(StencilArgs"))
+row = ablate(row.replace("stencil7x2_row_kernel(", "lab_row("))
 assert "ABL & 2" in col and "ABL & 1" in col and "ABL & 2" in row and "ABL & 1" in row
 open(os.path.join(HERE, "x2lab_kernel.inc"), "w").write(col + "\n" + rot + "\n" + row)
 h0 = src.index("// whole-wave lane shifts on the DPP path")
