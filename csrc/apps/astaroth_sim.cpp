@@ -12,12 +12,14 @@ using namespace stencil;
 
 int main(int argc, char **argv) {
   int64_t x = 512, y = 512, z = 512;
-  int iters = 5, nq = 8;
+  int iters = 5, nq = 8, temporal = 1;
   bool noOverlap = false, weak = false, fp64 = false;
   app::MethodArgs ma;
   ArgParser p("Astaroth proxy (reference bin/astaroth_sim.cu)");
   p.option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z").option(&iters, "-n,--iters", "iterations")
-      .option(&nq, "--q", "quantities").flag(&noOverlap, "--no-overlap", "no overlap")
+      .option(&nq, "--q", "quantities")
+      .option(&temporal, "--temporal", "steps fused per sweep (1 or 2)")
+      .flag(&noOverlap, "--no-overlap", "no overlap")
       .flag(&weak, "--weak", "treat x,y,z as per-GPU sizes").flag(&fp64, "--fp64", "fp64 quantities");
   ma.add(p);
   if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
@@ -34,20 +36,22 @@ int main(int argc, char **argv) {
   cfg.allDirections = true;
   cfg.quantities = nq;
   cfg.fp64 = fp64;
+  cfg.temporal = temporal;
   cfg.methods = ma.flags();
   cfg.placement = ma.placement();
   cfg.overlap = !noOverlap;
   StencilModel m(cfg, pg);
   m.init();
-  m.step();
+  const int per = m.temporal_blocking() ? 2 : 1; // timed unit = one sweep, reported per step
+  m.run(per);
   m.synchronize();
   Statistics st;
   for (int i = 0; i < iters; ++i) {
     pg->barrier();
     const double t0 = app::now();
-    m.step();
+    m.run(per);
     m.synchronize();
-    st.insert(pg->allreduce_max(app::now() - t0));
+    st.insert(pg->allreduce_max((app::now() - t0) / per));
   }
   if (pg->rank() == 0)
     std::printf("astaroth,%s,%d,%ld,%ld,%ld,%d,%e,%e,%.3f,%e\n", to_string(cfg.methods).c_str(), pg->size(), long(x),

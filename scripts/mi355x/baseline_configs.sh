@@ -9,5 +9,8 @@ step c2_bench 120 python bench.py &&
 step c3_bench_exchange 300 ./build/bin/bench_exchange --x 512 --y 512 --z 512 --fr 2 --iters 30 &&
 step c4_astaroth 300 ./build/bin/astaroth_sim --x 512 --y 512 --z 512 --q 8 -n 5 &&
 step c5_weak_fp64 300 ./build/bin/weak 1024 1024 1024 10 --q 4 --fp64 &&
-step c5_astaroth_fp64 400 ./build/bin/astaroth_sim --x 1024 --y 1024 --z 1024 --q 8 --fp64 -n 3
+step c5_astaroth_fp64 400 ./build/bin/astaroth_sim --x 1024 --y 1024 --z 1024 --q 8 --fp64 -n 3 &&
+step app_jacobi_t2 200 ./build/bin/jacobi3d 512 512 512 -n 20 --temporal 2 &&
+step app_jacobi_t1 200 ./build/bin/jacobi3d 512 512 512 -n 20 &&
+step c4_astaroth_t2 300 ./build/bin/astaroth_sim --x 512 --y 512 --z 512 --q 8 -n 6 --temporal 2
 echo "done rc=$?"
