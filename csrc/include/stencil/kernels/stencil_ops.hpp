@@ -50,9 +50,10 @@ struct StencilTune {
   // z lookahead (1/2/3). 12 waves get 3 waves/SIMD and up to 168 VGPRs (no spills at any lookahead, fp32 or fp64);
   // one MI355X, 512^3, bench.py: 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s
   int x2nw = 12, x2pf = 3;
-  // fused pairs of fp32 sub-domains whose x axis is wrapped in-kernel and 512 cells long: one wave per whole row
-  // (two 16-B chunks per lane, periodic x-neighbours by lane rotates; stencil7x2_row_kernel). 0 = always the
-  // 256-cell column kernel
+  // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells
+  // long; x-neighbours and the wrap by DPP lane rotates, stencil7x2_row_kernel), or 512-cell columns (x a whole
+  // number of 512-cell columns: two 16-B chunks per lane, only the column ends from outside the wave,
+  // stencil7x2_col2_kernel). 0 = always the 256-cell column kernel
   int x2row = 1;
   // fused-pair work split: 1 (default) = one block per resident slot, each taking an equal share of the
   // (column, plane) space (one or two z segments): no partly empty last round and the fewest warm-up planes;

@@ -567,6 +567,249 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   } // segments
 }
 
+// 512-cell columns (fp32): the whole-row layout of stencil7x2_row_kernel (two 16-B chunks per lane, 256 cells apart,
+// x-neighbours by lane rotates) for rows longer than one wave: a column of 512 cells per wave, and only the two
+// cells beyond each column end come from outside the wave - a pair left of the column (lane 0 of chunk 0) and a pair
+// right of it (lane 63 of chunk 1). Those pairs have one address per wave (a broadcast load each, shifted by the
+// period at the wrapped row ends), and the neighbour rows' pairs come through LDS, as the edge scalars of
+// stencil7x2_kernel. Taken for x extents that are whole multiples of 512 cells (the 1024-wide sub-domains of the
+// 8-GPU weak-scaling ladder): per row and plane the edge work and the fixed per-step cost of the 256-cell column
+// kernel are paid once per 512 cells. Summation order, exact /6 and spheres as everywhere: bitwise equal to two
+// single steps.
+template <int NW, int PF, int KIND, int WRAP>
+__global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void stencil7x2_col2_kernel(
+    StencilArgs<float> a) {
+  using T = float;
+  using NV = nf4;
+  using P2 = typename Pk<T>::t;
+  constexpr int V = 4, H = 2;   // chunks per lane
+  constexpr int HS = 64 * V;    // cells between a lane's chunks
+  constexpr int CW = H * HS;    // cells per column
+  constexpr int YO = NW - 4;
+  constexpr int NC = 3 + PF;
+  static_assert(NW == 12, "3 waves per SIMD: the 168-VGPR budget");
+  __shared__ NV cs[2][NW][H][64]; // src rows (plane z+2dz at publish)
+  __shared__ NV us[2][NW][H][64]; // u1 rows (plane z+dz at publish)
+  __shared__ T ce[2][NW][2];      // src at x-1 and x+512 of the published rows
+
+  const uint32_t nb = gridDim.x;
+  const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
+  const int lane = threadIdx.x;
+  const int w = int(threadIdx.y);
+  const uint32_t nzt = uint32_t(a.hiz - a.loz);
+  uint32_t s, e;
+  if (a.seg) {
+    const uint64_t W = uint64_t(uint32_t(a.gx) * uint32_t(a.gy)) * nzt;
+    s = uint32_t(uint64_t(lb) * W / nb);
+    e = uint32_t(uint64_t(lb + 1) * W / nb);
+  } else {
+    const uint32_t col = lb / uint32_t(a.gz);
+    s = col * nzt + (lb % uint32_t(a.gz)) * uint32_t(a.zc);
+    e = min(s + uint32_t(a.zc), (col + 1) * nzt);
+  }
+  bool odd = a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0;
+  while (s < e) { // block-uniform
+  const uint32_t col = s / nzt;
+  const int zo = int(s - col * nzt);
+  const int nzs = int(min(nzt - uint32_t(zo), e - s));
+  s += uint32_t(nzs);
+  int bx, by;
+  if (a.xfast) {
+    by = int(col / uint32_t(a.gx));
+    bx = int(col - uint32_t(by) * uint32_t(a.gx));
+  } else {
+    bx = int(col / uint32_t(a.gy));
+    by = int(col - uint32_t(bx) * uint32_t(a.gy));
+  }
+  const int zs = a.loz + zo;
+  const int ze = zs + nzs;
+  const bool down = odd != (a.flip != 0);
+  odd = !odd;
+  const int xcol = a.x0 + bx * CW;  // first cell of the column
+  const int xb = xcol + lane * V;   // chunk h at xb + h * HS
+  const int yblk = a.loy + YO * by;
+  const int y = yblk - 2 + w;
+  if (yblk >= a.hiy) continue;
+  const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy;
+  const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
+  const bool lane0 = lane == 0, lane63 = lane == 63;
+
+  const int yw =
+      (WRAP >= 1 && (a.wrapm & 2)) ? (y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y)) : y;
+  const int yc = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
+  const uint32_t rowoff = uint32_t((yc * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+  const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+  // the edge pairs (x-2, x-1 left of the column; x+512, x+513 right of it): one address per wave; x wrap moves the
+  // left pair of the first column and the right pair of the last one by the period
+  int xl = xcol - 2, xr = xcol + CW;
+  if (WRAP == 2 && (a.wrapm & 1)) {
+    if (xcol == a.wlo[0]) xl += a.wn[0];
+    if (xcol + CW == a.wlo[0] + a.wn[0]) xr -= a.wn[0];
+  }
+  const uint32_t loff = uint32_t((yc * int64_t(a.px) + xl) * int64_t(sizeof(T)));
+  const uint32_t roff = uint32_t((yc * int64_t(a.px) + xr) * int64_t(sizeof(T)));
+  const int zwn = (WRAP >= 1 && (a.wrapm & 4)) ? a.wn[2] : 0, zwlo = a.wlo[2], zwhi = a.wlo[2] + zwn;
+  auto zcl = [&](int zz) {
+    if constexpr (WRAP >= 1) {
+      zz += zz < zwlo ? zwn : 0;
+      zz -= zz >= zwhi ? zwn : 0;
+    }
+    return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
+  };
+  auto planep = [&](int zz) -> const char * { return reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy); };
+  struct RowSph {
+    int dh, dc;
+    bool hit;
+  };
+  auto row_sph = [&](int P) -> RowSph {
+    RowSph r{0, 0, false};
+    if (KIND == 0 && a.r1sq > 0) {
+      r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
+      r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
+      r.hit = r.dh < a.r1sq || r.dc < a.r1sq;
+    }
+    return r;
+  };
+  auto fix = [&](const RowSph &rs, int x, T v) -> T {
+    const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
+    const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+    return hot ? T(1) : (cold ? T(0) : v);
+  };
+  // S of the wave's column: x-neighbours by lane rotates, eL / eR beyond the column ends
+  auto apply_row = [&](const NV (&cm)[H], const NV (&up)[H], const NV (&dn)[H], const NV (&zp)[H], const NV (&zm)[H],
+                       T eL, T eR, const RowSph &rs, NV (&o)[H]) {
+    T r3[H], l0[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      r3[h] = rot_prev(cm[h][V - 1]);
+      l0[h] = rot_next(cm[h][0]);
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const T left = lane0 ? (h == 0 ? eL : r3[h - 1]) : r3[h];
+      const T right = lane63 ? (h == H - 1 ? eR : l0[h + 1]) : l0[h];
+      NV vpx, vmx;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        vpx[k] = k < V - 1 ? cm[h][k + 1] : right;
+        vmx[k] = k > 0 ? cm[h][k - 1] : left;
+      }
+      o[h] = div6v<T, NV, V>(sum6v<T, KIND>(vpx, vmx, dn[h], up[h], zp[h], zm[h]));
+    }
+    if (KIND == 0 && rs.hit) {
+#pragma unroll
+      for (int h = 0; h < H; ++h)
+#pragma unroll
+        for (int k = 0; k < V; ++k) o[h][k] = fix(rs, xb + h * HS + k, o[h][k]);
+    }
+  };
+
+  auto march = [&](auto downTag) {
+    constexpr bool DOWN = decltype(downTag)::value;
+    constexpr int dz = DOWN ? -1 : 1;
+    const int z0 = DOWN ? ze - 1 : zs;
+    NV C[NC][H];
+    P2 EL[NC], ER[NC]; // (x-2, x-1) and (x+512, x+513) of the column, per window plane
+    NV Ub[H], Uc[H], Ua[H];
+    P2 UcE, UaE; // u1 at (x-1, x+512), planes z and z+dz
+    auto load_row = [&](int zz, int k) {
+      const char *b = planep(zz);
+#pragma unroll
+      for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + rowoff + h * HS * int(sizeof(T)));
+      EL[k] = *reinterpret_cast<const P2 *>(b + loff);
+      ER[k] = *reinterpret_cast<const P2 *>(b + roff);
+    };
+    auto publish_src = [&](int bufi, int k) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) cs[bufi][w][h][lane] = C[k][h];
+      if (lane0) {
+        ce[bufi][w][0] = EL[k][1];
+        ce[bufi][w][1] = ER[k][0];
+      }
+    };
+    {
+      const int zw = z0 - 2 * dz;
+#pragma unroll
+      for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, k);
+      publish_src(0, 1);
+      __syncthreads();
+    }
+    int buf = 0;
+    int t = -2;
+    auto step = [&](auto phase) -> bool {
+      constexpr int k = decltype(phase)::value;
+      constexpr int s0 = k % NC, s1 = (k + 1) % NC, s2 = (k + 2) % NC, sn = (k + NC - 1) % NC;
+      if (t >= nzs) return false;
+      const int z = z0 + t * dz;
+      const int P = z + dz;
+      load_row(z + (NC - 1) * dz, sn);
+      {
+        NV cA[H], cB[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          cA[h] = cs[buf][wA][h][lane];
+          cB[h] = cs[buf][wB][h][lane];
+        }
+        const T cAL = ce[buf][wA][0], cAR = ce[buf][wA][1]; // LDS broadcasts
+        const T cBL = ce[buf][wB][0], cBR = ce[buf][wB][1];
+        const RowSph rs = row_sph(P);
+        apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], EL[s1][1], ER[s1][0], rs, Ua);
+        // u1 just outside the column: (x-1) on lane 0, (x+512) on lane 63
+        const P2 epx = {C[s1][0][0], ER[s1][1]}, emx = {EL[s1][0], C[s1][H - 1][V - 1]}, epy = {cBL, cBR},
+                 emy = {cAL, cAR};
+        const P2 ezp = DOWN ? P2{EL[s0][1], ER[s0][0]} : P2{EL[s2][1], ER[s2][0]};
+        const P2 ezm = DOWN ? P2{EL[s2][1], ER[s2][0]} : P2{EL[s0][1], ER[s0][0]};
+        UaE = div6v<T, P2, 2>(sum6v<T, KIND>(epx, emx, epy, emy, ezp, ezm));
+        if (KIND == 0 && rs.hit) {
+          UaE[0] = fix(rs, xcol - 1, UaE[0]);
+          UaE[1] = fix(rs, xcol + CW, UaE[1]);
+        }
+      }
+      if (t >= 0) {
+        NV uA[H], uB[H], o[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          uA[h] = us[buf][wA][h][lane];
+          uB[h] = us[buf][wB][h][lane];
+        }
+        apply_row(Uc, uA, uB, DOWN ? Ub : Ua, DOWN ? Ua : Ub, UcE[0], UcE[1], row_sph(z), o);
+        if (outRow) {
+          char *dp = reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff;
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            NV *q = reinterpret_cast<NV *>(dp + h * HS * int(sizeof(T)));
+            if (a.nt)
+              __builtin_nontemporal_store(o[h], q);
+            else
+              *q = o[h];
+          }
+        }
+      }
+      const int nbuf = buf ^ 1;
+      publish_src(nbuf, s2);
+#pragma unroll
+      for (int h = 0; h < H; ++h) us[nbuf][w][h][lane] = Ua[h];
+      __syncthreads();
+      buf = nbuf;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        Ub[h] = Uc[h];
+        Uc[h] = Ua[h];
+      }
+      UcE = UaE;
+      ++t;
+      return true;
+    };
+    while (run_phases(step, std::make_integer_sequence<int, NC>{})) {
+    }
+  };
+  if (down)
+    march(std::true_type{});
+  else
+    march(std::false_type{});
+  } // segments
+}
+
 // S o S on a few small boxes (the exterior slabs of an overlapped step: interior sweep during the exchange, these
 // after it). One thread per output cell: u2 = S of the six u1 neighbours, each u1 = S of its six src neighbours,
 // in the single step's summation order with the exact /6 and the spheres, i.e. the same bits as the sweep kernel
@@ -885,6 +1128,58 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   return true;
 }
 
+// 512-cell column kernel: fp32, the region's x extent a whole number of 512-cell columns starting on a 16-B chunk
+template <int KIND, int PF, int WRAP>
+static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph,
+                           hipStream_t stream, const StencilTune &tune) {
+  constexpr int NW = 12, YO = NW - 4;
+  StencilArgs<float> a = make_args<float>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
+  a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
+  a.nt = tune.nontemporal ? 1 : 0;
+  a.wrapm = tune.wrap;
+  a.xfast = tune.x2xfast;
+  a.remap = tune.xcdRemap ? 1 : 0;
+  a.x0 = a.lox; // 16-B aligned (checked by the caller)
+  a.nchunks = (a.hix - a.x0) / 4;
+  const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  a.gx = (a.hix - a.x0) / 512;
+  a.gy = (ny + YO - 1) / YO;
+  const void *kern = (const void *)stencil7x2_col2_kernel<NW, PF, KIND, WRAP>;
+  const int64_t cols = int64_t(a.gx) * a.gy;
+  const int64_t resident = x2_resident_blocks(kern, 64 * NW);
+  uint32_t blocks;
+  if (tune.x2sched != 0 && tune.zchunk <= 0) {
+    a.seg = 1;
+    a.zc = 1;
+    a.gz = 1;
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dom.gpu()) != hipSuccess) cus = 256;
+    const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
+    const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
+    blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 16)));
+  } else {
+    int zc = tune.zchunk;
+    if (zc <= 0) zc = pick_zchunk(cols, nz, resident, 4, 16);
+    a.zc = zc;
+    a.gz = (nz + zc - 1) / zc;
+    blocks = uint32_t(cols * a.gz);
+  }
+  dom.set_device();
+  hipLaunchKernelGGL((stencil7x2_col2_kernel<NW, PF, KIND, WRAP>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int KIND, int PF>
+static void apply_x2col2_wrap(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph,
+                              hipStream_t stream, const StencilTune &tune) {
+  if (tune.wrap & 1)
+    apply_x2col2_t<KIND, PF, 2>(dom, qi, region, sph, stream, tune);
+  else if (tune.wrap)
+    apply_x2col2_t<KIND, PF, 1>(dom, qi, region, sph, stream, tune);
+  else
+    apply_x2col2_t<KIND, PF, 0>(dom, qi, region, sph, stream, tune);
+}
+
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune) {
   if (region.empty()) return;
@@ -908,6 +1203,15 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
                      : (pf == 2 ? apply_x2row_t<1, 2>(dom, qi, region, sph, stream, tune)
                                 : apply_x2row_t<1, 3>(dom, qi, region, sph, stream, tune));
     if (done) return;
+    // x a whole number of 512-cell columns from a 16-B aligned first cell: the 512-cell column kernel
+    const Rect3 rr(region.lo - dom.accessor_origin(), region.hi - dom.accessor_origin());
+    const int64_t nx = rr.hi.x - rr.lo.x;
+    if (nx % 512 == 0 && (rr.lo.x - dom.radius().x(-1)) % 4 == 0) {
+      // one plane of lookahead (two would spill the Jacobi instance; the row kernel shows no difference)
+      jac ? apply_x2col2_wrap<0, 1>(dom, qi, region, sph, stream, tune)
+          : apply_x2col2_wrap<1, 1>(dom, qi, region, sph, stream, tune);
+      return;
+    }
   }
   // shapes (rows per lane, waves per block, min waves/SIMD): 1x8 keeps everything in registers at 6 waves/SIMD;
   // 2x4 at 3 waves/SIMD; 2x8 at 4 (spills)

@@ -240,6 +240,40 @@ def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf):
             assert torch.equal(_gather(m), u), f"x2row={1 - ms.index(m)} after run({n})"
 
 
+@pytest.mark.parametrize("kind,size,gpus,wrap,cost", [
+    ("astaroth", (1024, 24, 20), [0], True, (4, 2, 3)),     # periodic x: two 512-cell columns
+    ("astaroth", (1024, 20, 16), [0], False, (4, 2, 3)),    # x halos in memory
+    ("astaroth", (512, 20, 24), [0], False, (4, 2, 3)),     # one column between halos
+    ("astaroth", (1024, 16, 20), [0, 0], True, (1, 1, 1)),  # x cut: 512-wide halves, halos from the other half
+    ("jacobi", (1024, 216, 212), [0], True, (4, 2, 3)),     # spheres
+    ("jacobi", (512, 120, 116), [0], False, (4, 2, 3)),
+])
+def test_temporal2_col512_kernel(st, kind, size, gpus, wrap, cost):
+    """Fused pairs on x extents of whole 512-cell columns take the 512-cell column kernel (two chunks per lane, the
+    column-end pairs by broadcast loads, stencil7x2_col2_kernel): bitwise equal to single steps and to the 256-cell
+    column kernel (x2row = 0)."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    ms = []
+    for row in (1, 0):
+        t = st.StencilTune()
+        t.x2row = row
+        ms.append(cls(size, gpus=gpus, temporal=2, tune=t, wrap_self=wrap, axis_cost=cost, **kw))
+    for m in ms:
+        m.init()
+        assert m.temporal_blocking()
+    u = _gather(ms[0])
+    for n in (5, 16):
+        for m in ms:
+            m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        for m in ms:
+            m.synchronize()
+            assert torch.equal(_gather(m), u), f"x2row={1 - ms.index(m)} after run({n})"
+
+
 @pytest.mark.parametrize("temporal", [1, 2])
 def test_prepare_graph_blocks(st, temporal):
     """prepare() records run()'s hipGraph blocks for both buffer parities without running anything: the field is
