@@ -77,19 +77,40 @@ def scenario_canary(backend, methods, radius_name, size, iters=12):
 
 
 def scenario_jacobi(backend, methods, size):
+    """Jacobi3D (or, with MP_KIND=astaroth, the Astaroth proxy started from an analytic global field) across ranks,
+    compared with the torch oracle after 3 single steps and run(5)."""
     g = st.init_process_group()
     gpus = [0] if backend == st.Backend.Device else [0]
     temporal = int(os.environ.get("MP_TEMPORAL", "1"))
-    m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g, temporal=temporal)
+    kind = os.environ.get("MP_KIND", "jacobi")
+    if kind == "astaroth":
+        from stencil2_amd.ops import astaroth_step_reference as ref
+        m = st.AstarothSim(size, quantities=1, gpus=gpus, backend=backend, methods=methods, group=g,
+                           temporal=temporal)
+    else:
+        ref = jacobi_step_reference
+        m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g, temporal=temporal)
     m.init()
     L = m.domain.size()
-    u = torch.full((L.z, L.y, L.x), 0.5)
+    if kind == "astaroth":
+        z = torch.arange(L.z, dtype=torch.float64).view(-1, 1, 1)
+        y = torch.arange(L.y, dtype=torch.float64).view(1, -1, 1)
+        x = torch.arange(L.x, dtype=torch.float64).view(1, 1, -1)
+        u = (torch.sin(0.37 * x + 0.11 * y * y) * torch.cos(0.23 * z + 0.05 * x * y)).to(torch.float32)
+        for di in range(m.domain.num_domains()):
+            d = m.domain.domain(di)
+            o, s = d.origin(), d.size()
+            m.interior(di).copy_(u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x].to(m.interior(di).device))
+        if backend == st.Backend.Device:
+            torch.cuda.synchronize()
+    else:
+        u = torch.full((L.z, L.y, L.x), 0.5)
     for _ in range(3):
         m.step()
-        u = jacobi_step_reference(u)
+        u = ref(u)
     m.run(5)  # fused pairs when temporal blocking is on
     for _ in range(5):
-        u = jacobi_step_reference(u)
+        u = ref(u)
     m.synchronize()
     bad = 0
     for di in range(m.domain.num_domains()):

@@ -473,6 +473,19 @@ def test_colocated_ipc_jacobi_two_ranks(temporal, ranks):
         assert rc == 0, out[-3000:]
 
 
+@pytest.mark.parametrize("size", ["512,264,16", "1024,520,12"])  # the model cuts y (cost 4,2,3)
+def test_colocated_ipc_wide_rows_two_ranks(size):
+    """The whole-row (512) and 512-cell column (1024) fused-pair kernels in the overlapped multi-rank step: y is cut
+    between two ranks sharing one GPU (HIP IPC), x stays whole and wrapped in-kernel; S o S of the local interior
+    runs while the remote y halos are in flight (Astaroth proxy from an analytic field, bitwise vs the oracle)."""
+    outs = run_ranks(2, WORKER, ["jacobi", size],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": "2", "MP_KIND": "astaroth", "MP_EXPECT_OVERLAP": "1"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out
+
+
 def test_ipc_probe_failure_falls_back_on_shared_gpu():
     """Co-located ranks on one GPU whose IPC pre-flight fails (forced) must not pick RCCL (it refuses two ranks on
     one device): the runtime drops Colocated and Rccl and stages through the host; results stay exact."""
