@@ -17,12 +17,22 @@ col = src[a:b].replace("template <typename T, int NW, int PF, int KIND, int WRAP
                        "template <typename T, int NW, int PF, int KIND, int WRAP, int ABL>")
 col = ablate(col.replace("void stencil7x2_kernel(StencilArgs<T> a)", "void lab_col(StencilArgs<T> a)"))
 c = src.index("template <int NW, int PF, int KIND>\n__global__")
-d = src.index("// S o S on a few small boxes")
+d = src.index("// 512-cell columns (fp32)") if "// 512-cell columns (fp32)" in src else src.index("// S o S on a few small boxes")
 rot = src[b:c]
 row = src[c:d].replace("template <int NW, int PF, int KIND>", "template <int NW, int PF, int KIND, int ABL>")
 row = ablate(row.replace("stencil7x2_row_kernel(", "lab_row("))
 assert "ABL & 2" in col and "ABL & 1" in col and "ABL & 2" in row and "ABL & 1" in row
-open(os.path.join(HERE, "x2lab_kernel.inc"), "w").write(col + "\n" + rot + "\n" + row)
+# lab_rownt: the row kernel with nontemporal loads for the rows no other block reads (waves 4..7 of 12)
+old_ld = "#pragma unroll\n      for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + h * HS * int(sizeof(T)));"
+assert old_ld in row
+rownt = row.replace("lab_row(", "lab_rownt(").replace(old_ld, """      if (w >= 4 && w < 8) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) C[k][h] = __builtin_nontemporal_load(reinterpret_cast<const NV *>(b + h * HS * int(sizeof(T))));
+      } else {
+#pragma unroll
+        for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + h * HS * int(sizeof(T)));
+      }""")
+open(os.path.join(HERE, "x2lab_kernel.inc"), "w").write(col + "\n" + rot + "\n" + row + "\n" + rownt)
 h0 = src.index("// whole-wave lane shifts on the DPP path")
 h1 = src.index("// Block = NW waves, ONE src row per wave")
 open(os.path.join(HERE, "x2lab_helpers.inc"), "w").write("namespace stencil {\n" + src[h0:h1] + "}\n")
