@@ -71,11 +71,12 @@ struct StencilTune {
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous
   // step wrote last, which are still in the MALL / L2
   bool alternateZ = true;
-  // fused pairs only: bitmask of axes (1 = x, 2 = y, 4 = z) along which the sub-domain is its own periodic
+  // bitmask of axes (1 = x, 2 = y, 4 = z) along which the sub-domain is its own periodic
   // neighbour and the kernels read the periodic image in place of the halo (StencilModel sets it together with
   // DistributedDomain::exchange_async(.., skipWrapped), which then skips those same-GPU self copies). Needs the
   // region to span the whole compute region along wrapped axes, and for x an extent that is a multiple of the
-  // 16-B chunk (>= 2 chunks). 0 = read halos.
+  // 16-B chunk (fused pairs: >= 2 chunks). Fused pairs: stencil7x2_wrappable_axes; single steps (stencil7_apply):
+  // stencil7_wrappable_axes. 0 = read halos.
   int wrap = 0;
 };
 // axes (mask as StencilTune::wrap) the fused-pair kernels can wrap in-kernel for this quantity's layout
@@ -143,6 +144,9 @@ void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vec
 // the sweep kernel (6 waves per block for 2-row slabs), thin x slabs by a lanes-on-rows kernel
 void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &interior, StencilKind kind,
                                const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());
+// axes (mask as StencilTune::wrap) stencil7_apply can wrap in-kernel for this quantity's layout: with tune.wrap set
+// the single step reads the periodic image along those axes instead of the halo (the region must span them)
+int stencil7_wrappable_axes(const LocalDomain &dom, int64_t qi);
 // MFMA variant of the single step (fp32 Jacobi; StencilTune::variant == kMfma routes stencil7_apply here)
 bool stencil7_mfma_supported(const LocalDomain &dom, int64_t qi);
 void stencil7_mfma_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,

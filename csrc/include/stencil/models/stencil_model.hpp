@@ -52,7 +52,8 @@ struct StencilModelConfig {
   // fused pairs: along axes where the decomposition has one sub-domain (periodic self-neighbour,
   // DistributedDomain::self_wrap_axes) the pair kernels read the periodic image in place of the halo, and the
   // pair's exchange skips those same-GPU copies (on one MI355X at 512^3 the depth-2 self-copy is ~34 us of a ~300 us
-  // pair, mostly the strided x faces). Single steps keep the full exchange. Off: every halo is copied.
+  // pair, mostly the strided x faces). Single steps do the same when they do not overlap or forward (the
+  // exchange then leaves out every self copy). Off: every halo is copied.
   bool wrapSelf = true;
   bool setBackend = false;
   Backend backend = Backend::Device;
@@ -84,6 +85,7 @@ public:
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }
   int wrap_axes() const { return pairTune_.wrap; } // axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
+  int step_wrap_axes() const { return stepTune_.wrap; } // same for single steps (stencil7_apply)
 
 private:
   StencilModelConfig cfg_;
@@ -99,6 +101,7 @@ private:
   bool forward_ = false;
   bool pairs_ = false; // temporal blocking active
   StencilTune pairTune_; // cfg_.tune + the in-kernel wrap axes of the fused pairs
+  StencilTune stepTune_; // cfg_.tune + the in-kernel wrap axes of single steps
   std::vector<std::vector<std::unique_ptr<HaloForwarder>>> fwd_; // [domain][quantity]
   std::vector<Event> stepDone_;                                    // forwarding with several sub-domains
   hipGraphExec_t graphExec_[2] = {nullptr, nullptr};

@@ -613,6 +613,7 @@ PYBIND11_MODULE(_C, m) {
       .def("forwarding", &StencilModel::forwarding)
       .def("temporal_blocking", &StencilModel::temporal_blocking)
       .def("wrap_axes", &StencilModel::wrap_axes)
+      .def("step_wrap_axes", &StencilModel::step_wrap_axes)
       .def("compute_stream", [](StencilModel &mdl, size_t di) { return reinterpret_cast<uintptr_t>(mdl.compute_stream(di)); })
       .def("domain",
            [](std::shared_ptr<StencilModel> mdl) {

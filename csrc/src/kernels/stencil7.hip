@@ -197,7 +197,11 @@ __device__ __forceinline__ void forward_edges(const StencilArgs<T> &a, T *dp, co
 // reads per output row drop from (TY+2)/TY to (NW*TY+2)/(NW*TY).
 // PF = z-planes of lookahead: 1 loads plane z+1 while computing plane z (the loads are consumed in the same step,
 // so only other waves hide their latency); 2 loads plane z+2, so every load has a whole step to land.
-template <typename T, int TY, int NW, int KIND, bool NT, bool REMAP, bool FWD, int PF = 1>
+// WRAP: along the axes set in a.wrapm the sub-domain is its own periodic neighbour (StencilTune::wrap): rows and
+// planes beyond a face, and the edge scalars of the first / last chunk of a row, are read at their periodic image,
+// so those halos need not be exchanged (one conditional shift per access; needs the chunk grid to start at lox and
+// whole chunks along x).
+template <typename T, int TY, int NW, int KIND, bool NT, bool REMAP, bool FWD, int PF = 1, bool WRAP = false>
 __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void stencil7_lds_kernel(StencilArgs<T> a) {
   using VT = typename Vec16<T>::type;
   constexpr int V = Vec16<T>::N;
@@ -274,11 +278,26 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
   const int slotAbove = w == 0 ? 2 * NW : 2 * (w - 1) + 1;
   const int slotBelow = w == NW - 1 ? 2 * NW + 1 : 2 * (w + 1);
 
+  // periodic images (WRAP): y beyond the region's y faces, z beyond its z faces (then clamped into the allocation:
+  // the lookahead planes past the march end are loaded but never used)
+  const int ywn = WRAP && (a.wrapm & 2) ? a.wn[1] : 0, ywlo = a.wlo[1], ywhi = a.wlo[1] + ywn;
+  const int zwn = WRAP && (a.wrapm & 4) ? a.wn[2] : 0, zwlo = a.wlo[2], zwhi = a.wlo[2] + zwn;
   auto rowp = [&](int y, int z) -> const T * {
+    if constexpr (WRAP) {
+      y += y < ywlo ? ywn : 0;
+      y -= y >= ywhi ? ywn : 0;
+      z += z < zwlo ? zwn : 0;
+      z -= z >= zwhi ? zwn : 0;
+      z = z < 0 ? 0 : (z > a.rawZm1 ? a.rawZm1 : z);
+    }
     y = min(y, a.rawYm1);
     return a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
   };
   auto ld = [&](const T *p) -> VT { return *reinterpret_cast<const VT *>(p); };
+  // x edge scalars: left of the row's first chunk / right of its last one at the periodic image
+  const bool xw = WRAP && (a.wrapm & 1);
+  const int offL = -1 + (xw && xb == a.lox ? a.wn[0] : 0);
+  const int offR = V - (xw && xb + V == a.hix ? a.wn[0] : 0);
 
   VT prev[TY], cur[TY], nxt[TY];
   T curL[TY], curR[TY], nxtL[TY], nxtR[TY];
@@ -294,8 +313,8 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
   for (int i = 0; i < TY; ++i) {
     const T *p = rowp(ybase + i, z0);
     cur[i] = ld(p);
-    curL[i] = edgeL ? p[-1] : T(0);
-    curR[i] = edgeR ? p[V] : T(0);
+    curL[i] = edgeL ? p[offL] : T(0);
+    curR[i] = edgeR ? p[offR] : T(0);
   }
   if (w == 0) lds[0][2 * NW][lane] = ld(rowp(yblk - 1, z0));
   if (w == NW - 1) lds[0][2 * NW + 1][lane] = ld(rowp(yblk + NW * TY, z0));
@@ -307,8 +326,8 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
     for (int i = 0; i < TY; ++i) {
       const T *p = rowp(ybase + i, z1);
       nxt[i] = ld(p);
-      nxtL[i] = edgeL ? p[-1] : T(0);
-      nxtR[i] = edgeR ? p[V] : T(0);
+      nxtL[i] = edgeL ? p[offL] : T(0);
+      nxtR[i] = edgeR ? p[offR] : T(0);
     }
     if (w == 0) haloN = ld(rowp(yblk - 1, z1));
     if (w == NW - 1) haloN = ld(rowp(yblk + NW * TY, z1));
@@ -319,8 +338,8 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
       for (int i = 0; i < TY; ++i) {
         const T *p = rowp(ybase + i, zk);
         fut[k][i] = ld(p);
-        futL[k][i] = edgeL ? p[-1] : T(0);
-        futR[k][i] = edgeR ? p[V] : T(0);
+        futL[k][i] = edgeL ? p[offL] : T(0);
+        futR[k][i] = edgeR ? p[offR] : T(0);
       }
       if (w == 0) futH[k] = ld(rowp(yblk - 1, zk));
       if (w == NW - 1) futH[k] = ld(rowp(yblk + NW * TY, zk));
@@ -342,8 +361,8 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
 #pragma unroll
         for (int i = 0; i < TY; ++i) {
           const T *p = rowp(ybase + i, zn);
-          nxtL[i] = edgeL ? p[-1] : T(0);
-          nxtR[i] = edgeR ? p[V] : T(0);
+          nxtL[i] = edgeL ? p[offL] : T(0);
+          nxtR[i] = edgeR ? p[offR] : T(0);
         }
       }
     } else {
@@ -353,8 +372,8 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
       for (int i = 0; i < TY; ++i) {
         const T *p = rowp(ybase + i, zf);
         fut[NF - 1][i] = ld(p);
-        futL[NF - 1][i] = edgeL ? p[-1] : T(0);
-        futR[NF - 1][i] = edgeR ? p[V] : T(0);
+        futL[NF - 1][i] = edgeL ? p[offL] : T(0);
+        futR[NF - 1][i] = edgeR ? p[offR] : T(0);
       }
       if (w == 0) futH[NF - 1] = ld(rowp(yblk - 1, zf));
       if (w == NW - 1) futH[NF - 1] = ld(rowp(yblk + NW * TY, zf));
@@ -798,7 +817,7 @@ static int64_t resident_blocks(const void *kernel, int threads) {
   return r;
 }
 
-template <typename T, int TY, int NW, int KIND>
+template <typename T, int TY, int NW, int KIND, bool WRAP = false>
 static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t stream) {
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = (a.nchunks + 63) / 64;
@@ -809,7 +828,8 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
     // end (512^3, 2 rows/lane: 1024 blocks at 768 resident ran 20% slower than 768 or 512). z-chunks >= 16
     // planes (the warm-up planes of neighbouring chunks are shared, see kernel).
     const int64_t cols = int64_t(a.gx) * a.gy;
-    const void *kern = a.fmask ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>
+    const void *kern = WRAP      ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 2, true>
+                       : a.fmask ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>
                        : tune.variant == 2 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 2>
                        : tune.variant == 3 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 3>
                        : tune.variant == 4 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 4>
@@ -822,7 +842,10 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
   a.gz = (nz + zc - 1) / zc;
   const uint32_t blocks = uint32_t(a.gx) * a.gy * a.gz;
   const dim3 block(64, NW);
-  if (a.fmask)
+  if (WRAP)
+    hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 2, WRAP>), dim3(blocks), block, 0, stream,
+                       a);
+  else if (a.fmask)
     hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, true>), dim3(blocks), block, 0, stream, a);
   else if (tune.variant == 2)
     hipLaunchKernelGGL((stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 2>), dim3(blocks), block, 0, stream, a);
@@ -872,6 +895,23 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
   const bool fits = a.x0 + int64_t(a.nchunks) * V < a.px - dom.pad_x(qi);
   dom.set_device();
   STENCIL_REQUIRE(!fwd || (alignedLayout && fits), "halo forwarding needs the aligned vector layout");
+  if (tune.wrap != 0) {
+    // in-kernel periodic wrap: the lookahead-2 LDS kernel (the default shape) reading periodic images
+    STENCIL_REQUIRE(fwd == nullptr, "in-kernel wrap and halo forwarding are exclusive");
+    STENCIL_REQUIRE((tune.wrap & ~stencil7_wrappable_axes(dom, qi)) == 0,
+                    "in-kernel wrap " << tune.wrap << " not supported by this layout (" << stencil7_wrappable_axes(dom, qi)
+                                      << ")");
+    const Rect3 cr = dom.get_compute_region();
+    const int64_t lo[3] = {region.lo.x, region.lo.y, region.lo.z}, hi[3] = {region.hi.x, region.hi.y, region.hi.z};
+    const int64_t clo[3] = {cr.lo.x, cr.lo.y, cr.lo.z}, chi[3] = {cr.hi.x, cr.hi.y, cr.hi.z};
+    for (int ax = 0; ax < 3; ++ax)
+      STENCIL_REQUIRE(!((tune.wrap >> ax) & 1) || (lo[ax] == clo[ax] && hi[ax] == chi[ax]),
+                      "region " << region << " does not span wrapped axis " << ax << " of " << cr);
+    STENCIL_REQUIRE(alignedLayout && fits && a.x0 == a.lox, "in-kernel wrap needs the aligned vector layout");
+    a.wrapm = tune.wrap;
+    launch_lds<T, 2, 8, KIND, true>(a, tune, stream);
+    return;
+  }
   if (alignedLayout && fits && (fwd || std::getenv("STENCIL_GENERIC_KERNEL") == nullptr)) {
     if (fwd) {
       // the forwarding epilogue needs registers: 2 rows per lane keeps it spill-free at >= 4 waves/SIMD
@@ -907,6 +947,23 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
   }
 }
 
+int stencil7_wrappable_axes(const LocalDomain &dom, int64_t qi) {
+  if (dom.backend() != Backend::Device) return 0;
+  const DType dt = dom.dtype(qi);
+  const int64_t es = dom.elem_size(qi);
+  if (!(dt == DType::F32 || dt == DType::F64 || (dt == DType::Bytes && (es == 4 || es == 8)))) return 0;
+  const int64_t V = 16 / es;
+  const int64_t lox = dom.radius().x(-1), nx = dom.size().x;
+  const Dim3 p = dom.pitch(qi);
+  // the chunk grid starts at lox (16-B aligned) and the vector loads stay inside the padded row (apply_t's `fits`)
+  const bool aligned = (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + lox * es) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + lox * es) % 16 == 0) &&
+                       (p.x * es) % 16 == 0;
+  if (!aligned || lox + (nx + V - 1) / V * V >= p.x - dom.pad_x(qi)) return 0;
+  // x: whole chunks (the last chunk's right edge is the face); y / z: one conditional shift per access
+  return (nx % V == 0 ? 1 : 0) | 2 | 4;
+}
+
 void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                     hipStream_t stream, const StencilTune &tune, const HaloForwarder *fwd) {
   STENCIL_REQUIRE(dom.radius().x(-1) >= 1 && dom.radius().x(1) >= 1 && dom.radius().y(-1) >= 1 &&
@@ -918,6 +975,7 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
                   "stencil region " << region << " outside compute region " << cr);
   if (tune.variant == StencilTune::kMfma) {
     STENCIL_REQUIRE(fwd == nullptr, "the MFMA variant does not forward halos");
+    STENCIL_REQUIRE(tune.wrap == 0, "the MFMA variant reads halos (no in-kernel wrap)");
     stencil7_mfma_apply(dom, qi, region, kind, sph, stream, tune);
     return;
   }

@@ -25,83 +25,9 @@
 
 #include "stencil/rt/hip_check.hpp"
 #include "stencil_common.hpp"
+#include "stencil_wave.hpp"
 
 namespace stencil {
-
-// Packed-math helpers. A wave64 fp32 VALU op covers 64 lanes x 1 value; v_pk_{add,mul,fma}_f32 cover 64 x 2 at the
-// same issue cost, so rows are summed as pairs (2 pk ops per 4-float chunk per term). fp64 has no packed form: the
-// pair type is then two scalar ops. IEEE per element, so results are bitwise those of the scalar code.
-template <typename T> struct Pk;
-template <> struct Pk<float> { typedef float t __attribute__((ext_vector_type(2))); };
-template <> struct Pk<double> { typedef double t __attribute__((ext_vector_type(2))); };
-
-// whole-wave lane shifts on the DPP path (a VALU mov, no LDS round trip as with ds_bpermute): lane i receives
-// lane i-1 (wave_shr:1) / lane i+1 (wave_shl:1); the lanes shifted in from outside the wave get 0 and are replaced
-// by the edge scalars
-__device__ __forceinline__ int dpp_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
-__device__ __forceinline__ int dpp_shl1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }
-template <typename T> __device__ __forceinline__ T from_prev_lane(T v);
-template <typename T> __device__ __forceinline__ T from_next_lane(T v);
-template <> __device__ __forceinline__ float from_prev_lane<float>(float v) { return __int_as_float(dpp_shr1(__float_as_int(v))); }
-template <> __device__ __forceinline__ float from_next_lane<float>(float v) { return __int_as_float(dpp_shl1(__float_as_int(v))); }
-template <> __device__ __forceinline__ double from_prev_lane<double>(double v) {
-  const int64_t b = __double_as_longlong(v);
-  return __longlong_as_double(int64_t(uint32_t(dpp_shr1(int(b)))) | (int64_t(dpp_shr1(int(b >> 32))) << 32));
-}
-template <> __device__ __forceinline__ double from_next_lane<double>(double v) {
-  const int64_t b = __double_as_longlong(v);
-  return __longlong_as_double(int64_t(uint32_t(dpp_shl1(int(b)))) | (int64_t(dpp_shl1(int(b >> 32))) << 32));
-}
-
-// Six-term sums in the reference's order (sum6 in stencil_common.hpp), element-wise over a vector type. The fp32
-// sums start from the first term instead of 0 + first term: the two differ only in the sign of an all-zero sum,
-// and the exact /6 below maps both zeros to +0 as the 0-started sum does. fp64 keeps the 0 start (true division).
-template <typename T, int KIND, typename X>
-__device__ __forceinline__ X sum6v(const X &vpx, const X &vmx, const X &vpy, const X &vmy, const X &vpz, const X &vmz) {
-  X s;
-  if constexpr (KIND == 0) {
-    s = std::is_same<T, float>::value ? vpx : X(T(0)) + vpx;
-    s += vmx;
-    s += vpy;
-    s += vmy;
-    s += vpz;
-    s += vmz;
-  } else {
-    s = std::is_same<T, float>::value ? vmx : X(T(0)) + vmx;
-    s += vmy;
-    s += vmz;
-    s += vpx;
-    s += vpy;
-    s += vpz;
-  }
-  return s;
-}
-// exact element-wise /6 (div6): fp32 two FMAs around the reciprocal, packed; sums with 0 < |s| < 2^-100 (where the
-// FMA form is not exact) take the true division in a branch no wave normally enters
-template <typename T, typename X, int N> __device__ __forceinline__ X div6v(const X &s) {
-  if constexpr (std::is_same<T, float>::value) {
-    const X c = X(1.0f / 6.0f), six = X(6.0f);
-    const X q0 = s * c;
-    const X r = __builtin_elementwise_fma(-q0, six, s);
-    X q = __builtin_elementwise_fma(r, c, q0);
-    float m = __builtin_fabsf(s[0]);
-#pragma unroll
-    for (int e = 1; e < N; ++e) m = __builtin_fminf(m, __builtin_fabsf(s[e]));
-    if (__builtin_expect(m < 0x1p-100f, 0)) {
-#pragma unroll
-      for (int e = 0; e < N; ++e)
-        if (__builtin_fabsf(s[e]) < 0x1p-100f && s[e] != 0.0f) q[e] = s[e] / 6.0f;
-    }
-    return q;
-  } else {
-    return s / X(T(6));
-  }
-}
-
-// calls f(integral_constant<I>) for I = 0, 1, ... while it returns true; true if all did
-template <typename F, int... I> __device__ __forceinline__ bool run_phases(F &f, std::integer_sequence<int, I...>) {
-  return (f(std::integral_constant<int, I>{}) && ...);
-}
 
 // Block = NW waves, ONE src row per wave: the block's src rows are [yblk-2, yblk-2+NW); u1 is valid on the inner
 // NW-2 of them and u2 (the output) on the inner NW-4, so the block writes YO = NW-4 rows and every wave runs the
@@ -373,13 +299,6 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
 // sphere tests, loop control, one barrier per 12 rows of 512 cells instead of 256). Each chunk load / store is one
 // fully coalesced 1 KB wave instruction. Block, z-march, LDS y-neighbours, summation order, exact /6 and spheres
 // are those of stencil7x2_kernel: S(S(src)) is bitwise equal to two single steps.
-__device__ __forceinline__ float rot_prev(float v) { // lane i <- lane i-1, lane 0 <- lane 63 (wave_ror:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x13C, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float rot_next(float v) { // lane i <- lane i+1, lane 63 <- lane 0 (wave_rol:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xf, 0xf, false));
-}
-
 template <int NW, int PF, int KIND>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void stencil7x2_row_kernel(
     StencilArgs<float> a) {

@@ -61,6 +61,7 @@ hipStream_t StencilModel::compute_stream(size_t di) const { return compute_.empt
 
 void StencilModel::init() {
   TraceRange tr("StencilModel::init");
+  cfg_.tune.wrap = 0; // in-kernel wrap axes are the model's decision (pairTune_ / stepTune_ below)
   dd_->realize();
   const Rect3 cReg = dd_->get_compute_region();
   sph_ = cfg_.kind == StencilKind::Jacobi ? Spheres::jacobi(cReg) : Spheres();
@@ -129,6 +130,20 @@ void StencilModel::init() {
     }
     if (const char *e = std::getenv("STENCIL_WRAP_AXES")) w &= std::atoi(e); // restrict (experiments)
     pairTune_.wrap = w;
+    if (w != 0) dd_->prepare_skip_wrapped(w);
+  }
+  // single steps (whole compute region, no overlap / forwarding): the self-periodic axes are read in-kernel at their
+  // periodic image and their same-GPU copies leave the exchange (a fully periodic sub-domain exchanges nothing; one
+  // MI355X at 512^3: the ~25 us copy-plan kernel of a ~225 us step)
+  stepTune_ = cfg_.tune;
+  stepTune_.wrap = 0;
+  if (!pairs_ && !forward_ && !overlap_ && cfg_.wrapSelf && cfg_.tune.variant != StencilTune::kMfma &&
+      !doms0.empty() && std::getenv("STENCIL_NO_WRAP") == nullptr) {
+    int w = dd_->self_wrap_axes();
+    if (const char *e = std::getenv("STENCIL_WRAP_AXES")) w &= std::atoi(e);
+    for (const auto &d : doms0)
+      for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7_wrappable_axes(d, q);
+    stepTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
@@ -329,12 +344,12 @@ void StencilModel::enqueue_step(int k) {
   } else {
     // one device: enqueue the exchange on the compute stream itself (no cross-stream hand-offs)
     const bool single = device && doms.size() == 1;
-    dd_->exchange_async(single ? compute_[0].get() : nullptr);
+    dd_->exchange_async(single ? compute_[0].get() : nullptr, stepTune_.wrap);
     for (size_t di = 0; di < doms.size(); ++di) {
       hipStream_t s = device ? compute_[di].get() : nullptr;
       if (!single) dd_->wait_exchange(di, s);
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
-        stencil7_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, cfg_.tune);
+        stencil7_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, stepTune_);
     }
   }
 }

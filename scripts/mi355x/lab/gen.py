@@ -1,4 +1,4 @@
-"""Build x2lab_kernel.inc / x2lab_helpers.inc from csrc/src/kernels/stencil7x2.hip: lab_col = stencil7x2_kernel and
+"""Build x2lab_kernel.inc from csrc/src/kernels/stencil7x2.hip (the helpers come from stencil_wave.hpp): lab_col = stencil7x2_kernel and
 lab_row = stencil7x2_row_kernel, each with ablation bits ABL (1: no output stores, 2: no lookahead loads)."""
 import os
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +33,3 @@ rownt = row.replace("lab_row(", "lab_rownt(").replace(old_ld, """      if (w >= 
         for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + h * HS * int(sizeof(T)));
       }""")
 open(os.path.join(HERE, "x2lab_kernel.inc"), "w").write(col + "\n" + rot + "\n" + row + "\n" + rownt)
-h0 = src.index("// whole-wave lane shifts on the DPP path")
-h1 = src.index("// Block = NW waves, ONE src row per wave")
-open(os.path.join(HERE, "x2lab_helpers.inc"), "w").write("namespace stencil {\n" + src[h0:h1] + "}\n")

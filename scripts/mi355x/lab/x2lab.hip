@@ -6,12 +6,7 @@
 #include <cstring>
 #include <vector>
 #include "stencil_common.hpp"
-namespace stencil {
-template <typename T> struct Pk;
-template <> struct Pk<float> { typedef float t __attribute__((ext_vector_type(2))); };
-template <> struct Pk<double> { typedef double t __attribute__((ext_vector_type(2))); };
-}
-#include "x2lab_helpers.inc"
+#include "stencil_wave.hpp"
 namespace stencil {
 #include "x2lab_kernel.inc"
 }

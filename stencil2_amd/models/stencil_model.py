@@ -84,6 +84,10 @@ class StencilModel:
         """Axes (mask 1=x, 2=y, 4=z) the fused pairs read periodically in-kernel instead of from copied halos."""
         return self._m.wrap_axes()
 
+    def step_wrap_axes(self) -> int:
+        """Axes single steps read periodically in-kernel instead of from copied halos (0 = every halo copied)."""
+        return self._m.step_wrap_axes()
+
     def forwarding(self) -> bool:
         """True when the stencil kernels write the neighbours' halos directly (in-process exchanges only)."""
         return self._m.forwarding()

@@ -240,6 +240,41 @@ def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf):
             assert torch.equal(_gather(m), u), f"x2row={1 - ms.index(m)} after run({n})"
 
 
+@pytest.mark.parametrize("kind,size,gpus,fp64", [("jacobi", (512, 120, 116), [0], False),
+                                                 ("jacobi", (200, 72, 64), [0, 0], False),
+                                                 ("jacobi", (130, 40, 36), [0], False),
+                                                 ("astaroth", (512, 36, 28), [0], False),
+                                                 ("astaroth", (96, 260, 40), [0, 0, 0, 0], False),
+                                                 ("astaroth", (66, 30, 20), [0, 0], True)])
+def test_single_step_in_kernel_wrap(st, kind, size, gpus, fp64):
+    """Single steps read the periodic image along every self-periodic axis in-kernel (StencilTune.wrap on the LDS
+    kernel) and leave those self copies out of the exchange: bitwise equal to the torch oracle (spheres inside the
+    grid for Jacobi) and to the model that copies every halo (wrap_self=False), through run() (hipGraph blocks) and
+    step(); fp32 and fp64, x extents a multiple of the 16-B chunk or not."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    ms = [cls(size, gpus=gpus, temporal=1, wrap_self=ws, fp64=fp64, axis_cost=(4, 2, 3), **kw) for ws in (True, False)]
+    for m in ms:
+        m.init()
+        assert not m.temporal_blocking()
+    w = ms[0].domain.self_wrap_axes()
+    v = 2 if fp64 else 4
+    expect = w if size[0] % v == 0 else w & 6
+    assert ms[0].step_wrap_axes() == expect and ms[1].step_wrap_axes() == 0
+    assert (w == 7) == (len(gpus) == 1)
+    u = _gather(ms[0])
+    for n in (3, 16):
+        for m in ms:
+            m.run(n)
+            m.step()
+        for _ in range(n + 1):
+            u = ref(u)
+        for m in ms:
+            m.synchronize()
+            assert torch.equal(_gather(m), u), f"wrap_self={ms.index(m) == 0} after run({n}) + step()"
+
+
 @pytest.mark.parametrize("kind,size,gpus,wrap,cost", [
     ("astaroth", (1024, 24, 20), [0], True, (4, 2, 3)),     # periodic x: two 512-cell columns
     ("astaroth", (1024, 20, 16), [0], False, (4, 2, 3)),    # x halos in memory
