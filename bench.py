@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--wrap", type=int, default=1,
                     help="fused pairs read the periodic image along axes the decomposition leaves whole (no self-copy "
                          "of those halos); 0 = copy every halo")
-    ap.add_argument("--axis-cost", default="4,2,3",
+    ap.add_argument("--axis-cost", default="4,3,2",
                     help="NodeAware partition cost per interface cell of x,y,z cuts (1,1,1 = the reference's rule)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU)")

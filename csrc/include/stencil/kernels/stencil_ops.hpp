@@ -79,8 +79,9 @@ struct StencilTune {
   // stencil7_wrappable_axes. 0 = read halos.
   int wrap = 0;
 };
-// axes (mask as StencilTune::wrap) the fused-pair kernels can wrap in-kernel for this quantity's layout
-int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi);
+// axes (mask as StencilTune::wrap) the fused-pair kernels can wrap in-kernel for this quantity's layout; x2row as
+// StencilTune::x2row (0: no whole-row kernel, so ragged x extents are not wrappable)
+int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi, int x2row = 1);
 
 // Halo forwarding: the producer writes its neighbours' halos. For every direction whose receiving halo lives in a
 // sub-domain this process can store into directly (same GPU, or a P2P-mapped peer GPU over xGMI), the stencil

@@ -26,11 +26,12 @@ struct StencilModelConfig {
   MethodFlags methods = MethodFlags::All;
   PlacementStrategy placement = PlacementStrategy::NodeAware;
   // NodeAware cut costs (DistributedDomain::set_axis_cost): x faces count double, so weak-scaled cubes are cut
-  // along y and z only (8 GPUs: 1x4x2 instead of 2x2x2, the same face bytes per GPU for 512^3 per GPU, but
-  // row-contiguous faces whose exchange the fused pairs can overlap); y cuts cost less than z cuts so sub-domains
-  // keep long z columns for the z-marching sweeps (one MI355X, fused pairs: 1024x256x512 885 vs 1024x512x256
-  // 708-767 Gcells/s; 645x323x645 731 vs 645x645x323 704)
-  Dim3 axisCost{4, 2, 3};
+  // along y and z only (x faces are strided, and whole periodic rows feed the whole-row fused-pair kernels); z cuts
+  // cost less than y cuts (contiguous faces, and at these shapes the sweeps are faster with long y than long z).
+  // One MI355X, fused pairs, per-GPU shapes of the weak-scaling ladder (profiles/r2/r2_ragged_shapes2.log):
+  // N=2 645x645x323 837 vs 645x323x645 790; N=4 813x407x407 664 (either order); N=8 1024x512x256 1000 vs
+  // 1024x256x512 972 Gcells/s
+  Dim3 axisCost{4, 3, 2};
   std::vector<int> gpus;       // empty = automatic
   bool overlap = true;
   // when every halo comes from this GPU (periodic self-wrap / co-resident sub-domains) the exchange is a local

@@ -299,16 +299,24 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
 // sphere tests, loop control, one barrier per 12 rows of 512 cells instead of 256). Each chunk load / store is one
 // fully coalesced 1 KB wave instruction. Block, z-march, LDS y-neighbours, summation order, exact /6 and spheres
 // are those of stencil7x2_kernel: S(S(src)) is bitwise equal to two single steps.
-template <int NW, int PF, int KIND>
-__global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void stencil7x2_row_kernel(
-    StencilArgs<float> a) {
+//
+// Ragged rows (RAG: 256 (H-1) < nx < 256 H, e.g. the 645- and 813-cell rows of the 2- and 4-GPU weak-scaling
+// ladder): H chunks per lane, the last chunk group partly past the row end. The periodic neighbours of the row ends
+// are then not where the rotates put them, so each row application broadcasts the first cell (x = 0) and the last one
+// (x = nx-1, lane Lr, element kr of chunk H-1) with v_readlane and selects them in: left of x = 0 on lane 0, right of
+// x = nx-1 on lane Lr. Chunks wholly past the row end load the row start (finite values, never selected) and store
+// nothing; the partial chunk stores its cells one by one.
+template <int NW, int PF, int KIND, int H = 2, bool RAG = false>
+__global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
+stencil7x2_row_kernel(StencilArgs<float> a) {
   using T = float;
   using NV = nf4;
-  constexpr int V = 4, H = 2;   // chunks per lane
+  constexpr int V = 4;          // H = chunks per lane
   constexpr int HS = 64 * V;    // cells between a lane's chunks
   constexpr int YO = NW - 4;
   constexpr int NC = 3 + PF;
-  static_assert(NW == 12, "3 waves per SIMD: the 168-VGPR budget");
+  static_assert(NW == 12 && H <= 3, "3 waves per SIMD: the 168-VGPR budget; 144 KiB of LDS at H = 3");
+  static_assert(RAG || H == 2, "unragged rows: 512 cells");
   __shared__ NV cs[2][NW][H][64]; // src rows (plane z+2dz at publish)
   __shared__ NV us[2][NW][H][64]; // u1 rows (plane z+dz at publish)
 
@@ -344,6 +352,13 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy;
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
   const bool lane0 = lane == 0, lane63 = lane == 63;
+  // ragged rows: the last cell x = nx-1 sits in chunk H-1 of lane Lr, element kr
+  const int xl = a.hix - a.lox - 1 - HS * (H - 1);
+  const int Lr = xl >> 2, kr = xl & 3;
+  const bool lastIn = !RAG || lane <= Lr; // chunk H-1 of this lane holds cells of the row
+  auto choff = [&](int h) -> int { // byte offset of chunk h from the lane's first chunk
+    return (h < H - 1 || lastIn) ? h * HS * int(sizeof(T)) : 0;
+  };
 
   const int yw = (a.wrapm & 2) ? (y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y)) : y;
   const int yc = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
@@ -383,15 +398,25 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
       r3[h] = rot_prev(cm[h][V - 1]);
       l0[h] = rot_next(cm[h][0]);
     }
+    T first = 0, last = 0; // ragged rows: the cells x = 0 and x = nx-1, broadcast
+    if constexpr (RAG) {
+      first = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cm[0][0]), 0));
+      const T e = kr == 0 ? cm[H - 1][0] : (kr == 1 ? cm[H - 1][1] : (kr == 2 ? cm[H - 1][2] : cm[H - 1][3]));
+      last = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), Lr));
+    }
 #pragma unroll
     for (int h = 0; h < H; ++h) {
-      const T left = lane0 ? r3[(h + H - 1) % H] : r3[h];
+      const T left = lane0 ? (RAG && h == 0 ? last : r3[(h + H - 1) % H]) : r3[h];
       const T right = lane63 ? l0[(h + 1) % H] : l0[h];
       NV vpx, vmx;
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         vpx[k] = k < V - 1 ? cm[h][k + 1] : right;
         vmx[k] = k > 0 ? cm[h][k - 1] : left;
+      }
+      if (RAG && h == H - 1) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) vpx[k] = (lane == Lr && kr == k) ? first : vpx[k];
       }
       o[h] = div6v<T, NV, V>(sum6v<T, KIND>(vpx, vmx, dn[h], up[h], zp[h], zm[h]));
     }
@@ -412,7 +437,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
     auto load_row = [&](int zz, int k) {
       const char *b = planep(zz) + rowoff;
 #pragma unroll
-      for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + h * HS * int(sizeof(T)));
+      for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + choff(h));
     };
     {
       const int zw = z0 - 2 * dz;
@@ -453,10 +478,18 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
 #pragma unroll
           for (int h = 0; h < H; ++h) {
             NV *q = reinterpret_cast<NV *>(dp + h * HS * int(sizeof(T)));
-            if (a.nt)
+            if (RAG && h == H - 1 && !(lane < Lr || (lane == Lr && kr == V - 1))) {
+              if (lane == Lr) { // the partial chunk: cells x .. nx-1
+                T *qs = reinterpret_cast<T *>(q);
+#pragma unroll
+                for (int k = 0; k < V - 1; ++k)
+                  if (k <= kr) qs[k] = o[h][k];
+              }
+            } else if (a.nt) {
               __builtin_nontemporal_store(o[h], q);
-            else
+            } else {
               *q = o[h];
+            }
           }
         }
       }
@@ -929,10 +962,14 @@ bool stencil7x2_supported(const LocalDomain &dom, int64_t qi) {
   return aligned && lox - 2 + dom.pad_x(qi) >= 0 && lox + nchunks * V + 1 < p.x - dom.pad_x(qi);
 }
 
-int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi) {
+int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi, int x2row) {
   if (!stencil7x2_supported(dom, qi)) return 0;
   const int64_t es = dom.elem_size(qi), V = 16 / es;
   const int64_t lox = dom.radius().x(-1), nx = dom.size().x, px = dom.pitch(qi).x, pad = dom.pad_x(qi);
+  // ragged fp32 rows of 257-768 cells: the whole-row kernel wraps x by broadcasting the row-end cells (its last
+  // chunk reads at most 3 cells past the row end, inside the padded row)
+  const bool rowX = x2row != 0 && es == 4 && nx > 256 && nx <= 768 && lox + (nx + V - 1) / V * V < px - pad;
+  if (rowX && nx % V != 0) return 1 | (dom.size().y >= 2 ? 2 : 0) | (dom.size().z >= 2 ? 4 : 0);
   // x: whole chunks only (the chunk grid starts at the 16-B aligned lox), at least two, and the last chunk not on
   // lane 0 of its column (a wrap lane shifts both of its edge pairs: its other edge must be the unused one, never a
   // column boundary); the unused edge pair of a wrap lane (x-2 .. x+V+1 shifted by +-nx) must stay in the row
@@ -1004,14 +1041,17 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   HIP_CHECK(hipGetLastError());
 }
 
-// whole-row kernel: fp32, x wrapped in-kernel, 512 interior cells per row starting on a 16-B chunk
-template <int KIND, int PF>
+// whole-row kernel: fp32, x wrapped in-kernel, rows starting on a 16-B chunk; H chunks per lane (RAG: rows shorter
+// than 256 H cells)
+template <int KIND, int PF, int H = 2, bool RAG = false, int NW = 12>
 static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
                           const StencilTune &tune) {
-  constexpr int NW = 12, YO = NW - 4;
+  constexpr int YO = NW - 4;
   StencilArgs<float> a = make_args<float>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   const int rxm = int(dom.radius().x(-1));
-  if (!(tune.wrap & 1) || a.hix - a.lox != 512 || (a.lox - rxm) % 4 != 0) return false;
+  const int nx = a.hix - a.lox;
+  const bool fitsH = RAG ? (nx > 256 * (H - 1) && nx <= 256 * H) : nx == 512;
+  if (!(tune.wrap & 1) || !fitsH || (a.lox - rxm) % 4 != 0) return false;
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
   a.wrapm = tune.wrap;
@@ -1021,7 +1061,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = 1;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = (const void *)stencil7x2_row_kernel<NW, PF, KIND>;
+  const void *kern = (const void *)stencil7x2_row_kernel<NW, PF, KIND, H, RAG>;
   const int64_t cols = a.gy;
   const int64_t resident = x2_resident_blocks(kern, 64 * NW);
   uint32_t blocks;
@@ -1042,7 +1082,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     blocks = uint32_t(cols * a.gz);
   }
   dom.set_device();
-  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG>), dim3(blocks), dim3(64, NW), 0, stream, a);
   HIP_CHECK(hipGetLastError());
   return true;
 }
@@ -1122,9 +1162,22 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
                      : (pf == 2 ? apply_x2row_t<1, 2>(dom, qi, region, sph, stream, tune)
                                 : apply_x2row_t<1, 3>(dom, qi, region, sph, stream, tune));
     if (done) return;
-    // x a whole number of 512-cell columns from a 16-B aligned first cell: the 512-cell column kernel
     const Rect3 rr(region.lo - dom.accessor_origin(), region.hi - dom.accessor_origin());
     const int64_t nx = rr.hi.x - rr.lo.x;
+    // ragged periodic rows (x wrapped, 256 < nx <= 768 but not 512): H = 2 / 3 chunks per lane, first / last cell
+    // broadcast for the wrap (one plane of lookahead: the 3-chunk window leaves no registers for more). Four chunks
+    // per lane (rows of 769-1024) need 10-wave blocks for the LDS and spill at their 168-VGPR budget: 358 vs 668
+    // Gcells/s for the column kernel at 813x407x407 (profiles/r2/r2_ragged_shapes.log), so not instantiated.
+    if ((tune.wrap & 1) && nx > 256 && nx <= 768) {
+      if (nx <= 512)
+        done = jac ? apply_x2row_t<0, 1, 2, true>(dom, qi, region, sph, stream, tune)
+                   : apply_x2row_t<1, 1, 2, true>(dom, qi, region, sph, stream, tune);
+      else
+        done = jac ? apply_x2row_t<0, 1, 3, true>(dom, qi, region, sph, stream, tune)
+                   : apply_x2row_t<1, 1, 3, true>(dom, qi, region, sph, stream, tune);
+      if (done) return;
+    }
+    // x a whole number of 512-cell columns from a 16-B aligned first cell: the 512-cell column kernel
     if (nx % 512 == 0 && (rr.lo.x - dom.radius().x(-1)) % 4 == 0) {
       // one plane of lookahead (two would spill the Jacobi instance; the row kernel shows no difference)
       jac ? apply_x2col2_wrap<0, 1>(dom, qi, region, sph, stream, tune)
@@ -1132,6 +1185,9 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
       return;
     }
   }
+  // the column kernels wrap x only for whole chunks (ragged periodic rows are the whole-row kernel's)
+  STENCIL_REQUIRE(!(tune.wrap & 1) || (stencil7x2_wrappable_axes(dom, qi, 0) & 1),
+                  "in-kernel x wrap of a ragged row needs the whole-row kernel (fp32, x2row, 256 < nx < 1024)");
   // shapes (rows per lane, waves per block, min waves/SIMD): 1x8 keeps everything in registers at 6 waves/SIMD;
   // 2x4 at 3 waves/SIMD; 2x8 at 4 (spills)
   // shape = waves per block (one src row each; NW-4 output rows) x planes of z lookahead

@@ -120,7 +120,7 @@ void StencilModel::init() {
     int w = dd_->self_wrap_axes();
     for (size_t di = 0; di < doms0.size(); ++di) {
       const auto &d = doms0[di];
-      for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7x2_wrappable_axes(d, q);
+      for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7x2_wrappable_axes(d, q, cfg_.tune.x2row);
       // the swept regions must span every wrapped axis (a forced full split cuts all of them)
       const Rect3 c = d.get_compute_region();
       const Rect3 r = overlap_ ? pairInteriors_[di] : c;

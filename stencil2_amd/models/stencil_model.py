@@ -44,8 +44,8 @@ class StencilModel:
             cfg.backend = backend
         if tune is not None:
             cfg.tune = tune
-        if axis_cost is not None:  # NodeAware cut costs per axis (default (4, 2, 3): x faces are strided;
-            # y cuts before z cuts keep long z columns)
+        if axis_cost is not None:  # NodeAware cut costs per axis (default (4, 3, 2): x faces are strided and
+            # whole periodic rows feed the whole-row kernels; z cuts before y cuts)
             cfg.axis_cost = _C.Dim3(*axis_cost)
         self.config = cfg
         self._m = _C.StencilModel(cfg, group if group is not None else get_group())

@@ -83,13 +83,15 @@ def scenario_jacobi(backend, methods, size):
     gpus = [0] if backend == st.Backend.Device else [0]
     temporal = int(os.environ.get("MP_TEMPORAL", "1"))
     kind = os.environ.get("MP_KIND", "jacobi")
+    cost = os.environ.get("MP_AXIS_COST")  # NodeAware cut costs, e.g. "4,2,3" (default: the model's)
+    kw = {"axis_cost": tuple(int(v) for v in cost.split(","))} if cost else {}
     if kind == "astaroth":
         from stencil2_amd.ops import astaroth_step_reference as ref
         m = st.AstarothSim(size, quantities=1, gpus=gpus, backend=backend, methods=methods, group=g,
-                           temporal=temporal)
+                           temporal=temporal, **kw)
     else:
         ref = jacobi_step_reference
-        m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g, temporal=temporal)
+        m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g, temporal=temporal, **kw)
     m.init()
     L = m.domain.size()
     if kind == "astaroth":
@@ -118,6 +120,8 @@ def scenario_jacobi(backend, methods, size):
         o, s = d.origin(), d.size()
         got = m.interior(di).cpu()
         bad += int((got != u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x]).sum())
+    if os.environ.get("MP_EXPECT_WRAP") is not None:  # axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
+        bad += int(m.wrap_axes() != int(os.environ["MP_EXPECT_WRAP"]))
     if os.environ.get("MP_EXPECT_OVERLAP") is not None:
         bad += int(m.overlapping() != (os.environ["MP_EXPECT_OVERLAP"] == "1"))
     xb = {k: m.domain.exchange_bytes_for_method(getattr(st.MethodFlags, k))

@@ -210,25 +210,31 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
-@pytest.mark.parametrize("kind,size,gpus", [("jacobi", (512, 120, 116), [0]), ("jacobi", (512, 300, 112), [0, 0]),
-                                            ("astaroth", (512, 36, 28), [0]), ("astaroth", (512, 520, 40), [0, 0, 0, 0])])
-@pytest.mark.parametrize("pf", [1, 2, 3])
-def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf):
-    """Fused pairs on 512-cell periodic rows take the whole-row kernel (one wave per row, x-neighbours by lane
-    rotates, StencilTune.x2row): bitwise equal to single steps, with the hot/cold spheres (Jacobi) inside the grid,
-    and to the column kernel (x2row = 0)."""
+@pytest.mark.parametrize("kind,size,gpus,pf,row", [
+    *[(k, sz, g, pf, 1) for k, sz, g in [("jacobi", (512, 120, 116), [0]), ("jacobi", (512, 300, 112), [0, 0]),
+                                         ("astaroth", (512, 36, 28), [0]), ("astaroth", (512, 520, 40), [0, 0, 0, 0])]
+      for pf in (1, 2, 3)],
+    # ragged periodic rows: 2 / 3 / 4 chunks per lane, the row-end cells broadcast for the wrap
+    ("astaroth", (645, 20, 24), [0], 1, 1), ("astaroth", (301, 24, 20), [0], 1, 1), ("astaroth", (300, 20, 16), [0], 1, 1),
+    ("astaroth", (768, 12, 16), [0], 1, 1), ("astaroth", (646, 520, 12), [0, 0], 1, 1), ("jacobi", (645, 136, 136), [0], 1, 1),
+])
+def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf, row):
+    """Fused pairs on periodic rows of 257-768 cells take the whole-row kernel (one wave per row, x-neighbours by
+    lane rotates, StencilTune.x2row; ragged rows broadcast their end cells): bitwise equal to single steps, with the
+    hot/cold spheres (Jacobi) inside the grid, and to the column kernel (x2row = 0, which copies ragged x halos)."""
     from stencil2_amd.ops import astaroth_step_reference
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
     ms = []
-    for row in (1, 0):
+    for r in (row, 0):
         t = st.StencilTune()
         t.x2pf = pf
-        t.x2row = row
+        t.x2row = r
         ms.append(cls(size, gpus=gpus, temporal=2, tune=t, axis_cost=(4, 2, 3), **kw))  # bench.py's cut: x stays whole
     for m in ms:
         m.init()
-        assert m.temporal_blocking() and m.wrap_axes() & 1
+        assert m.temporal_blocking()
+    assert ms[0].wrap_axes() & 1 and bool(ms[1].wrap_axes() & 1) == (size[0] % 4 == 0)
     u = _gather(ms[0])
     for n in (5, 16):
         for m in ms:
@@ -237,7 +243,7 @@ def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf):
             u = ref(u)
         for m in ms:
             m.synchronize()
-            assert torch.equal(_gather(m), u), f"x2row={1 - ms.index(m)} after run({n})"
+            assert torch.equal(_gather(m), u), f"x2row={(row, 0)[ms.index(m)]} after run({n})"
 
 
 @pytest.mark.parametrize("kind,size,gpus,fp64", [("jacobi", (512, 120, 116), [0], False),
@@ -508,14 +514,17 @@ def test_colocated_ipc_jacobi_two_ranks(temporal, ranks):
         assert rc == 0, out[-3000:]
 
 
-@pytest.mark.parametrize("size", ["512,264,16", "1024,520,12"])  # the model cuts y (cost 4,2,3)
-def test_colocated_ipc_wide_rows_two_ranks(size):
-    """The whole-row (512) and 512-cell column (1024) fused-pair kernels in the overlapped multi-rank step: y is cut
-    between two ranks sharing one GPU (HIP IPC), x stays whole and wrapped in-kernel; S o S of the local interior
-    runs while the remote y halos are in flight (Astaroth proxy from an analytic field, bitwise vs the oracle)."""
+@pytest.mark.parametrize("size,cost", [("512,264,16", "4,2,3"), ("1024,520,12", "4,2,3"), ("645,520,12", "4,2,3"),
+                                       ("512,16,300", "4,3,2"), ("645,12,520", "4,3,2")])  # y cut / z cut
+def test_colocated_ipc_wide_rows_two_ranks(size, cost):
+    """The whole-row (512, ragged 645) and 512-cell column (1024) fused-pair kernels in the overlapped multi-rank
+    step: y (cost 4,2,3) or z (the default 4,3,2) is cut between two ranks sharing one GPU (HIP IPC), x stays whole
+    and wrapped in-kernel (also in the exterior slabs); S o S of the local interior runs while the remote halos are
+    in flight (Astaroth proxy from an analytic field, bitwise vs the oracle)."""
     outs = run_ranks(2, WORKER, ["jacobi", size],
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
-                                "MP_TEMPORAL": "2", "MP_KIND": "astaroth", "MP_EXPECT_OVERLAP": "1"})
+                                "MP_TEMPORAL": "2", "MP_KIND": "astaroth", "MP_EXPECT_OVERLAP": "1",
+                                "MP_AXIS_COST": cost, "MP_EXPECT_WRAP": "5" if cost == "4,2,3" else "3"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out

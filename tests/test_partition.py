@@ -50,8 +50,13 @@ def test_node_partition_min_interface(st):
     assert st.NodePartition(D(1024, 1024, 1024), r, 1, 8, c).dim() == D(1, 2, 4)
     assert st.NodePartition(D(813, 813, 813), r, 1, 4, c).dim() == D(1, 2, 2)
     assert st.NodePartition(D(645, 645, 645), r, 1, 2, c).dim() == D(1, 1, 2)
-    # the models' default (4, 2, 3): equal face area, but y cuts preferred, so sub-domains keep long z columns
-    # (fewer warm-up planes per fused-pair segment: 1024x256x512 885 vs 1024x512x256 708-767 Gcells/s on one GPU)
+    # the models' default (4, 3, 2): equal face area, z cuts preferred (contiguous faces; the whole-row sweeps are
+    # faster with long y: 1024x512x256 1000 vs 1024x256x512 972, 645x645x323 837 vs 645x323x645 790 Gcells/s)
+    c = D(4, 3, 2)
+    assert st.NodePartition(D(1024, 1024, 1024), r, 1, 8, c).dim() == D(1, 2, 4)
+    assert st.NodePartition(D(813, 813, 813), r, 1, 4, c).dim() == D(1, 2, 2)
+    assert st.NodePartition(D(645, 645, 645), r, 1, 2, c).dim() == D(1, 1, 2)
+    # the round-1 default (4, 2, 3): y cuts preferred
     c = D(4, 2, 3)
     assert st.NodePartition(D(1024, 1024, 1024), r, 1, 8, c).dim() == D(1, 4, 2)
     assert st.NodePartition(D(813, 813, 813), r, 1, 4, c).dim() == D(1, 2, 2)
