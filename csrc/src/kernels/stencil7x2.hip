@@ -980,10 +980,11 @@ int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi, int x2row) {
 }
 
 // along wrapped axes the region must be the whole compute region (the kernels wrap at its faces)
-static void check_wrap(const LocalDomain &dom, int64_t qi, const Rect3 &region, int wrap) {
+static void check_wrap(const LocalDomain &dom, int64_t qi, const Rect3 &region, int wrap, int x2row) {
   if (wrap == 0) return;
-  STENCIL_REQUIRE((wrap & ~stencil7x2_wrappable_axes(dom, qi)) == 0,
-                  "in-kernel wrap " << wrap << " not supported by this layout (" << stencil7x2_wrappable_axes(dom, qi) << ")");
+  STENCIL_REQUIRE((wrap & ~stencil7x2_wrappable_axes(dom, qi, x2row)) == 0,
+                  "in-kernel wrap " << wrap << " not supported by this layout ("
+                                    << stencil7x2_wrappable_axes(dom, qi, x2row) << ")");
   const Rect3 cr = dom.get_compute_region();
   const int64_t lo[3] = {region.lo.x, region.lo.y, region.lo.z}, hi[3] = {region.hi.x, region.hi.y, region.hi.z};
   const int64_t clo[3] = {cr.lo.x, cr.lo.y, cr.lo.z}, chi[3] = {cr.hi.x, cr.hi.y, cr.hi.z};
@@ -1147,7 +1148,7 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   const Rect3 cr = dom.get_compute_region();
   STENCIL_REQUIRE(cr.contains(region.lo) && region.hi.x <= cr.hi.x && region.hi.y <= cr.hi.y && region.hi.z <= cr.hi.z,
                   "stencil region " << region << " outside compute region " << cr);
-  check_wrap(dom, qi, region, tune.wrap);
+  check_wrap(dom, qi, region, tune.wrap, tune.x2row);
   const bool f32 = dom.elem_size(qi) == 4;
   const bool jac = kind == StencilKind::Jacobi;
   if (f32 && tune.x2row) { // whole rows of 512 cells in one wave (x wrapped in-kernel)
@@ -1167,7 +1168,8 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
     // ragged periodic rows (x wrapped, 256 < nx <= 768 but not 512): H = 2 / 3 chunks per lane, first / last cell
     // broadcast for the wrap (one plane of lookahead: the 3-chunk window leaves no registers for more). Four chunks
     // per lane (rows of 769-1024) need 10-wave blocks for the LDS and spill at their 168-VGPR budget: 358 vs 668
-    // Gcells/s for the column kernel at 813x407x407 (profiles/r2/r2_ragged_shapes.log), so not instantiated.
+    // Gcells/s for the column kernel at 813x407x407 (profiles/r2/r2_ragged_shapes.log); 8-wave blocks (2 waves per
+    // SIMD, 200 VGPRs, 4 output rows of 8) 597 vs 668 (r2_ragged_h4_8waves.log). Not instantiated.
     if ((tune.wrap & 1) && nx > 256 && nx <= 768) {
       if (nx <= 512)
         done = jac ? apply_x2row_t<0, 1, 2, true>(dom, qi, region, sph, stream, tune)
@@ -1263,7 +1265,7 @@ void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vec
   if (rs.empty()) return;
   dom.set_device();
   const bool f32 = dom.elem_size(qi) == 4;
-  STENCIL_REQUIRE((wrap & ~stencil7x2_wrappable_axes(dom, qi)) == 0, "in-kernel wrap " << wrap << " not supported");
+  STENCIL_REQUIRE((wrap & ~7) == 0, "in-kernel wrap mask " << wrap);  // wrap_coord: any extent
   if (f32)
     kind == StencilKind::Jacobi ? apply_x2_regions_t<float, 0>(dom, qi, rs, sph, stream, wrap)
                                 : apply_x2_regions_t<float, 1>(dom, qi, rs, sph, stream, wrap);
@@ -1337,7 +1339,7 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
   STENCIL_REQUIRE(c.contains(in.lo) && in.hi.x <= c.hi.x && in.hi.y <= c.hi.y && in.hi.z <= c.hi.z,
                   "interior " << in << " outside compute region " << c);
   // a wrapped axis is never cut by the interior: no slab is thin along it (x slabs load unwrapped row windows)
-  check_wrap(dom, qi, in, tune.wrap);
+  check_wrap(dom, qi, in, tune.wrap, tune.x2row);
   const Dim3 lo = in.lo - c.lo, hi = c.hi - in.hi;
   if (std::max({lo.x, lo.y, lo.z, hi.x, hi.y, hi.z}) > 4) {
     // thick shells: the thread-per-cell kernel
