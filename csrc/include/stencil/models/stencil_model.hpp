@@ -83,6 +83,7 @@ public:
   int64_t steps_done() const { return steps_; }
   const Spheres &spheres() const { return sph_; }
   bool overlapping() const { return overlap_; }
+  bool local_interior_steps() const { return localSteps_; } // overlapped single steps on get_local_interior
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }
   int wrap_axes() const { return pairTune_.wrap; } // axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
@@ -103,6 +104,9 @@ private:
   bool pairs_ = false; // temporal blocking active
   StencilTune pairTune_; // cfg_.tune + the in-kernel wrap axes of the fused pairs
   StencilTune stepTune_; // cfg_.tune + the in-kernel wrap axes of single steps
+  bool localSteps_ = false;                      // overlapped single steps on the local interior (see init)
+  std::vector<Rect3> stepInteriors_;             // get_local_interior(1)
+  std::vector<std::vector<Rect3>> stepExteriors_; // the slabs at remote faces
   std::vector<std::vector<std::unique_ptr<HaloForwarder>>> fwd_; // [domain][quantity]
   std::vector<Event> stepDone_;                                    // forwarding with several sub-domains
   hipGraphExec_t graphExec_[2] = {nullptr, nullptr};

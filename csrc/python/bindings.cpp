@@ -610,6 +610,7 @@ PYBIND11_MODULE(_C, m) {
       .def("local_cells", &StencilModel::local_cells)
       .def("steps_done", &StencilModel::steps_done)
       .def("overlapping", &StencilModel::overlapping)
+      .def("local_interior_steps", &StencilModel::local_interior_steps)
       .def("forwarding", &StencilModel::forwarding)
       .def("temporal_blocking", &StencilModel::temporal_blocking)
       .def("wrap_axes", &StencilModel::wrap_axes)

@@ -622,6 +622,8 @@ __global__ __launch_bounds__(256) void stencil7_generic_kernel(StencilArgs<T> a)
 //     (centre, y+-1, z+-1) + 2 edge scalars per lane.
 //   COL slabs (thin in x, i.e. x faces): one wave = 64 consecutive y of one (x, z); lanes along y, so y-neighbours
 //     come from adjacent lanes and each lane touches its own row line once (x+-1 share it).
+// a.wrapm: along those axes neighbours beyond a face are read at their periodic image (StencilTune::wrap; x only
+// for whole 16-B chunks from the face, stencil7_wrappable_axes).
 constexpr int kMaxShell = 8;
 struct ShellTable {
   int lo[kMaxShell][3];
@@ -673,6 +675,14 @@ __global__ __launch_bounds__(256) void stencil7_shell_kernel(StencilArgs<T> a, S
   const int lane = threadIdx.x;
   const int lx = st.lo[k][0], ly = st.lo[k][1], lz = st.lo[k][2];
   const int ex = st.ext[k][0], ey = st.ext[k][1];
+  auto wrapc = [&](int c, int ax) { // one conditional shift (the neighbour of a face cell)
+    if ((a.wrapm >> ax) & 1) {
+      c += c < a.wlo[ax] ? a.wn[ax] : 0;
+      c -= c >= a.wlo[ax] + a.wn[ax] ? a.wn[ax] : 0;
+    }
+    return c;
+  };
+  auto at = [&](int x, int y, int z) { return a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + x; };
   if (!st.col[k]) {
     // ROW: wl -> (chunk wave cw, y, z)
     const int cws = (st.nch[k] + 63) / 64;
@@ -683,15 +693,16 @@ __global__ __launch_bounds__(256) void stencil7_shell_kernel(StencilArgs<T> a, S
     const int c = cw * 64 + lane;
     const bool valid = c < st.nch[k];
     const int xb = st.x0[k] + (valid ? c : st.nch[k] - 1) * V;
-    const T *p = a.src + int64_t(z) * a.pxy + int64_t(y) * a.px + xb;
+    const T *p = at(xb, y, z);
     const VT cc = *reinterpret_cast<const VT *>(p);
-    const VT yp = *reinterpret_cast<const VT *>(p + a.px);
-    const VT ym = *reinterpret_cast<const VT *>(p - a.px);
-    const VT zp = *reinterpret_cast<const VT *>(p + a.pxy);
-    const VT zm = *reinterpret_cast<const VT *>(p - a.pxy);
+    const VT yp = *reinterpret_cast<const VT *>(at(xb, wrapc(y + 1, 1), z));
+    const VT ym = *reinterpret_cast<const VT *>(at(xb, wrapc(y - 1, 1), z));
+    const VT zp = *reinterpret_cast<const VT *>(at(xb, y, wrapc(z + 1, 2)));
+    const VT zm = *reinterpret_cast<const VT *>(at(xb, y, wrapc(z - 1, 2)));
     const bool eL = lane == 0, eR = lane == 63 || c + 1 >= st.nch[k];
-    const T le = eL ? p[-1] : T(0);
-    const T re = eR ? p[V] : T(0);
+    const bool xw = (a.wrapm & 1) != 0;
+    const T le = eL ? p[-1 + (xw && xb == a.wlo[0] ? a.wn[0] : 0)] : T(0);
+    const T re = eR ? p[V - (xw && xb + V == a.wlo[0] + a.wn[0] ? a.wn[0] : 0)] : T(0);
     const T sl = shfl_up1<T>(vget<T>(cc, V - 1));
     const T sr = shfl_down1<T>(vget<T>(cc, 0));
     const T left = eL ? le : sl, right = eR ? re : sr;
@@ -715,11 +726,12 @@ __global__ __launch_bounds__(256) void stencil7_shell_kernel(StencilArgs<T> a, S
     const int y = ly + yb * 64 + lane;
     const bool valid = y < ly + ey;
     const int yl = valid ? y : ly + ey - 1;
-    const T *p = a.src + int64_t(z) * a.pxy + int64_t(yl) * a.px + x;
-    const T c0 = p[0], vpx = p[1], vmx = p[-1], vpz = p[a.pxy], vmz = p[-a.pxy];
+    const T *p = at(x, yl, z);
+    const T c0 = p[0], vpx = *at(wrapc(x + 1, 0), yl, z), vmx = *at(wrapc(x - 1, 0), yl, z);
+    const T vpz = *at(x, yl, wrapc(z + 1, 2)), vmz = *at(x, yl, wrapc(z - 1, 2));
     const bool eL = lane == 0, eR = lane == 63 || !(y + 1 < ly + ey);
-    const T ue = eL ? p[-a.px] : T(0);
-    const T de = eR ? p[a.px] : T(0);
+    const T ue = eL ? *at(x, wrapc(yl - 1, 1), z) : T(0);
+    const T de = eR ? *at(x, wrapc(yl + 1, 1), z) : T(0);
     const T su = shfl_up1<T>(c0);   // value of y-1
     const T sd = shfl_down1<T>(c0); // value of y+1
     const T vmy = eL ? ue : su, vpy = eR ? de : sd;
@@ -834,7 +846,13 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
                        : tune.variant == 3 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 3>
                        : tune.variant == 4 ? (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false, 4>
                                            : (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false>;
-    const int64_t targetBlocks = resident_blocks(kern, 64 * NW);
+    int64_t targetBlocks = resident_blocks(kern, 64 * NW);
+    if (tune.reserveCUs > 0) { // leave that many CUs to the comm stream's kernels (overlapped steps)
+      int cus = 256;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
+      const int64_t perCU = std::max<int64_t>(1, targetBlocks / std::max(1, cus));
+      targetBlocks = std::max<int64_t>(perCU, targetBlocks - perCU * std::min(tune.reserveCUs, cus / 2));
+    }
     const int64_t nzc = std::max<int64_t>(1, targetBlocks / cols);
     zc = int(std::max<int64_t>(16, (nz + nzc - 1) / nzc));
   }
@@ -999,10 +1017,11 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
 
 template <typename T, int KIND>
 static void apply_regions_t(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, const Spheres &sph,
-                            hipStream_t stream) {
+                            hipStream_t stream, int wrap) {
   constexpr int V = Vec16<T>::N;
   StencilArgs<T> a = make_args<T>(dom, qi, dom.get_compute_region(), KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth,
                                   sph);
+  a.wrapm = wrap;
   const Dim3 org = dom.accessor_origin();
   const int rxm = int(dom.radius().x(-1));
   const bool aligned = (reinterpret_cast<uintptr_t>(a.src + rxm) % 16 == 0) &&
@@ -1010,6 +1029,8 @@ static void apply_regions_t(const LocalDomain &dom, int64_t qi, const std::vecto
   std::vector<Rect3> rs;
   for (const auto &r : regions)
     if (!r.empty()) rs.push_back(Rect3(r.lo - org, r.hi - org));
+  STENCIL_REQUIRE(wrap == 0 || (aligned && std::getenv("STENCIL_GENERIC_EXTERIOR") == nullptr),
+                  "in-kernel wrap of exterior slabs needs the aligned layout");
   if (aligned && std::getenv("STENCIL_GENERIC_EXTERIOR") == nullptr) {
     for (size_t k0 = 0; k0 < rs.size(); k0 += kMaxShell) {
       ShellTable st{};
@@ -1069,9 +1090,12 @@ static void apply_regions_t(const LocalDomain &dom, int64_t qi, const std::vecto
 void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
                             const Spheres &sph, hipStream_t stream, const StencilTune &tune) {
   if (dom.backend() == Backend::Host || std::getenv("STENCIL_EXTERIOR_PER_REGION")) {
+    STENCIL_REQUIRE(tune.wrap == 0 || dom.backend() == Backend::Device, "in-kernel wrap needs a device sub-domain");
     for (const auto &r : regions) stencil7_apply(dom, qi, r, kind, sph, stream, tune);
     return;
   }
+  STENCIL_REQUIRE((tune.wrap & ~stencil7_wrappable_axes(dom, qi)) == 0,
+                  "in-kernel wrap " << tune.wrap << " not supported by this layout");
   for (const auto &r : regions) {
     const Rect3 cr = dom.get_compute_region();
     STENCIL_REQUIRE(r.empty() || (cr.contains(r.lo) && r.hi.x <= cr.hi.x && r.hi.y <= cr.hi.y && r.hi.z <= cr.hi.z),
@@ -1080,11 +1104,11 @@ void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vecto
   dom.set_device();
   const bool f64 = dom.elem_size(qi) == 8;
   if (!f64)
-    kind == StencilKind::Jacobi ? apply_regions_t<float, 0>(dom, qi, regions, sph, stream)
-                                : apply_regions_t<float, 1>(dom, qi, regions, sph, stream);
+    kind == StencilKind::Jacobi ? apply_regions_t<float, 0>(dom, qi, regions, sph, stream, tune.wrap)
+                                : apply_regions_t<float, 1>(dom, qi, regions, sph, stream, tune.wrap);
   else
-    kind == StencilKind::Jacobi ? apply_regions_t<double, 0>(dom, qi, regions, sph, stream)
-                                : apply_regions_t<double, 1>(dom, qi, regions, sph, stream);
+    kind == StencilKind::Jacobi ? apply_regions_t<double, 0>(dom, qi, regions, sph, stream, tune.wrap)
+                                : apply_regions_t<double, 1>(dom, qi, regions, sph, stream, tune.wrap);
 }
 
 // ---------------------------------------------------------------------------------------------------------

@@ -132,17 +132,56 @@ void StencilModel::init() {
     pairTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
-  // single steps (whole compute region, no overlap / forwarding): the self-periodic axes are read in-kernel at their
-  // periodic image and their same-GPU copies leave the exchange (a fully periodic sub-domain exchanges nothing; one
-  // MI355X at 512^3: the ~25 us copy-plan kernel of a ~225 us step)
+  // single steps: the self-periodic axes are read in-kernel at their periodic image and their same-GPU copies leave
+  // the exchange (a fully periodic sub-domain exchanges nothing; one MI355X at 512^3: the ~25 us copy-plan kernel of
+  // a ~225 us step). Overlapped, as for the fused pairs: the same-GPU translate first, the interior shrunk only at
+  // faces whose halo arrives from another GPU (get_local_interior) during the remote transfers, the slabs at those
+  // faces after them, and the sweep leaves x2reserve CUs to the transports' kernels.
   stepTune_ = cfg_.tune;
   stepTune_.wrap = 0;
-  if (!pairs_ && !forward_ && !overlap_ && cfg_.wrapSelf && cfg_.tune.variant != StencilTune::kMfma &&
-      !doms0.empty() && std::getenv("STENCIL_NO_WRAP") == nullptr) {
+  localSteps_ = false;
+  const bool stepDevice = !doms0.empty() && doms0[0].backend() == Backend::Device;
+  if (!pairs_ && !forward_ && overlap_ && stepDevice && cfg_.wrapSelf && cfg_.tune.variant != StencilTune::kMfma &&
+      std::getenv("STENCIL_NO_LOCAL_INTERIOR") == nullptr) {
+    const auto li = dd_->get_local_interior(1);
+    bool remote = false, ok = true;
+    for (size_t di = 0; di < doms0.size(); ++di) {
+      const Rect3 c = doms0[di].get_compute_region();
+      remote = remote || !(li[di].lo == c.lo && li[di].hi == c.hi);
+      ok = ok && !li[di].empty();
+    }
+    if (remote && ok) {
+      localSteps_ = true;
+      stepInteriors_ = li;
+      stepExteriors_.assign(doms0.size(), {});
+      for (size_t di = 0; di < doms0.size(); ++di) {
+        const Rect3 c = doms0[di].get_compute_region(), in = li[di];
+        for (const Rect3 &r : {Rect3(c.lo, Dim3(c.hi.x, c.hi.y, in.lo.z)), Rect3(Dim3(c.lo.x, c.lo.y, in.hi.z), c.hi),
+                               Rect3(Dim3(c.lo.x, c.lo.y, in.lo.z), Dim3(c.hi.x, in.lo.y, in.hi.z)),
+                               Rect3(Dim3(c.lo.x, in.hi.y, in.lo.z), Dim3(c.hi.x, c.hi.y, in.hi.z)),
+                               Rect3(Dim3(c.lo.x, in.lo.y, in.lo.z), Dim3(in.lo.x, in.hi.y, in.hi.z)),
+                               Rect3(Dim3(in.hi.x, in.lo.y, in.lo.z), Dim3(c.hi.x, in.hi.y, in.hi.z))})
+          if (!r.empty()) stepExteriors_[di].push_back(r);
+      }
+      dd_->set_comm_max_blocks(cfg_.tune.x2reserve);
+    } else if (!remote && cfg_.autoOverlap) {
+      overlap_ = false; // every halo from this GPU: exchange -> whole-region step
+    }
+  }
+  if (!pairs_ && !forward_ && (!overlap_ || localSteps_) && stepDevice && cfg_.wrapSelf &&
+      cfg_.tune.variant != StencilTune::kMfma && std::getenv("STENCIL_NO_WRAP") == nullptr) {
     int w = dd_->self_wrap_axes();
     if (const char *e = std::getenv("STENCIL_WRAP_AXES")) w &= std::atoi(e);
-    for (const auto &d : doms0)
+    for (size_t di = 0; di < doms0.size(); ++di) {
+      const auto &d = doms0[di];
       for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7_wrappable_axes(d, q);
+      // the swept regions must span every wrapped axis
+      const Rect3 c = d.get_compute_region();
+      const Rect3 r = localSteps_ ? stepInteriors_[di] : c;
+      if (r.lo.x != c.lo.x || r.hi.x != c.hi.x) w &= ~1;
+      if (r.lo.y != c.lo.y || r.hi.y != c.hi.y) w &= ~2;
+      if (r.lo.z != c.lo.z || r.hi.z != c.hi.z) w &= ~4;
+    }
     stepTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
@@ -322,6 +361,25 @@ void StencilModel::enqueue_step(int k) {
     }
     if (multi)
       for (size_t di = 0; di < doms.size(); ++di) stepDone_[di].record(compute_[di]);
+    return;
+  }
+  if (localSteps_) {
+    // single step, overlapped against the remote part of the exchange only (see init)
+    dd_->exchange_async(nullptr, stepTune_.wrap);
+    StencilTune ti = stepTune_;
+    ti.reserveCUs = cfg_.tune.x2reserve;
+    for (size_t di = 0; di < doms.size(); ++di) {
+      dd_->wait_translated(di, compute_[di]);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7_apply(doms[di], q, stepInteriors_[di], cfg_.kind, sph_, compute_[di].get(), ti);
+    }
+    for (size_t di = 0; di < doms.size(); ++di) {
+      hipStream_t s = dd_->comm_stream(di);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        stencil7_apply_regions(doms[di], q, stepExteriors_[di], cfg_.kind, sph_, s, stepTune_);
+      exteriorDone_[di].record(s);
+      exteriorDone_[di].wait_on(compute_[di]);
+    }
     return;
   }
   if (overlap_) {

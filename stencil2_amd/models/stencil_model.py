@@ -76,6 +76,11 @@ class StencilModel:
     def overlapping(self) -> bool:
         return self._m.overlapping()
 
+    def local_interior_steps(self) -> bool:
+        """True when overlapped single steps sweep the local interior (shrunk only at remote faces) during the
+        remote transfers and wrap the self-periodic axes in-kernel."""
+        return self._m.local_interior_steps()
+
     def temporal_blocking(self) -> bool:
         """True when run() advances in fused pairs of steps (stencil7x2, one depth-2 exchange per pair)."""
         return self._m.temporal_blocking()

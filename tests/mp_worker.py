@@ -122,6 +122,9 @@ def scenario_jacobi(backend, methods, size):
         bad += int((got != u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x]).sum())
     if os.environ.get("MP_EXPECT_WRAP") is not None:  # axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
         bad += int(m.wrap_axes() != int(os.environ["MP_EXPECT_WRAP"]))
+    if os.environ.get("MP_EXPECT_STEP_WRAP") is not None:  # single steps: in-kernel wrap axes, local interior
+        bad += int(m.step_wrap_axes() != int(os.environ["MP_EXPECT_STEP_WRAP"]))
+        bad += int(not m.local_interior_steps())
     if os.environ.get("MP_EXPECT_OVERLAP") is not None:
         bad += int(m.overlapping() != (os.environ["MP_EXPECT_OVERLAP"] == "1"))
     xb = {k: m.domain.exchange_bytes_for_method(getattr(st.MethodFlags, k))

@@ -530,6 +530,24 @@ def test_colocated_ipc_wide_rows_two_ranks(size, cost):
         assert "jacobi bad 0" in out
 
 
+@pytest.mark.parametrize("kind,size,cost", [("astaroth", "512,16,300", "4,3,2"), ("jacobi", "96,80,36", "4,2,3"),
+                                            ("astaroth", "645,12,520", "4,3,2")])
+def test_colocated_single_steps_local_interior(kind, size, cost):
+    """Overlapped single steps across two ranks sharing one GPU (HIP IPC): the interior is shrunk only at the remote
+    faces (get_local_interior) and swept during the transfer, the self-periodic axes are wrapped in-kernel and left
+    out of the exchange, the slabs at the remote faces follow (shell kernel with wrap). Bitwise vs the oracle."""
+    expect = "3" if cost == "4,3,2" else "5"
+    if size.startswith("645"):
+        expect = "2"  # ragged x: single steps copy the x faces (whole 16-B chunks only)
+    outs = run_ranks(2, WORKER, ["jacobi", size],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": "1", "MP_KIND": kind, "MP_EXPECT_OVERLAP": "1",
+                                "MP_AXIS_COST": cost, "MP_EXPECT_STEP_WRAP": expect})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out
+
+
 def test_ipc_probe_failure_falls_back_on_shared_gpu():
     """Co-located ranks on one GPU whose IPC pre-flight fails (forced) must not pick RCCL (it refuses two ranks on
     one device): the runtime drops Colocated and Rccl and stages through the host; results stay exact."""
