@@ -12,6 +12,7 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_BRANCH"; do
   i=$((i+1))
   case $SETS in *$i*) ;; *) continue ;; esac
-  timeout -s KILL 90 rocprofv3 --pmc $set -d $D/p$i -o pmc --output-format csv -- python3 bench.py --steps 4 --warmup 0 --exchange-iters 1 $BENCH_ARGS > $D/p$i.log 2>&1 || { echo "pmc $i rc=$?"; tail -5 $D/p$i.log; exit 1; }
+  # PMC_CMD: the program to count (default: bench.py, 4 steps)
+  timeout -s KILL 90 rocprofv3 --pmc $set -d $D/p$i -o pmc --output-format csv -- ${PMC_CMD:-python3 bench.py --steps 4 --warmup 0 --exchange-iters 1 $BENCH_ARGS} > $D/p$i.log 2>&1 || { echo "pmc $i rc=$?"; tail -5 $D/p$i.log; exit 1; }
 done
 python3 scripts/mi355x/summarize_pmc.py $D | tee $D/summary.txt

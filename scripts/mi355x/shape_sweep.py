@@ -14,13 +14,19 @@ ap.add_argument("--steps", type=int, default=32)
 ap.add_argument("--shapes", default="512x512x512,645x323x645,813x407x407,1024x256x512")
 ap.add_argument("--x2sched", default="1")
 ap.add_argument("--x2row", default="1,0", help="whole-row kernel on/off (StencilTune.x2row)")
+ap.add_argument("--x2xfast", default="0", help="fused-pair column order: 1 x-major, 0 y-major (list)")
+ap.add_argument("--x2pf", default="3", help="fused-pair planes of lookahead (list)")
 args = ap.parse_args()
-for sched, row in ((int(a), int(b)) for a in args.x2sched.split(",") for b in args.x2row.split(",")):
+for sched, row, xf, pf in ((int(a), int(b), int(c), int(d)) for a in args.x2sched.split(",")
+                           for b in args.x2row.split(",") for c in args.x2xfast.split(",")
+                           for d in args.x2pf.split(",")):
     for sh in args.shapes.split(","):
         L = tuple(int(v) for v in sh.split("x"))
         t = st.StencilTune()
         t.x2sched = sched
         t.x2row = row
+        t.x2xfast = xf
+        t.x2pf = pf
         m = st.Jacobi3D(L, gpus=[0], temporal=2, tune=t)
         m.init()
         m.run(8)
@@ -30,7 +36,7 @@ for sched, row in ((int(a), int(b)) for a in args.x2sched.split(",") for b in ar
         m.synchronize()
         dt = time.perf_counter() - t0
         cells = L[0] * L[1] * L[2]
-        print(json.dumps({"shape": sh, "x2sched": sched, "x2row": row, "us_per_step": round(dt / args.steps * 1e6, 1),
+        print(json.dumps({"shape": sh, "x2sched": sched, "x2row": row, "x2xfast": xf, "x2pf": pf, "us_per_step": round(dt / args.steps * 1e6, 1),
                           "gcells": round(cells * args.steps / dt / 1e9, 1)}), flush=True)
         del m
         torch.cuda.empty_cache()
