@@ -20,6 +20,28 @@ import sys
 import time
 
 
+def weak_grid(st, per_gpu: int, n: int, rule: str, axis_cost) -> tuple:
+    """Global grid of the weak-scaling run on n GPUs.
+
+    cbrt: the reference's cube of side per_gpu * n^(1/3) (bin/jacobi3d.cu:167-169).
+    exact: the same NodeAware decomposition of that cube (e.g. 1x1x2 / 1x2x2 / 1x2x4 for n = 2 / 4 / 8 with the
+    default cut costs), but every sub-domain exactly per_gpu^3, so per-GPU work is the N=1 work to the cell.
+    """
+    L = st.models.weak_scaled_size(per_gpu, n)
+    if rule == "cbrt" or n == 1:
+        return (L, L, L)
+    r = st.Radius.constant(0)
+    r.set_face(1)
+    cost = st.Dim3(*axis_cost)
+    d = st.NodePartition(st.Dim3(L, L, L), r, 1, n, cost).dim()
+    grid = (per_gpu * d.x, per_gpu * d.y, per_gpu * d.z)
+    p = st.NodePartition(st.Dim3(*grid), r, 1, n, cost)
+    if p.dim() != d or any(p.subdomain_size(st.Dim3(i, j, k)) != st.Dim3(per_gpu, per_gpu, per_gpu)
+                           for i in range(d.x) for j in range(d.y) for k in range(d.z)):
+        return (L, L, L)  # the partitioner would not cut the scaled grid into equal cubes: the reference rule
+    return grid
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -51,6 +73,10 @@ def main():
                          "of those halos); 0 = copy every halo")
     ap.add_argument("--axis-cost", default="4,3,2",
                     help="NodeAware partition cost per interface cell of x,y,z cuts (1,1,1 = the reference's rule)")
+    ap.add_argument("--grid", choices=["exact", "cbrt"], default="exact",
+                    help="weak-scaling grid: exact = every GPU holds exactly per_gpu^3 cells (global grid = per_gpu x the "
+                         "decomposition of the cbrt-scaled cube); cbrt = the reference's rule, a per_gpu*N^(1/3) cube "
+                         "(bin/jacobi3d.cu:167-169: 645^3 / 813^3 / 1024^3 at N = 2 / 4 / 8, ragged sub-domains)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU)")
     args = ap.parse_args()
@@ -79,6 +105,8 @@ def main():
     pg = st.init_process_group()
     n = world
     L = st.models.weak_scaled_size(args.per_gpu, n)
+    axis_cost = tuple(int(v) for v in args.axis_cost.split(","))
+    grid = weak_grid(st, args.per_gpu, n, args.grid, axis_cost)
     methods = st.MethodFlags.All
     if args.methods != "all":
         methods = st.MethodFlags.None_
@@ -150,9 +178,9 @@ def main():
     tune.x2sched = args.x2sched
     tune.x2xfast = args.x2xfast
     overlap = not args.no_overlap and args.overlap != "off"
-    model = st.Jacobi3D((L, L, L), gpus=[device], methods=methods, overlap=overlap,
+    model = st.Jacobi3D(grid, gpus=[device], methods=methods, overlap=overlap,
                         auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
-                        axis_cost=tuple(int(v) for v in args.axis_cost.split(",")), wrap_self=bool(args.wrap))
+                        axis_cost=axis_cost, wrap_self=bool(args.wrap))
     model.init()
     model.prepare()  # hipGraph capture + instantiation (no steps run) outside the timed region
     model.run(args.warmup)
@@ -169,7 +197,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    cells = L ** 3
+    cells = grid[0] * grid[1] * grid[2]
     gcells = cells * args.steps / elapsed / 1e9
 
     # exchange-only loop on the same decomposition (halo-exchange GB/s, bench_exchange definition)
@@ -206,8 +234,8 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (reference Jacobi3D initial condition: 0.5 + hot/cold spheres)",
-            "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": L,
-                       "grid": [L, L, L], "per_gpu": args.per_gpu, "radius": 1,
+            "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": max(grid),
+                       "grid": list(grid), "grid_rule": args.grid, "per_gpu": args.per_gpu, "radius": 1,
                        "parallelism": f"domain-decomp{n}",
                        "decomposition": "x".join(str(v) for v in (model.domain.placement_dim().x,
                                                                    model.domain.placement_dim().y,

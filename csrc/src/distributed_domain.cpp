@@ -859,6 +859,15 @@ std::vector<Rect3> DistributedDomain::get_local_interior(int reach) const {
       for (int a = 0; a < 3; ++a)
         if (comp(d, a) != 0) sh[a][comp(d, a) > 0] = std::max<int64_t>(sh[a][comp(d, a) > 0], 1);
     }
+    // measurement knob: treat the faces of these axes (mask 1=x, 2=y, 4=z) as remote, so one GPU runs the split
+    // (local interior during the transfers, slabs after) of a multi-GPU decomposition
+    if (const char *e = std::getenv("STENCIL_FAKE_REMOTE_AXES"))
+      for (int a = 0; a < 3; ++a)
+        if (std::atoi(e) >> a & 1)
+          for (int s = 0; s < 2; ++s) {
+            const Dim3 d(a == 0 ? 2 * s - 1 : 0, a == 1 ? 2 * s - 1 : 0, a == 2 ? 2 * s - 1 : 0);
+            sh[a][s] = std::max<int64_t>(sh[a][s], std::min<int64_t>(reach, radius_.dir(d)));
+          }
     Rect3 in = com;
     in.lo.x += sh[0][0];
     in.hi.x -= sh[0][1];

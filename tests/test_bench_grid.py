@@ -1,0 +1,34 @@
+"""bench.py's weak-scaling grids: exact 512^3 per GPU (default) and the reference's cbrt cube."""
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+@pytest.mark.parametrize("n,want", [(1, (512, 512, 512)), (2, (512, 512, 1024)), (4, (512, 1024, 1024)),
+                                    (8, (512, 1024, 2048))])
+def test_exact_grid_keeps_512_cubed_per_gpu(st, n, want):
+    g = bench.weak_grid(st, 512, n, "exact", (4, 3, 2))
+    assert g == want
+    r = st.Radius.constant(0)
+    r.set_face(1)
+    p = st.NodePartition(st.Dim3(*g), r, 1, n, st.Dim3(4, 3, 2))
+    d = p.dim()
+    assert d.x * d.y * d.z == n
+    for i in range(d.x):
+        for j in range(d.y):
+            for k in range(d.z):
+                assert p.subdomain_size(st.Dim3(i, j, k)) == st.Dim3(512, 512, 512)
+
+
+def test_exact_grid_reference_costs_is_a_cube_at_8(st):
+    # the reference's equal cut costs decompose 8 GPUs 2x2x2: the exact grid is then the cbrt cube itself
+    assert bench.weak_grid(st, 512, 8, "exact", (1, 1, 1)) == (1024, 1024, 1024)
+
+
+@pytest.mark.parametrize("n,side", [(1, 512), (2, 645), (4, 813), (8, 1024)])
+def test_cbrt_grid_is_the_reference_rule(st, n, side):
+    assert bench.weak_grid(st, 512, n, "cbrt", (4, 3, 2)) == (side, side, side)
