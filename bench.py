@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--x2pf", type=int, default=3, help="planes of z lookahead of the fused two-step kernel (1/2/3)")
     ap.add_argument("--x2row", type=int, default=1,
                     help="fused pairs: one wave per whole 512-cell row when x wraps in-kernel (fp32); 0 = columns")
+    ap.add_argument("--x2reserve", type=int, default=8,
+                    help="overlapped fused pairs: CUs the interior sweep leaves to the transport kernels")
     ap.add_argument("--zchunk", type=int, default=0, help="z planes per block (0 = auto)")
     ap.add_argument("--x2sched", type=int, default=1,
                     help="fused-pair work split: 1 = balanced segments over the resident blocks, 0 = fixed z-chunks")
@@ -175,6 +177,7 @@ def main():
     tune.x2pf = args.x2pf
     tune.x2row = args.x2row
     tune.zchunk = args.zchunk
+    tune.x2reserve = args.x2reserve
     tune.x2sched = args.x2sched
     tune.x2xfast = args.x2xfast
     overlap = not args.no_overlap and args.overlap != "off"

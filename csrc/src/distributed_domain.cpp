@@ -134,6 +134,7 @@ struct DevCtx {
   int dev = -1;
   Stream comm;
   Event done, translated;
+  bool translateEmpty = false; // the last exchange_async translated nothing on this device
   std::vector<int> doms;
   SegList translate;              // Kernel + PeerCopy originating here (variant = parity)
   SegList translateSkip;          // same without the directions crossing Impl::skipAxes (prepare_skip_wrapped)
@@ -928,6 +929,9 @@ void DistributedDomain::record_ready(size_t di, hipStream_t s) {
 void DistributedDomain::wait_translated(size_t di, hipStream_t s) {
   if (backend_ != Backend::Device) return;
   const DevCtx &ctx = impl_->devs[impl_->devIndex.at(domains_.at(di).gpu())];
+  // nothing translated on this device (every same-GPU halo wrapped in-kernel, the rest remote): the caller's stream
+  // already orders everything the local interior reads, so skip the cross-stream hop (~10 us per exchange)
+  if (ctx.translateEmpty) return;
   ctx.translated.wait_on(s);
 }
 
@@ -1089,7 +1093,8 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     HIP_CHECK(hipSetDevice(ctx.dev));
     TraceRange t("kernel/peer translate");
     const SegList &tl = skipAxes != 0 ? ctx.translateSkip : ctx.translate;
-    if (!tl.host[parity].empty()) tl.run_device(parity, S(ctx));
+    ctx.translateEmpty = tl.host[parity].empty();
+    if (!ctx.translateEmpty) tl.run_device(parity, S(ctx));
     if (!over) ctx.translated.record(S(ctx)); // events only matter across streams
   }
 

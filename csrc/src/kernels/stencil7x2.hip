@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <type_traits>
@@ -1308,7 +1309,7 @@ static void launch_thin(const LocalDomain &dom, int64_t qi, const std::vector<Re
 
 template <typename T, int KIND>
 static void apply_exterior_t(const LocalDomain &dom, int64_t qi, const Rect3 &c, const Rect3 &in, const Spheres &sph,
-                             hipStream_t stream, int wrap) {
+                             hipStream_t stream, int wrap, bool zDone) {
   auto nonempty = [](std::initializer_list<Rect3> l) {
     std::vector<Rect3> v;
     for (const Rect3 &r : l)
@@ -1322,7 +1323,7 @@ static void apply_exterior_t(const LocalDomain &dom, int64_t qi, const Rect3 &c,
                             Rect3(Dim3(c.lo.x, in.hi.y, in.lo.z), Dim3(c.hi.x, c.hi.y, in.hi.z))});
   const auto xs = nonempty({Rect3(Dim3(c.lo.x, in.lo.y, in.lo.z), Dim3(in.lo.x, in.hi.y, in.hi.z)),
                             Rect3(Dim3(in.hi.x, in.lo.y, in.lo.z), Dim3(c.hi.x, in.hi.y, in.hi.z))});
-  launch_thin<T, KIND, 2, 0, 1>(dom, qi, zs, sph, stream, wrap);
+  if (!zDone) launch_thin<T, KIND, 2, 0, 1>(dom, qi, zs, sph, stream, wrap);
   launch_thin<T, KIND, 1, 0, 2>(dom, qi, ys, sph, stream, wrap);
   launch_thin<T, KIND, 0, 1, 2>(dom, qi, xs, sph, stream, wrap);
 }
@@ -1353,12 +1354,27 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
   }
   dom.set_device();
   const bool f32 = dom.elem_size(qi) == 4, jac = kind == StencilKind::Jacobi;
+  // z slabs (whole x-y planes) of periodic 512-cell rows: the whole-row kernel, one block per 8 output rows of a
+  // slab (fixed z chunk = the slab: every block marches only its slab's planes)
+  bool zDone = false;
+  const char *zr = std::getenv("STENCIL_ZSLAB_ROW");
+  if (f32 && tune.x2row && (tune.wrap & 1) && (zr == nullptr || std::atoi(zr) != 0) && lo.z <= 4 && hi.z <= 4) {
+    StencilTune tz = tune;
+    tz.x2sched = 0;
+    tz.reserveCUs = 0;
+    zDone = true;
+    for (const Rect3 &r : {Rect3(c.lo, Dim3(c.hi.x, c.hi.y, in.lo.z)), Rect3(Dim3(c.lo.x, c.lo.y, in.hi.z), c.hi)}) {
+      if (r.empty()) continue;
+      tz.zchunk = int(r.hi.z - r.lo.z);
+      stencil7x2_apply(dom, qi, r, kind, sph, stream, tz);
+    }
+  }
   if (f32)
-    jac ? apply_exterior_t<float, 0>(dom, qi, c, in, sph, stream, tune.wrap)
-        : apply_exterior_t<float, 1>(dom, qi, c, in, sph, stream, tune.wrap);
+    jac ? apply_exterior_t<float, 0>(dom, qi, c, in, sph, stream, tune.wrap, zDone)
+        : apply_exterior_t<float, 1>(dom, qi, c, in, sph, stream, tune.wrap, zDone);
   else
-    jac ? apply_exterior_t<double, 0>(dom, qi, c, in, sph, stream, tune.wrap)
-        : apply_exterior_t<double, 1>(dom, qi, c, in, sph, stream, tune.wrap);
+    jac ? apply_exterior_t<double, 0>(dom, qi, c, in, sph, stream, tune.wrap, zDone)
+        : apply_exterior_t<double, 1>(dom, qi, c, in, sph, stream, tune.wrap, zDone);
 }
 
 } // namespace stencil

@@ -66,7 +66,7 @@ void StencilModel::init() {
   const Rect3 cReg = dd_->get_compute_region();
   sph_ = cfg_.kind == StencilKind::Jacobi ? Spheres::jacobi(cReg) : Spheres();
   overlap_ = cfg_.overlap;
-  if (cfg_.overlap && cfg_.autoOverlap &&
+  if (cfg_.overlap && cfg_.autoOverlap && std::getenv("STENCIL_FAKE_REMOTE_AXES") == nullptr &&
       dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All))
     overlap_ = false;
   auto &doms0 = dd_->domains();
