@@ -80,7 +80,10 @@ def main():
                          "decomposition of the cbrt-scaled cube); cbrt = the reference's rule, a per_gpu*N^(1/3) cube "
                          "(bin/jacobi3d.cu:167-169: 645^3 / 813^3 / 1024^3 at N = 2 / 4 / 8, ragged sub-domains)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
-                    help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU)")
+                    help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU, and then "
+                         "overlapped or whole-region pairs, whichever runs faster in the warm-up)")
+    ap.add_argument("--tune-steps", type=int, default=8,
+                    help="steps per timed round of the overlap choice (auto, remote halos only; 0 = no choice)")
     args = ap.parse_args()
 
     import torch
@@ -189,6 +192,31 @@ def main():
     model.run(args.warmup)
     model.synchronize()
     barrier()
+    # overlapped vs whole-region pairs (remote halos only): both run, the faster one (max over ranks, best of two
+    # rounds) is kept for the timed loop -- part of the warm-up, every rank takes the same decision
+    overlap_tuned = None
+    if args.overlap == "auto" and args.tune_steps > 0 and model.can_toggle_overlap():
+        def timed_run(k):
+            barrier()
+            t = time.perf_counter()
+            model.run(k)
+            model.synchronize()
+            dt = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=red_dev)
+            if world > 1:
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            return float(dt.item()) / k * 1e3
+        best = {}
+        for on in (True, False, True, False):
+            model.set_overlap(on)
+            model.run(2)
+            model.synchronize()
+            best[on] = min(best.get(on, float("inf")), timed_run(args.tune_steps))
+        choice = best[True] <= best[False]
+        model.set_overlap(choice)
+        model.run(2)
+        model.synchronize()
+        barrier()
+        overlap_tuned = {"on_ms": round(best[True], 4), "off_ms": round(best[False], 4)}
     t0 = time.perf_counter()
     model.run(args.steps)  # every step is enqueued; whole blocks of steps replay as one hipGraph where possible
     model.synchronize()
@@ -243,7 +271,7 @@ def main():
                        "decomposition": "x".join(str(v) for v in (model.domain.placement_dim().x,
                                                                    model.domain.placement_dim().y,
                                                                    model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
-                       "overlap": model.overlapping(), "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
+                       "overlap": model.overlapping(), "overlap_tuned": overlap_tuned, "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
                        "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
                        "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none"},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),

@@ -83,6 +83,11 @@ public:
   int64_t steps_done() const { return steps_; }
   const Spheres &spheres() const { return sph_; }
   bool overlapping() const { return overlap_; }
+  // fused pairs with remote halos: overlapped (local interior during the transfers, slabs after) and whole-region
+  // (exchange, then one sweep) share the wrap mask, so either can run; set_overlap() switches between them (after a
+  // synchronize), e.g. to keep whichever the hardware runs faster
+  bool can_toggle_overlap() const { return overlapToggle_; }
+  void set_overlap(bool on);
   bool local_interior_steps() const { return localSteps_; } // overlapped single steps on get_local_interior
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }
@@ -102,6 +107,7 @@ private:
   bool graphs_ = false;
   bool forward_ = false;
   bool pairs_ = false; // temporal blocking active
+  bool overlapToggle_ = false;
   StencilTune pairTune_; // cfg_.tune + the in-kernel wrap axes of the fused pairs
   StencilTune stepTune_; // cfg_.tune + the in-kernel wrap axes of single steps
   bool localSteps_ = false;                      // overlapped single steps on the local interior (see init)

@@ -610,6 +610,8 @@ PYBIND11_MODULE(_C, m) {
       .def("local_cells", &StencilModel::local_cells)
       .def("steps_done", &StencilModel::steps_done)
       .def("overlapping", &StencilModel::overlapping)
+      .def("can_toggle_overlap", &StencilModel::can_toggle_overlap)
+      .def("set_overlap", &StencilModel::set_overlap, py::call_guard<py::gil_scoped_release>())
       .def("local_interior_steps", &StencilModel::local_interior_steps)
       .def("forwarding", &StencilModel::forwarding)
       .def("temporal_blocking", &StencilModel::temporal_blocking)

@@ -116,21 +116,39 @@ void StencilModel::init() {
   }
   pairTune_ = cfg_.tune;
   pairTune_.wrap = 0;
+  // overlapped and whole-region pairs can be switched at run time when both would wrap the same axes: the local
+  // interior is shrunk only along axes cut across GPUs, which are never self-wrapped (set_overlap)
+  bool sameWrap = true;
   if (pairs_ && cfg_.wrapSelf && std::getenv("STENCIL_NO_WRAP") == nullptr) {
     int w = dd_->self_wrap_axes();
     for (size_t di = 0; di < doms0.size(); ++di) {
       const auto &d = doms0[di];
       for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7x2_wrappable_axes(d, q, cfg_.tune.x2row);
-      // the swept regions must span every wrapped axis (a forced full split cuts all of them)
-      const Rect3 c = d.get_compute_region();
-      const Rect3 r = overlap_ ? pairInteriors_[di] : c;
-      if (r.lo.x != c.lo.x || r.hi.x != c.hi.x) w &= ~1;
-      if (r.lo.y != c.lo.y || r.hi.y != c.hi.y) w &= ~2;
-      if (r.lo.z != c.lo.z || r.hi.z != c.hi.z) w &= ~4;
     }
+    int wOn = w;
+    for (size_t di = 0; di < doms0.size() && !pairInteriors_.empty(); ++di) {
+      // the swept regions must span every wrapped axis (a forced full split cuts all of them)
+      const Rect3 c = doms0[di].get_compute_region();
+      const Rect3 &r = pairInteriors_[di];
+      if (r.lo.x != c.lo.x || r.hi.x != c.hi.x) wOn &= ~1;
+      if (r.lo.y != c.lo.y || r.hi.y != c.hi.y) wOn &= ~2;
+      if (r.lo.z != c.lo.z || r.hi.z != c.hi.z) wOn &= ~4;
+    }
+    sameWrap = wOn == w;
+    if (overlap_) w = wOn;
     if (const char *e = std::getenv("STENCIL_WRAP_AXES")) w &= std::atoi(e); // restrict (experiments)
     pairTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
+  }
+  if (pairs_ && sameWrap && !pairInteriors_.empty()) {
+    const auto li = dd_->get_local_interior(2);
+    bool remote = false, ok = true;
+    for (size_t di = 0; di < doms0.size(); ++di) {
+      const Rect3 c = doms0[di].get_compute_region();
+      remote = remote || !(li[di].lo == c.lo && li[di].hi == c.hi);
+      ok = ok && !pairInteriors_[di].empty();
+    }
+    overlapToggle_ = remote && ok && doms0[0].backend() == Backend::Device;
   }
   // single steps: the self-periodic axes are read in-kernel at their periodic image and their same-GPU copies leave
   // the exchange (a fully periodic sub-domain exchanges nothing; one MI355X at 512^3: the ~25 us copy-plan kernel of
@@ -410,6 +428,15 @@ void StencilModel::enqueue_step(int k) {
         stencil7_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, stepTune_);
     }
   }
+}
+
+void StencilModel::set_overlap(bool on) {
+  STENCIL_REQUIRE(overlapToggle_, "set_overlap: this model's pairs cannot switch overlap (no remote halos, or the "
+                                  "overlapped sweep would wrap other axes)");
+  if (on == overlap_) return;
+  synchronize();
+  overlap_ = on;
+  dd_->set_comm_max_blocks(on ? cfg_.tune.x2reserve : 0);
 }
 
 void StencilModel::synchronize() {

@@ -76,6 +76,15 @@ class StencilModel:
     def overlapping(self) -> bool:
         return self._m.overlapping()
 
+    def can_toggle_overlap(self) -> bool:
+        """True when the fused pairs have remote halos and can run overlapped or whole-region (set_overlap)."""
+        return self._m.can_toggle_overlap()
+
+    def set_overlap(self, on: bool):
+        """Switch fused pairs between overlapped (local interior during the transfers, slabs after) and whole-region
+        (exchange, then one sweep); synchronizes first."""
+        self._m.set_overlap(bool(on))
+
     def local_interior_steps(self) -> bool:
         """True when overlapped single steps sweep the local interior (shrunk only at remote faces) during the
         remote transfers and wrap the self-periodic axes in-kernel."""

@@ -113,8 +113,16 @@ def scenario_jacobi(backend, methods, size):
     m.run(5)  # fused pairs when temporal blocking is on
     for _ in range(5):
         u = ref(u)
-    m.synchronize()
     bad = 0
+    if os.environ.get("MP_TOGGLE_OVERLAP"):  # whole-region pairs, then back to overlapped ones (set_overlap)
+        bad += int(not m.can_toggle_overlap())
+        if m.can_toggle_overlap():
+            for _ in range(2):
+                m.set_overlap(not m.overlapping())
+                m.run(4)
+                for _ in range(4):
+                    u = ref(u)
+    m.synchronize()
     for di in range(m.domain.num_domains()):
         d = m.domain.domain(di)
         o, s = d.origin(), d.size()

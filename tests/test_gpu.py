@@ -541,6 +541,16 @@ def test_colocated_ipc_jacobi_two_ranks(temporal, ranks):
         assert rc == 0, out[-3000:]
 
 
+def test_colocated_ipc_overlap_toggle_two_ranks():
+    """Fused pairs over HIP IPC switched from overlapped to whole-region and back (StencilModel::set_overlap, the
+    bench's warm-up choice): bitwise equal to the oracle throughout."""
+    outs = run_ranks(2, WORKER, ["jacobi", "48,48,48"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": "2", "MP_EXPECT_OVERLAP": "1", "MP_TOGGLE_OVERLAP": "1"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
 @pytest.mark.parametrize("size,cost", [("512,264,16", "4,2,3"), ("1024,520,12", "4,2,3"), ("645,520,12", "4,2,3"),
                                        ("512,16,300", "4,3,2"), ("645,12,520", "4,3,2")])  # y cut / z cut
 def test_colocated_ipc_wide_rows_two_ranks(size, cost):
