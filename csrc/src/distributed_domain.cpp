@@ -948,17 +948,66 @@ hipStream_t DistributedDomain::comm_stream(size_t di) const {
 
 void DistributedDomain::sync_exchange() {
   if (backend_ != Backend::Device) return;
-  for (auto &d : impl_->devs) {
+  Impl &I = *impl_;
+  if (I.rccl) {
+    // RCCL watchdog: poll the streams that carry RCCL work, check every communicator's asynchronous
+    // error, and give up after the wait timeout with the plan on stderr (a peer that died or never posted its
+    // matching send/recv would otherwise block here forever)
+    const double t0 = now_s();
+    auto done = [&]() {
+      bool all = true;
+      for (auto &d : I.devs) {
+        HIP_CHECK(hipSetDevice(d.dev));
+        const hipError_t q = hipStreamQuery(d.comm);
+        if (q == hipErrorNotReady) {
+          (void)hipGetLastError();
+          all = false;
+        } else {
+          HIP_CHECK(q);
+        }
+      }
+      if (I.callerPending) {
+        const hipError_t q = hipEventQuery(I.callerDone);
+        if (q == hipErrorNotReady) {
+          (void)hipGetLastError();
+          all = false;
+        } else {
+          HIP_CHECK(q);
+        }
+      }
+      return all;
+    };
+    while (!done()) {
+      for (auto &d : I.devs) {
+        if (!d.nccl) continue;
+        ncclResult_t r = ncclSuccess;
+        if (ncclCommGetAsyncError(d.nccl, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress) {
+          LOG_ERROR("RCCL asynchronous error on device " << d.dev << ": " << ncclGetErrorString(r) << "\n"
+                                                          << plan_summary());
+          LOG_FATAL("halo exchange failed in RCCL (epoch " << I.epoch << ")");
+        }
+      }
+      if (now_s() - t0 > I.waitTimeout) {
+        LOG_ERROR("halo exchange still running after " << I.waitTimeout << " s (epoch " << I.epoch
+                                                        << "); plan:\n" << plan_summary());
+        for (auto &d : I.devs)
+          if (d.nccl) (void)ncclCommAbort(d.nccl), d.nccl = nullptr;
+        LOG_FATAL("halo exchange timed out in RCCL; a peer rank is stalled or dead");
+      }
+      std::this_thread::yield();
+    }
+  }
+  for (auto &d : I.devs) {
     HIP_CHECK(hipSetDevice(d.dev));
     HIP_CHECK(hipStreamSynchronize(d.comm));
   }
-  if (impl_->callerPending) {
-    impl_->callerDone.sync();
-    impl_->callerPending = false;
+  if (I.callerPending) {
+    I.callerDone.sync();
+    I.callerPending = false;
   }
-  if (*impl_->errHost) {
-    const int code = *impl_->errHost;
-    LOG_FATAL("halo exchange timed out waiting for a colocated peer (code " << code << ", epoch " << impl_->epoch
+  if (*I.errHost) {
+    const int code = *I.errHost;
+    LOG_FATAL("halo exchange timed out waiting for a colocated peer (code " << code << ", epoch " << I.epoch
                                                                            << "); a peer rank is stalled or dead");
   }
 }
