@@ -206,17 +206,19 @@ def main():
                 dist.all_reduce(dt, op=dist.ReduceOp.MAX)
             return float(dt.item()) / k * 1e3
         best = {}
-        for on in (True, False, True, False):
-            model.set_overlap(on)
+        k = max(2, args.tune_steps // 2 * 2)
+        for mode in (1, 2, 0, 1, 2, 0):  # 1: slabs beside the sweep, 2: slabs after it, 0: whole-region pairs
+            model.set_overlap_mode(mode)
             model.run(2)
             model.synchronize()
-            best[on] = min(best.get(on, float("inf")), timed_run(args.tune_steps))
-        choice = best[True] <= best[False]
-        model.set_overlap(choice)
+            best[mode] = min(best.get(mode, float("inf")), timed_run(k))
+        choice = min((1, 2, 0), key=lambda m: best[m])
+        model.set_overlap_mode(choice)
         model.run(2)
         model.synchronize()
         barrier()
-        overlap_tuned = {"on_ms": round(best[True], 4), "off_ms": round(best[False], 4)}
+        overlap_tuned = {"mode": choice, "beside_ms": round(best[1], 4), "after_ms": round(best[2], 4),
+                         "off_ms": round(best[0], 4)}
     t0 = time.perf_counter()
     model.run(args.steps)  # every step is enqueued; whole blocks of steps replay as one hipGraph where possible
     model.synchronize()

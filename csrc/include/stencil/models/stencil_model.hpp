@@ -88,6 +88,11 @@ public:
   // synchronize), e.g. to keep whichever the hardware runs faster
   bool can_toggle_overlap() const { return overlapToggle_; }
   void set_overlap(bool on);
+  // overlapped pairs, where the slabs at the remote faces run: 1 = on the comm stream right behind the exchange,
+  // beside the interior sweep (default); 2 = on the compute stream after the interior sweep (the sweep then shares the
+  // GPU with the transport kernels only). 0 = whole-region pairs (set_overlap(false)).
+  void set_overlap_mode(int mode);
+  int overlap_mode() const { return overlap_ ? (slabsAfter_ ? 2 : 1) : 0; }
   bool local_interior_steps() const { return localSteps_; } // overlapped single steps on get_local_interior
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }
@@ -108,6 +113,7 @@ private:
   bool forward_ = false;
   bool pairs_ = false; // temporal blocking active
   bool overlapToggle_ = false;
+  bool slabsAfter_ = false; // overlap mode 2 (see set_overlap_mode)
   StencilTune pairTune_; // cfg_.tune + the in-kernel wrap axes of the fused pairs
   StencilTune stepTune_; // cfg_.tune + the in-kernel wrap axes of single steps
   bool localSteps_ = false;                      // overlapped single steps on the local interior (see init)

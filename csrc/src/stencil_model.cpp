@@ -203,6 +203,8 @@ void StencilModel::init() {
     stepTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
+  // experiments: overlapped pairs with the slabs after the interior sweep (set_overlap_mode(2)) from the start
+  if (const char *e = std::getenv("STENCIL_OVERLAP_MODE")) slabsAfter_ = pairs_ && overlap_ && std::atoi(e) == 2;
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
@@ -341,6 +343,14 @@ void StencilModel::enqueue_step(int k) {
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
         stencil7x2_apply(doms[di], q, pairInteriors_[di], cfg_.kind, sph_, compute_[di].get(), ti);
     }
+    if (slabsAfter_) { // mode 2: the slabs follow the interior sweep on the compute stream, once the halos are in
+      for (size_t di = 0; di < doms.size(); ++di) {
+        dd_->wait_exchange(di, compute_[di]);
+        for (int64_t q = 0; q < doms[di].num_data(); ++q)
+          stencil7x2_apply_exterior(doms[di], q, pairInteriors_[di], cfg_.kind, sph_, compute_[di].get(), pairTune_);
+      }
+      return;
+    }
     for (size_t di = 0; di < doms.size(); ++di) {
       hipStream_t s = dd_->comm_stream(di);
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
@@ -437,6 +447,13 @@ void StencilModel::set_overlap(bool on) {
   synchronize();
   overlap_ = on;
   dd_->set_comm_max_blocks(on ? cfg_.tune.x2reserve : 0);
+}
+
+void StencilModel::set_overlap_mode(int mode) {
+  STENCIL_REQUIRE(mode >= 0 && mode <= 2, "overlap mode " << mode);
+  if (mode == overlap_mode()) return;
+  set_overlap(mode != 0);
+  slabsAfter_ = mode == 2;
 }
 
 void StencilModel::synchronize() {

@@ -85,6 +85,14 @@ class StencilModel:
         (exchange, then one sweep); synchronizes first."""
         self._m.set_overlap(bool(on))
 
+    def set_overlap_mode(self, mode: int):
+        """0 = whole-region pairs; 1 = overlapped, slabs on the comm stream beside the interior sweep; 2 = overlapped,
+        slabs after the interior sweep on the compute stream."""
+        self._m.set_overlap_mode(int(mode))
+
+    def overlap_mode(self) -> int:
+        return self._m.overlap_mode()
+
     def local_interior_steps(self) -> bool:
         """True when overlapped single steps sweep the local interior (shrunk only at remote faces) during the
         remote transfers and wrap the self-periodic axes in-kernel."""

@@ -117,8 +117,9 @@ def scenario_jacobi(backend, methods, size):
     if os.environ.get("MP_TOGGLE_OVERLAP"):  # whole-region pairs, then back to overlapped ones (set_overlap)
         bad += int(not m.can_toggle_overlap())
         if m.can_toggle_overlap():
-            for _ in range(2):
-                m.set_overlap(not m.overlapping())
+            for mode in (0, 2, 1):
+                m.set_overlap_mode(mode)
+                bad += int(m.overlap_mode() != mode)
                 m.run(4)
                 for _ in range(4):
                     u = ref(u)

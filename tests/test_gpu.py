@@ -443,25 +443,26 @@ def test_temporal2_overlapped(st, methods, size, gpus, kind):
     assert torch.equal(_gather(m), u)
 
 
-@pytest.mark.parametrize("zrow", ["1", "0"])
+@pytest.mark.parametrize("zrow,mode", [("1", "1"), ("0", "1"), ("1", "2")])
 @pytest.mark.parametrize("size,gpus,fake,kind", [((512, 112, 120), [0], 4, "jacobi"),
                                                  ((512, 112, 120), [0, 0], 4, "jacobi"),
                                                  ((512, 112, 120), [0, 0, 0, 0], 6, "jacobi"),
                                                  ((512, 20, 26), [0, 0], 6, "astaroth"),
                                                  ((645, 132, 136), [0, 0], 4, "jacobi")])
-def test_temporal2_overlapped_zslab_row_kernel(st, monkeypatch, zrow, size, gpus, fake, kind):
+def test_temporal2_overlapped_zslab_row_kernel(st, monkeypatch, zrow, mode, size, gpus, fake, kind):
     """Overlapped fused pairs with periodic 512-cell (and ragged) rows whose z (and y) faces are treated as remote
     (STENCIL_FAKE_REMOTE_AXES: the multi-GPU split on one GPU): the z slabs go through the whole-row kernel with the
     slab as its z chunk (STENCIL_ZSLAB_ROW=1, default) or the thin kernel (0); both bitwise equal to single steps."""
     from stencil2_amd.ops import astaroth_step_reference
     monkeypatch.setenv("STENCIL_ZSLAB_ROW", zrow)
     monkeypatch.setenv("STENCIL_FAKE_REMOTE_AXES", str(fake))
+    monkeypatch.setenv("STENCIL_OVERLAP_MODE", mode)  # 2: the slabs after the interior sweep
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
     m = cls(size, gpus=gpus, temporal=2, overlap=True, axis_cost=(64, 3, 2), **kw)
     m.init()
     assert m.temporal_blocking() and m.overlapping() and m.wrap_axes() == (1 if fake == 6 else 3)
-    assert m.domain.placement_dim().x == 1
+    assert m.domain.placement_dim().x == 1 and m.overlap_mode() == int(mode)
     u = _gather(m)
     m.run(6)
     for _ in range(6):
