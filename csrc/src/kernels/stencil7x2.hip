@@ -326,8 +326,18 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   const int lane = threadIdx.x;
   const int w = int(threadIdx.y);
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
-  uint32_t s, e;
-  if (a.seg) {
+  uint32_t s, e, s2 = 0, e2 = 0;
+  if (a.seg == 2) {
+    // lockstep: four blocks per column (quarters of the z range) for the first nb/4 columns, so y-adjacent blocks
+    // (4 apart, one XCD after the remap) march the same planes together and their shared y-halo rows meet in L2;
+    // the columns left over (grids of fewer than 4 x columns blocks) spread over all blocks as short second segments
+    const uint32_t cm = nb / 4, col = lb / 4, qq = lb % 4;
+    s = col * nzt + qq * nzt / 4;
+    e = col * nzt + (qq + 1) * nzt / 4;
+    const uint64_t LW = uint64_t(uint32_t(a.gy) - cm) * nzt;
+    s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
+    e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
+  } else if (a.seg) {
     const uint64_t W = uint64_t(uint32_t(a.gy)) * nzt;
     s = uint32_t(uint64_t(lb) * W / nb);
     e = uint32_t(uint64_t(lb + 1) * W / nb);
@@ -337,6 +347,11 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
     e = min(s + uint32_t(a.zc), (col + 1) * nzt);
   }
   bool odd = a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0;
+  for (int pass = 0; pass < 2; ++pass) {
+  if (pass == 1) {
+    s = s2;
+    e = e2;
+  }
   while (s < e) { // block-uniform
   const uint32_t by = s / nzt; // one column per row range
   const int zo = int(s - by * nzt);
@@ -518,6 +533,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   else
     march(std::false_type{});
   } // segments
+  } // passes
 }
 
 // 512-cell columns (fp32): the whole-row layout of stencil7x2_row_kernel (two 16-B chunks per lane, 256 cells apart,
@@ -1076,6 +1092,18 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
     const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
     blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 16)));
+    // lockstep quarters (a.seg = 2) when the resident blocks cover at most four per column and the quarters stay
+    // long: with 8 CUs left to the transports (248 blocks) the balanced split puts y-adjacent blocks 16 planes apart
+    // and their halo rows miss L2 (512^3 local interior: 276 vs 237 us at 256 blocks)
+    static const bool lockstep = [] {
+      const char *e = std::getenv("STENCIL_X2_LOCKSTEP");
+      return e == nullptr || std::atoi(e) != 0;
+    }();
+    const int64_t q4 = slots / 4 * 4;
+    if (lockstep && q4 >= 4 && q4 / 4 <= cols && nz >= 64) {
+      a.seg = 2;
+      blocks = uint32_t(q4);
+    }
   } else {
     int zc = tune.zchunk;
     if (zc <= 0) zc = pick_zchunk(cols, nz, resident, 4, 16);

@@ -471,6 +471,29 @@ def test_temporal2_overlapped_zslab_row_kernel(st, monkeypatch, zrow, mode, size
     assert torch.equal(_gather(m), u)
 
 
+@pytest.mark.parametrize("fake,reserve,lockstep", [(None, 8, "1"), ("4", 8, "1"), ("4", 4, "1"), ("4", 8, "0"),
+                                                    ("6", 8, "1")])
+def test_temporal2_row_kernel_lockstep_quarters(st, monkeypatch, fake, reserve, lockstep):
+    """Whole-row fused pairs over 64 row groups: the lockstep schedule (four blocks per column for the first
+    blocks/4 columns, the rest as short second segments: 256 / 248 / 252 resident blocks) and the balanced one are
+    bitwise equal to single steps (Astaroth proxy: no spheres, any grid thickness)."""
+    from stencil2_amd.ops import astaroth_step_reference
+    monkeypatch.setenv("STENCIL_X2_LOCKSTEP", lockstep)
+    if fake:
+        monkeypatch.setenv("STENCIL_FAKE_REMOTE_AXES", fake)
+    t = st.StencilTune()
+    t.x2reserve = reserve
+    m = st.AstarothSim((512, 512, 72), quantities=1, gpus=[0], temporal=2, tune=t, axis_cost=(64, 3, 2))
+    m.init()
+    assert m.temporal_blocking() and m.overlapping() == bool(fake)
+    u = _gather(m)
+    m.run(4)
+    for _ in range(4):
+        u = astaroth_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
 @pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy"])
 def test_jacobi_temporal2_transports(st, methods):
     """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs"""
