@@ -207,18 +207,23 @@ def main():
             return float(dt.item()) / k * 1e3
         best = {}
         k = max(2, args.tune_steps // 2 * 2)
-        for mode in (1, 2, 0, 1, 2, 0):  # 1: slabs beside the sweep, 2: slabs after it, 0: whole-region pairs
-            model.set_overlap_mode(mode)
+        r0 = args.x2reserve
+        # (mode, CUs left to the transports): 1 = slabs beside the sweep, 2 = slabs after it, 0 = whole-region pairs
+        cands = [(1, r0), (1, 2 * r0), (2, r0), (0, r0)]
+        for c in cands + cands:
+            model.set_overlap_mode(c[0])
+            model.set_comm_reserve(c[1])
             model.run(2)
             model.synchronize()
-            best[mode] = min(best.get(mode, float("inf")), timed_run(k))
-        choice = min((1, 2, 0), key=lambda m: best[m])
-        model.set_overlap_mode(choice)
+            best[c] = min(best.get(c, float("inf")), timed_run(k))
+        choice = min(cands, key=lambda c: best[c])
+        model.set_overlap_mode(choice[0])
+        model.set_comm_reserve(choice[1])
         model.run(2)
         model.synchronize()
         barrier()
-        overlap_tuned = {"mode": choice, "beside_ms": round(best[1], 4), "after_ms": round(best[2], 4),
-                         "off_ms": round(best[0], 4)}
+        overlap_tuned = {"mode": choice[0], "reserve": choice[1],
+                         **{f"m{c[0]}_r{c[1]}_ms": round(best[c], 4) for c in cands}}
     t0 = time.perf_counter()
     model.run(args.steps)  # every step is enqueued; whole blocks of steps replay as one hipGraph where possible
     model.synchronize()

@@ -93,6 +93,9 @@ public:
   // GPU with the transport kernels only). 0 = whole-region pairs (set_overlap(false)).
   void set_overlap_mode(int mode);
   int overlap_mode() const { return overlap_ ? (slabsAfter_ ? 2 : 1) : 0; }
+  // CUs the overlapped sweeps leave to the transport kernels (StencilTune::x2reserve); synchronizes first
+  void set_comm_reserve(int cus);
+  int comm_reserve() const { return cfg_.tune.x2reserve; }
   bool local_interior_steps() const { return localSteps_; } // overlapped single steps on get_local_interior
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }

@@ -456,6 +456,16 @@ void StencilModel::set_overlap_mode(int mode) {
   slabsAfter_ = mode == 2;
 }
 
+void StencilModel::set_comm_reserve(int cus) {
+  STENCIL_REQUIRE(cus >= 0 && cus <= 128, "comm reserve " << cus);
+  if (cus == cfg_.tune.x2reserve) return;
+  synchronize();
+  cfg_.tune.x2reserve = cus;
+  pairTune_.x2reserve = cus;
+  stepTune_.x2reserve = cus;
+  if (overlap_) dd_->set_comm_max_blocks(cus);
+}
+
 void StencilModel::synchronize() {
   for (auto &s : compute_) s.sync();
   if (dd_->realized()) dd_->sync_exchange();

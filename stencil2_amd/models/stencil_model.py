@@ -93,6 +93,13 @@ class StencilModel:
     def overlap_mode(self) -> int:
         return self._m.overlap_mode()
 
+    def set_comm_reserve(self, cus: int):
+        """CUs the overlapped sweeps leave to the transport kernels (StencilTune.x2reserve)."""
+        self._m.set_comm_reserve(int(cus))
+
+    def comm_reserve(self) -> int:
+        return self._m.comm_reserve()
+
     def local_interior_steps(self) -> bool:
         """True when overlapped single steps sweep the local interior (shrunk only at remote faces) during the
         remote transfers and wrap the self-periodic axes in-kernel."""

@@ -117,9 +117,10 @@ def scenario_jacobi(backend, methods, size):
     if os.environ.get("MP_TOGGLE_OVERLAP"):  # whole-region pairs, then back to overlapped ones (set_overlap)
         bad += int(not m.can_toggle_overlap())
         if m.can_toggle_overlap():
-            for mode in (0, 2, 1):
+            for mode, reserve in ((0, 8), (2, 8), (1, 16), (1, 8)):
                 m.set_overlap_mode(mode)
-                bad += int(m.overlap_mode() != mode)
+                m.set_comm_reserve(reserve)
+                bad += int(m.overlap_mode() != mode or m.comm_reserve() != reserve)
                 m.run(4)
                 for _ in range(4):
                     u = ref(u)
