@@ -366,6 +366,9 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   const int y = yblk - 2 + w;
   if (yblk >= a.hiy) continue;
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy;
+  // wave-uniform: u1 is needed on rows 1 .. NW-2 of the block (the y-neighbours of the output rows), u2 only on the
+  // output rows; the edge waves only load and publish their source rows
+  const bool needU1 = !a.edgeskip || (w >= 1 && w < NW - 1), needU2 = !a.edgeskip || (w >= 2 && w < NW - 2);
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
   const bool lane0 = lane == 0, lane63 = lane == 63;
   // ragged rows: the last cell x = nx-1 sits in chunk H-1 of lane Lr, element kr
@@ -472,7 +475,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
       const int z = z0 + t * dz;
       const int P = z + dz;
       load_row(z + (NC - 1) * dz, sn);
-      {
+      if (needU1) {
         NV cA[H], cB[H];
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -480,8 +483,11 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
           cB[h] = cs[buf][wB][h][lane];
         }
         apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], row_sph(P), Ua);
+      } else {
+#pragma unroll
+        for (int h = 0; h < H; ++h) Ua[h] = C[s1][h]; // never read: the edge waves' u1 feeds no output row
       }
-      if (t >= 0) {
+      if (t >= 0 && needU2) {
         NV uA[H], uB[H], o[H];
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -1076,6 +1082,11 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   a.x0 = a.lox;
   a.nchunks = 128;
   a.remap = tune.xcdRemap ? 1 : 0;
+  static const int edgeskip = [] {
+    const char *e = std::getenv("STENCIL_X2_EDGE_SKIP");
+    return e == nullptr || std::atoi(e) != 0 ? 1 : 0;
+  }();
+  a.edgeskip = edgeskip;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = 1;
   a.gy = (ny + YO - 1) / YO;
