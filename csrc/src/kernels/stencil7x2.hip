@@ -111,6 +111,8 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
   const bool fullX = xb >= a.lox && xb + V <= a.hix;
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy && cvalid;
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1; // outer waves: garbage u1, never consumed
+  // wave-uniform: u1 only on rows 1 .. NW-2, u2 only on the output rows (see stencil7x2_row_kernel)
+  const bool needU1 = !a.edgeskip || (w >= 1 && w < NW - 1), needU2 = !a.edgeskip || (w >= 2 && w < NW - 2);
 
   // y-wrapped rows read their periodic image (one conditional shift: rows reach 2 beyond the region, ny >= 2)
   const int yw =
@@ -233,7 +235,10 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
       const NV cA = cs[buf][wA][lane], cB = cs[buf][wB][lane];
       const T cAL = ce[buf][wA][0], cAR = ce[buf][wA][1]; // LDS broadcasts
       const T cBL = ce[buf][wB][0], cBR = ce[buf][wB][1];
-      {
+      if (!needU1) {
+        Ua = C[s1]; // never read
+        UaE = P2{T(0), T(0)};
+      } else {
         const RowSph rs = row_sph(P);
         Ua = apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], CL[s1], CR[s1], rs);
         const P2 epx = {C[s1][0], RR[s1]}, emx = {LL[s1], C[s1][V - 1]}, epy = {cBL, cBR}, emy = {cAL, cAR};
@@ -246,7 +251,7 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
         }
       }
       // 3. u2 at plane z
-      if (t >= 0) {
+      if (t >= 0 && needU2) {
         const NV uA = us[buf][wA][lane], uB = us[buf][wB][lane];
         const NV o = apply_row(Uc, uA, uB, DOWN ? Ub : Ua, DOWN ? Ua : Ub, UcE[0], UcE[1], row_sph(z));
         if (outRow) {
@@ -606,6 +611,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   const int y = yblk - 2 + w;
   if (yblk >= a.hiy) continue;
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy;
+  const bool needU1 = !a.edgeskip || (w >= 1 && w < NW - 1), needU2 = !a.edgeskip || (w >= 2 && w < NW - 2);
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
   const bool lane0 = lane == 0, lane63 = lane == 63;
 
@@ -718,7 +724,11 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
       const int z = z0 + t * dz;
       const int P = z + dz;
       load_row(z + (NC - 1) * dz, sn);
-      {
+      if (!needU1) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) Ua[h] = C[s1][h]; // never read
+        UaE = P2{T(0), T(0)};
+      } else {
         NV cA[H], cB[H];
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -740,7 +750,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
           UaE[1] = fix(rs, xcol + CW, UaE[1]);
         }
       }
-      if (t >= 0) {
+      if (t >= 0 && needU2) {
         NV uA[H], uB[H], o[H];
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -950,6 +960,15 @@ __global__ __launch_bounds__(256) void stencil7x2_thin_kernel(StencilArgs<T> a, 
 // ---------------------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------------------
+// STENCIL_X2_EDGE_SKIP=0: every wave computes u1 and u2 (A/B of the edge-wave skip)
+static int x2_edge_skip() {
+  static const int v = [] {
+    const char *e = std::getenv("STENCIL_X2_EDGE_SKIP");
+    return e == nullptr || std::atoi(e) != 0 ? 1 : 0;
+  }();
+  return v;
+}
+
 static int64_t x2_resident_blocks(const void *kernel, int threads) {
   static std::map<const void *, int64_t> cache;
   static std::mutex mu;
@@ -1033,6 +1052,7 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.gx = (a.nchunks + 63) / 64;
   a.gy = (ny + YO - 1) / YO;
   a.remap = tune.xcdRemap ? 1 : 0;
+  a.edgeskip = x2_edge_skip();
   const void *kern = (const void *)stencil7x2_kernel<T, NW, PF, KIND, 0>;
   const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x2_resident_blocks(kern, 64 * NW);
@@ -1082,11 +1102,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   a.x0 = a.lox;
   a.nchunks = 128;
   a.remap = tune.xcdRemap ? 1 : 0;
-  static const int edgeskip = [] {
-    const char *e = std::getenv("STENCIL_X2_EDGE_SKIP");
-    return e == nullptr || std::atoi(e) != 0 ? 1 : 0;
-  }();
-  a.edgeskip = edgeskip;
+  a.edgeskip = x2_edge_skip();
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = 1;
   a.gy = (ny + YO - 1) / YO;
@@ -1139,6 +1155,7 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
   a.wrapm = tune.wrap;
   a.xfast = tune.x2xfast;
   a.remap = tune.xcdRemap ? 1 : 0;
+  a.edgeskip = x2_edge_skip();
   a.x0 = a.lox; // 16-B aligned (checked by the caller)
   a.nchunks = (a.hix - a.x0) / 4;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
