@@ -58,7 +58,7 @@ def main():
                     help="single-step kernel variant (2: VALU LDS z-march, 8: MFMA x-line update; needs --temporal 1)")
     ap.add_argument("--nw", type=int, default=8, help="waves per block of the stencil kernel")
     ap.add_argument("--x2nw", type=int, default=12, help="waves per block of the fused two-step kernel (8/12/16)")
-    ap.add_argument("--x2pf", type=int, default=3, help="planes of z lookahead of the fused two-step kernel (1/2/3)")
+    ap.add_argument("--x2pf", type=int, default=1, help="planes of z lookahead of the fused two-step kernel (1/2/3)")
     ap.add_argument("--x2row", type=int, default=1,
                     help="fused pairs: one wave per whole 512-cell row when x wraps in-kernel (fp32); 0 = columns")
     ap.add_argument("--x2reserve", type=int, default=8,

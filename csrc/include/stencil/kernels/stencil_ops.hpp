@@ -49,7 +49,7 @@ struct StencilTune {
   // fused-pair kernel (stencil7x2): waves per block (8/12/16, one src row each, NW-4 output rows) and planes of
   // z lookahead (1/2/3). 12 waves get 3 waves/SIMD and up to 168 VGPRs (no spills at any lookahead, fp32 or fp64);
   // one MI355X, 512^3, bench.py: 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s
-  int x2nw = 12, x2pf = 3;
+  int x2nw = 12, x2pf = 1; // one plane of lookahead: best for the whole-row kernel once its edge waves skip u1/u2
   // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells
   // long; x-neighbours and the wrap by DPP lane rotates, stencil7x2_row_kernel), or 512-cell columns (x a whole
   // number of 512-cell columns: two 16-B chunks per lane, only the column ends from outside the wave,

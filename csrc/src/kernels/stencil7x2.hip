@@ -273,7 +273,7 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
       cs[nbuf][w][lane] = C[s2];
       if (edgeL) ce[nbuf][w][0] = CL[s2];
       if (edgeR) ce[nbuf][w][1] = CR[s2];
-      us[nbuf][w][lane] = Ua;
+      if (needU1) us[nbuf][w][lane] = Ua; // the edge waves' u1 is never read
       __syncthreads();
       buf = nbuf;
       // 5. the u1 window (computed values: plain moves)
@@ -524,7 +524,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         cs[nbuf][w][h][lane] = C[s2][h];
-        us[nbuf][w][h][lane] = Ua[h];
+        if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
       }
       __syncthreads();
       buf = nbuf;
@@ -773,7 +773,8 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
       const int nbuf = buf ^ 1;
       publish_src(nbuf, s2);
 #pragma unroll
-      for (int h = 0; h < H; ++h) us[nbuf][w][h][lane] = Ua[h];
+      for (int h = 0; h < H; ++h)
+        if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
       __syncthreads();
       buf = nbuf;
 #pragma unroll
