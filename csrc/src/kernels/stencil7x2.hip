@@ -332,13 +332,23 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   const int w = int(threadIdx.y);
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
   uint32_t s, e, s2 = 0, e2 = 0;
+  int qodd = -1; // lockstep quarter-major: z direction by quarter parity
   if (a.seg == 2) {
     // lockstep: four blocks per column (quarters of the z range) for the first nb/4 columns, so y-adjacent blocks
     // (4 apart, one XCD after the remap) march the same planes together and their shared y-halo rows meet in L2;
     // the columns left over (grids of fewer than 4 x columns blocks) spread over all blocks as short second segments
-    const uint32_t cm = nb / 4, col = lb / 4, qq = lb % 4;
+    const uint32_t cm = nb / 4;
+    uint32_t col, qq;
+    if (a.seg2q) { // quarter-major: consecutive blocks (one XCD after the remap) take y-adjacent columns of one
+      qq = lb / cm; //   quarter, so an XCD's blocks share every interior y-halo row through its L2
+      col = lb % cm;
+    } else {
+      col = lb / 4;
+      qq = lb % 4;
+    }
     s = col * nzt + qq * nzt / 4;
     e = col * nzt + (qq + 1) * nzt / 4;
+    if (a.seg2q) qodd = int(qq & 1);
     const uint64_t LW = uint64_t(uint32_t(a.gy) - cm) * nzt;
     s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
     e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
@@ -351,7 +361,9 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
     s = col * nzt + (lb % uint32_t(a.gz)) * uint32_t(a.zc);
     e = min(s + uint32_t(a.zc), (col + 1) * nzt);
   }
-  bool odd = a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0;
+  // z-march direction alternates between neighbouring segments (their shared boundary planes meet in cache); in the
+  // quarter-major lockstep order it alternates by quarter, so y-adjacent blocks march together
+  bool odd = qodd >= 0 ? qodd != 0 : (a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0);
   for (int pass = 0; pass < 2; ++pass) {
   if (pass == 1) {
     s = s2;
@@ -1131,6 +1143,11 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     if (lockstep && q4 >= 4 && q4 / 4 <= cols && nz >= 64) {
       a.seg = 2;
       blocks = uint32_t(q4);
+      static const int qmajor = [] {
+        const char *e = std::getenv("STENCIL_X2_QMAJOR");
+        return e == nullptr || std::atoi(e) != 0 ? 1 : 0;
+      }();
+      a.seg2q = qmajor;
     }
   } else {
     int zc = tune.zchunk;
