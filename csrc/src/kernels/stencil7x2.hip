@@ -1431,7 +1431,7 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
   // z slabs (whole x-y planes) of periodic 512-cell rows: the whole-row kernel, one block per 8 output rows of a
   // slab (fixed z chunk = the slab: every block marches only its slab's planes)
   bool zDone = false;
-  const char *zr = std::getenv("STENCIL_ZSLAB_ROW");
+  const char *zr = std::getenv("STENCIL_ZSLAB_ROW"); // read per call: tests switch it within one process
   if (f32 && tune.x2row && (tune.wrap & 1) && (zr == nullptr || std::atoi(zr) != 0) && lo.z <= 4 && hi.z <= 4) {
     StencilTune tz = tune;
     tz.x2sched = 0;
