@@ -70,7 +70,7 @@ struct StencilTune {
   bool nontemporal = true;
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous
   // step wrote last, which are still in the MALL / L2
-  bool alternateZ = true;
+  bool alternateZ = false; // r2s3: with lockstep quarters the per-step flip costs the fused pairs 3 % (1164 vs 1202)
   // bitmask of axes (1 = x, 2 = y, 4 = z) along which the sub-domain is its own periodic
   // neighbour and the kernels read the periodic image in place of the halo (StencilModel sets it together with
   // DistributedDomain::exchange_async(.., skipWrapped), which then skips those same-GPU self copies). Needs the
