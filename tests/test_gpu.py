@@ -473,7 +473,8 @@ def test_temporal2_overlapped_zslab_row_kernel(st, monkeypatch, zrow, mode, size
 
 @pytest.mark.parametrize("fake,reserve,lockstep", [(None, 8, "1"), ("4", 8, "1"), ("4", 4, "1"), ("4", 8, "0"),
                                                     ("6", 8, "1")])
-def test_temporal2_row_kernel_lockstep_quarters(st, monkeypatch, fake, reserve, lockstep):
+@pytest.mark.parametrize("alt", [False, True])
+def test_temporal2_row_kernel_lockstep_quarters(st, monkeypatch, fake, reserve, lockstep, alt):
     """Whole-row fused pairs over 64 row groups: the lockstep schedule (four blocks per column for the first
     blocks/4 columns, the rest as short second segments: 256 / 248 / 252 resident blocks) and the balanced one are
     bitwise equal to single steps (Astaroth proxy: no spheres, any grid thickness)."""
@@ -483,6 +484,7 @@ def test_temporal2_row_kernel_lockstep_quarters(st, monkeypatch, fake, reserve, 
         monkeypatch.setenv("STENCIL_FAKE_REMOTE_AXES", fake)
     t = st.StencilTune()
     t.x2reserve = reserve
+    t.alternate_z = alt  # per-step z-direction flip (off by default)
     m = st.AstarothSim((512, 512, 72), quantities=1, gpus=[0], temporal=2, tune=t, axis_cost=(64, 3, 2))
     m.init()
     assert m.temporal_blocking() and m.overlapping() == bool(fake)
