@@ -62,8 +62,16 @@ def run_ranks(n, script, args=(), env_extra=None, per_rank_env=None, timeout=240
         try:
             out, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
+            # report where every rank was (its output so far) instead of a bare timeout
             for q in procs:
                 q.kill()
-            raise
+            tails = []
+            for r, q in enumerate(procs):
+                try:
+                    o, _ = q.communicate(timeout=10)
+                except Exception:  # noqa: BLE001
+                    o = "<no output>"
+                tails.append(f"--- rank {r} (rc {q.returncode}) ---\n{(o or '')[-2000:]}")
+            raise AssertionError(f"ranks timed out after {timeout} s\n" + "\n".join(tails))
         outs.append((p.returncode, out))
     return outs

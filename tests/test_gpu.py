@@ -627,9 +627,9 @@ def test_ipc_probe_failure_falls_back_on_shared_gpu():
 @pytest.mark.parametrize("methods", ["Colocated|Kernel", "Staged|Kernel"])
 def test_race_canary_two_ranks_one_gpu(methods):
     """Race canary over HIP IPC (double-buffered inboxes + credits) and the staged path, with jitter."""
-    outs = run_ranks(2, WORKER, ["canary", "fec", "20,12,10"],
+    outs = run_ranks(2, WORKER, ["canary", "fec", "20,12,10"],  # ~2.5 s normally; 90 s: rank outputs on a hang
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20",
-                                "STENCIL_JITTER_US": "200"})
+                                "STENCIL_JITTER_US": "200"}, timeout=90)
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 
