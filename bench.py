@@ -210,7 +210,7 @@ def main():
         k = max(2, args.tune_steps // 2 * 2)
         r0 = args.x2reserve
         # (mode, CUs left to the transports): 1 = slabs beside the sweep, 2 = slabs after it, 0 = whole-region pairs
-        cands = [(1, r0), (1, 2 * r0), (2, r0), (0, r0)]
+        cands = [(1, r0), (1, max(1, r0 // 2)), (1, 2 * r0), (2, r0), (0, r0)]
         for c in cands + cands:
             model.set_overlap_mode(c[0])
             model.set_comm_reserve(c[1])
