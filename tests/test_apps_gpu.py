@@ -64,3 +64,24 @@ def test_bench_alltoallv_and_measure_buf_exchange():
     assert re.findall(r"^[a-zA-Z0-9_+-]+,1,\d+,", out, re.M), out[-2000:]
     out = run_app("measure_buf_exchange", "--rounds", 2, "--target-ms", 0.5)
     assert re.search(r"^round \d+: 0>0 [0-9.]+ms/[0-9.]+MiB", out, re.M), out[-2000:]
+
+
+def test_bench_py_json_contract():
+    """bench.py on one GPU prints one JSON line with the driver's fields (exact 512^3 grid, temporal pairs)."""
+    import json
+    import sys
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "4", "--warmup", "2",
+                        "--exchange-iters", "2"], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=100, cwd=REPO)
+    assert p.returncode == 0, p.stdout[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2 and d["value"] > 0
+    assert d["config"]["grid"] == [512, 512, 512] and d["config"]["temporal"] == 2
