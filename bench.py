@@ -83,6 +83,16 @@ def main():
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU, and then "
                          "overlapped or whole-region pairs, whichever runs faster in the warm-up)")
+    ap.add_argument("--colo-copy", choices=["auto", "store", "engine"], default="auto",
+                    help="co-located (HIP IPC) halos: the pack kernel stores into the peer's inbox (store), or a DMA "
+                         "engine copies the packed message (engine); auto: both tried in the warm-up")
+    ap.add_argument("--inbox", choices=["uncached", "fine", "coarse"], default="uncached",
+                    help="memory of the co-located receive slots (TransportOptions.inbox)")
+    ap.add_argument("--completion", choices=["kernel", "streamop"], default="kernel",
+                    help="co-located arrival/credit signalling: bounded spin kernels or hipStreamWait/WriteValue64")
+    ap.add_argument("--self-test", type=int, default=1,
+                    help="multi-process: verify the transports on a probe domain first and fall back along "
+                         "Colocated -> Rccl -> Staged until every halo arrives correctly")
     ap.add_argument("--tune-steps", type=int, default=8,
                     help="steps per timed round of the overlap choice (auto, remote halos only; 0 = no choice)")
     args = ap.parse_args()
@@ -126,50 +136,17 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # Transport pre-flight (multi-process only): one exchange of a coordinate-encoded field on a small grid with the
-    # model's radius and methods, checked cell by cell on every rank (the reference tests' oracle). If any rank sees
-    # a wrong halo or an error, every rank drops the co-located IPC path and uses RCCL instead, so a scaling run
-    # never times silently corrupted halos.
-    preflight = "skipped"
-    if world > 1:
-        from stencil2_amd.utils.testing import check_exchange, fill_coords
-
-        bad = 0
-        try:
-            pl = st.DistributedDomain(*(3 * [max(24, L // 8)]), group=pg)
-            r = st.Radius.constant(0)
-            r.set_face(2 if args.temporal >= 2 else 1)
-            if args.temporal >= 2:
-                r.set_edge(1)
-            pl.set_radius(r)
-            pl.set_axis_cost(st.Dim3(*(int(v) for v in args.axis_cost.split(","))))  # the model's decomposition
-            q = pl.add_data("coords", torch.int32)
-            pl.set_methods(methods)
-            pl.set_gpus([device])
-            pl.realize()
-            for it in range(2):
-                fill_coords(pl, q, offset=it)
-                pl.exchange()
-                torch.cuda.synchronize()
-                bad += check_exchange(pl, q, r, offset=it)
-            del pl
-        except Exception as e:  # noqa: BLE001 - any failure means: do not trust this transport set
-            print(f"rank {rank}: transport pre-flight failed: {e}", file=sys.stderr, flush=True)
-            bad += 1 << 20
-        if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # exercises the fallback (rehearsal scripts)
-            bad += 1
-        tb = torch.tensor([bad], dtype=torch.int64, device=red_dev)
-        dist.all_reduce(tb, op=dist.ReduceOp.SUM)
-        if int(tb.item()) == 0:
-            preflight = "ok"
-        else:
-            preflight = f"failed ({int(tb.item())} bad cells); colocated disabled"
-            methods = st.MethodFlags(int(methods) & ~int(st.MethodFlags.Colocated))
-            if shared:  # ranks sharing a GPU (rehearsal): RCCL refuses two ranks on one device
-                methods = st.MethodFlags(int(methods) & ~int(st.MethodFlags.Rccl) | int(st.MethodFlags.Staged))
-            if rank == 0:
-                print(f"transport pre-flight: {preflight}", file=sys.stderr, flush=True)
-        barrier()
+    # Transport self-test (multi-process only, DistributedDomain::set_self_test, run inside realize): a
+    # coordinate-encoded field on a small probe domain with the model's radius, placement and transports is exchanged
+    # and checked cell by cell on every rank; any wrong halo or error drops Colocated, then Rccl (host-staged), so a
+    # scaling run never times silently corrupted halos. An RCCL communicator that fails to form falls back to the
+    # host-staged path on every rank as well.
+    topt = st.TransportOptions()
+    topt.inbox = {"uncached": topt.Inbox.Uncached, "fine": topt.Inbox.Fine, "coarse": topt.Inbox.Coarse}[args.inbox]
+    topt.colo_copy = topt.Copy.Engine if args.colo_copy == "engine" else topt.Copy.Store
+    topt.completion = topt.Completion.StreamOp if args.completion == "streamop" else topt.Completion.Kernel
+    if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # rehearses the fallback (scripts): IPC probe reports failure
+        topt.fail_ipc_probe = True
 
     tune = st.StencilTune()
     tune.nontemporal = bool(args.nt)
@@ -187,8 +164,12 @@ def main():
     overlap = not args.no_overlap and args.overlap != "off"
     model = st.Jacobi3D(grid, gpus=[device], methods=methods, overlap=overlap,
                         auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
-                        axis_cost=axis_cost, wrap_self=bool(args.wrap))
+                        axis_cost=axis_cost, wrap_self=bool(args.wrap), transport=topt,
+                        self_test=bool(args.self_test) and world > 1)
     model.init()
+    methods = model.domain.methods()
+    preflight = model.domain.self_test_report() or "skipped"
+    colo = model.domain.exchange_bytes_for_method(st.MethodFlags.Colocated) > 0
     model.prepare()  # hipGraph capture + instantiation (no steps run) outside the timed region
     model.run(args.warmup)
     model.synchronize()
@@ -209,22 +190,33 @@ def main():
         best = {}
         k = max(2, args.tune_steps // 2 * 2)
         r0 = args.x2reserve
-        # (mode, CUs left to the transports): 1 = slabs beside the sweep, 2 = slabs after it, 0 = whole-region pairs
-        cands = [(1, r0), (1, max(1, r0 // 2)), (1, 2 * r0), (2, r0), (0, r0)]
-        for c in cands + cands:
+        # (mode, CUs left to the transports, co-located copy): mode 1 = slabs beside the sweep, 2 = slabs after
+        # it, 0 = whole-region pairs; copy "s" = pack kernel stores into the peer inbox, "e" = DMA engine copy (the
+        # transports then need fewer CUs: also tried with a quarter of the reserve)
+        copies = ["s", "e"] if colo and args.colo_copy == "auto" else ["e" if args.colo_copy == "engine" else "s"]
+        cands = []
+        for cp in copies:
+            cands += [(1, r0, cp), (1, max(1, r0 // 2), cp), (1, 2 * r0, cp), (2, r0, cp), (0, r0, cp)]
+            if cp == "e":
+                cands.append((1, max(1, r0 // 4), cp))
+
+        def apply(c):
             model.set_overlap_mode(c[0])
             model.set_comm_reserve(c[1])
+            model.domain.set_colo_copy(topt.Copy.Engine if c[2] == "e" else topt.Copy.Store)
+
+        for c in cands + cands:
+            apply(c)
             model.run(2)
             model.synchronize()
             best[c] = min(best.get(c, float("inf")), timed_run(k))
         choice = min(cands, key=lambda c: best[c])
-        model.set_overlap_mode(choice[0])
-        model.set_comm_reserve(choice[1])
+        apply(choice)
         model.run(2)
         model.synchronize()
         barrier()
-        overlap_tuned = {"mode": choice[0], "reserve": choice[1],
-                         **{f"m{c[0]}_r{c[1]}_ms": round(best[c], 4) for c in cands}}
+        overlap_tuned = {"mode": choice[0], "reserve": choice[1], "colo_copy": "engine" if choice[2] == "e" else "store",
+                         **{f"m{c[0]}_r{c[1]}_{c[2]}_ms": round(best[c], 4) for c in cands}}
     t0 = time.perf_counter()
     model.run(args.steps)  # every step is enqueued; whole blocks of steps replay as one hipGraph where possible
     model.synchronize()
@@ -281,7 +273,10 @@ def main():
                                                                    model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
                        "overlap": model.overlapping(), "overlap_tuned": overlap_tuned, "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
                        "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
-                       "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none"},
+                       "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none",
+                       "transport": {"inbox": args.inbox, "colo_copy": str(model.domain.transport_options().colo_copy).split(".")[-1].lower(),
+                                     "completion": args.completion},
+                       "build": st.build_info()["git_sha"]},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
                       "gcells_per_gpu": round(gcells / n, 3)},

@@ -1,13 +1,12 @@
 // Point-to-point ping-pong between rank pairs. Parity: reference bin/pingpong.cu (2^min..2^max bytes split over
 // concurrent pairs; host-memory MPI). Here: --host uses the native TCP process group (host memory); default uses
 // RCCL ncclSend/ncclRecv on device buffers over xGMI between rank r and r + size/2.
-#include <rccl/rccl.h>
-
 #include <chrono>
 #include <cstdio>
 #include <vector>
 
 #include "stencil/comm/proc_group.hpp"
+#include "stencil/comm/rccl_comm.hpp"
 #include "stencil/rt/argparse.hpp"
 #include "stencil/rt/hip_check.hpp"
 #include "stencil/topo/gpu_topology.hpp"
@@ -30,16 +29,31 @@ int main(int argc, char **argv) {
   const int half = n / 2;
   const int peer = r < half ? r + half : r - half;
   const bool leader = r < half;
-  ncclComm_t nc = nullptr;
+  rccl::Comm nc = nullptr;
   hipStream_t s = nullptr;
+  auto check = [&](const std::string &e) {
+    if (!e.empty()) LOG_FATAL("rank " << r << ": " << e);
+  };
   if (!host) {
     const int dev = pg->colocated_rank() % std::max(1, gpu_topo::device_count());
     HIP_CHECK(hipSetDevice(dev));
     HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    ncclUniqueId id;
-    if (r == 0) ncclGetUniqueId(&id);
-    pg->bcast(&id, sizeof(id), 0);
-    if (ncclCommInitRank(&nc, n, id, r) != ncclSuccess) LOG_FATAL("ncclCommInitRank failed");
+    rccl::UniqueId id{};
+    struct {
+      int ok;
+      rccl::UniqueId id;
+    } boot{1, {}};
+    std::string e;
+    if (r == 0) {
+      e = rccl::get_unique_id(&boot.id);
+      boot.ok = e.empty();
+    }
+    pg->bcast(&boot, sizeof(boot), 0);
+    if (!boot.ok) LOG_FATAL("RCCL unique id on rank 0 failed" << (e.empty() ? "" : ": " + e));
+    id = boot.id;
+    std::vector<rccl::Comm> comms;
+    check(rccl::init_ranks(&comms, n, id, {r}, {dev}));
+    nc = comms[0];
   }
   if (r == 0) std::printf("mode,bytes,pairs,one_way_s,GBps_per_pair\n");
   for (int lp = minP; lp <= maxP; ++lp) {
@@ -58,11 +72,11 @@ int main(int argc, char **argv) {
         }
       } else {
         if (leader) {
-          ncclSend(dbuf, bytes, ncclUint8, peer, nc, s);
-          ncclRecv(dbuf, bytes, ncclUint8, peer, nc, s);
+          check(rccl::send(dbuf, bytes, peer, nc, s));
+          check(rccl::recv(dbuf, bytes, peer, nc, s));
         } else {
-          ncclRecv(dbuf, bytes, ncclUint8, peer, nc, s);
-          ncclSend(dbuf, bytes, ncclUint8, peer, nc, s);
+          check(rccl::recv(dbuf, bytes, peer, nc, s));
+          check(rccl::send(dbuf, bytes, peer, nc, s));
         }
         HIP_CHECK(hipStreamSynchronize(s));
       }
@@ -76,6 +90,6 @@ int main(int argc, char **argv) {
     if (r == 0) std::printf("%s,%zu,%d,%e,%.3f\n", host ? "tcp-host" : "rccl-device", bytes, half, oneWay, bytes / oneWay / 1e9);
     if (dbuf) HIP_CHECK(hipFree(dbuf));
   }
-  if (nc) ncclCommDestroy(nc);
+  rccl::destroy(nc);
   return 0;
 }

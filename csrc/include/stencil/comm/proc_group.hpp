@@ -34,6 +34,16 @@ public:
 
   // collectives (every rank must call them in the same order)
   virtual void barrier() = 0;
+  // barrier that gives up after timeout_s (returns false; the group's collective sequence is then out of step, so
+  // only use it on the way out, e.g. in a destructor)
+  virtual bool barrier_for(double timeout_s) {
+    (void)timeout_s;
+    barrier();
+    return true;
+  }
+  // receive timeout of blocking recv / collectives (seconds)
+  virtual void set_timeout(double timeout_s) { (void)timeout_s; }
+  virtual double timeout() const { return 0; }
   virtual void bcast(void *buf, size_t n, int root) = 0;
   virtual void allgather(const void *in, size_t n, void *out) = 0;                           // out: size()*n bytes
   virtual void gatherv(const void *in, size_t n, std::vector<std::vector<char>> *out, int root) = 0; // root only

@@ -17,6 +17,7 @@
 // given to record_ready(); wait_exchange() makes a compute stream wait for the halos. exchange() keeps the
 // reference's blocking semantics.
 #include <array>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -65,6 +66,52 @@ struct PairInfo {
 // transport (the planner treats that as fatal).
 MethodFlags select_method(MethodFlags flags, const PairInfo &p);
 
+// Typed transport configuration (set before realize; the copy path and the completion method can also be switched
+// between exchanges with set_colo_copy / set_completion). Replaces the round-1/2 environment knobs.
+struct TransportOptions {
+  // Memory of a Colocated receiver's data slots (its arrival/credit flag words are always uncached):
+  //   Uncached  hipDeviceMallocUncached: every access bypasses the caches (coherent by construction; the unpack
+  //             reads the slots from HBM without L2 reuse)
+  //   Fine      hipDeviceMallocFinegrained: coherent at system scope, cached with the fine-grained MTYPE
+  //   Coarse    hipMalloc: L2-cached; relies on the kernel-boundary cache invalidate of the unpack's dispatch
+  enum class Inbox : int { Uncached = 0, Fine = 1, Coarse = 2 };
+  Inbox inbox = Inbox::Uncached;
+  // How a packed message reaches another GPU's memory (Colocated: the peer's IPC-mapped inbox; PeerCopy: the peer
+  // GPU's halo or receive buffer):
+  //   Store   the pack / translate kernel stores straight into the peer memory (CUs issue the xGMI writes)
+  //   Engine  pack into a local staging buffer, then hipMemcpyAsync(..., hipMemcpyDeviceToDeviceNoCU) / a peer
+  //           copy moves it on a DMA (SDMA) engine and the receiver unpacks (reference tx_cuda.cuh:141-162,
+  //           :270-283 use cudaMemcpyPeerAsync). Leaves the CUs to an overlapped interior sweep.
+  enum class Copy : int { Store = 0, Engine = 1 };
+  Copy coloCopy = Copy::Store;
+  Copy peerCopy = Copy::Store;
+  // Arrival / credit signalling of the Colocated transport:
+  //   Kernel    a one-wave kernel polls the flag word (bounded: stops after waitTimeout and reports) and a one-wave
+  //             kernel releases + stores it
+  //   StreamOp  hipStreamWaitValue64 / hipStreamWriteValue64 (the command processor waits; no CU is held, but the
+  //             wait itself is unbounded: sync_exchange's host watchdog reports a stall)
+  enum class Completion : int { Kernel = 0, StreamOp = 1 };
+  Completion completion = Completion::Kernel;
+  // seconds before a device-side spin, a host wait on a peer, or the RCCL watchdog gives up (<= 0: the
+  // STENCIL_WAIT_TIMEOUT environment variable, else 60)
+  double waitTimeout = 0;
+  // measurement hook: get_local_interior treats the faces of these axes (mask 1 = x, 2 = y, 4 = z) as remote, so
+  // one GPU runs the overlapped split of a multi-GPU decomposition (the exchange itself is unchanged)
+  int fakeRemoteAxes = 0;
+  // map every co-located rank's IPC block before planning (up to 3 attempts); Colocated is dropped on all ranks if
+  // any mapping fails. failIpcProbe forces that failure (rehearses the fallback).
+  bool ipcProbe = true;
+  bool failIpcProbe = false;
+  // test hook: RCCL communicator creation reports failure on this rank (rehearses the RCCL -> staged fallback)
+  bool failRcclInit = false;
+  // sleep a random 0..jitterUs microseconds between transport phases of every exchange (race canary; reference's
+  // unused rand_sleep(), packer.cuh:17-20)
+  int jitterUs = 0;
+};
+const char *to_string(TransportOptions::Inbox v);
+const char *to_string(TransportOptions::Copy v);
+const char *to_string(TransportOptions::Completion v);
+
 struct ExchangePlanEntry {
   MethodFlags method;
   Dim3 srcIdx, dstIdx;
@@ -110,6 +157,21 @@ public:
   // write plan_<rank>.txt during realize (reference src/stencil.cu:259-353); default on, off with STENCIL_PLAN_FILE=0
   void set_plan_file(const std::string &prefix) { planPrefix_ = prefix; }
   void set_padding(bool p) { pad_ = p; }
+  // opt-in self-test ladder run by realize() before planning (multi-rank runs): exchange a coordinate-encoded field
+  // on a small probe domain built like this one and check every halo cell on every rank; on any wrong cell or
+  // error drop Colocated, then Rccl (-> host-staged), i.e. the reference's always-terminating ladder
+  // (src/stencil.cu:163-194). methods() afterwards is the verified set; self_test_report() says what happened.
+  void set_self_test(bool on) { selfTest_ = on; }
+  const std::string &self_test_report() const { return selfTestReport_; }
+  // one probe: wrong halo cells summed over all ranks (0 = the transports of `m` deliver every halo correctly)
+  int64_t probe_transports(MethodFlags m);
+  // typed transport configuration (before realize)
+  void set_transport_options(const TransportOptions &o);
+  const TransportOptions &transport_options() const { return topt_; }
+  // switch how Colocated messages reach the peer inbox between exchanges (both paths are prepared by realize);
+  // waits for the exchanges in flight first
+  void set_colo_copy(TransportOptions::Copy c);
+  void set_completion(TransportOptions::Completion c);
 
   void realize();
   bool realized() const { return realized_; }
@@ -170,6 +232,12 @@ public:
   void wait_translated(size_t di, hipStream_t s);
   // block the host until the last exchange is complete (checks device-side timeouts)
   void sync_exchange();
+  // block the host until `streams` (e.g. compute streams that joined the exchange) and the last exchange are
+  // complete, polling instead of blocking: a transport error (RCCL asynchronous error, device-side timeout word) or
+  // no progress within the wait timeout fails with the plan on stderr instead of hanging in hipStreamSynchronize
+  void sync_streams(const std::vector<hipStream_t> &streams);
+  // non-empty after a fatal exchange error (the domain refuses further exchanges)
+  const std::string &poisoned() const { return poisoned_; }
   hipStream_t comm_stream(size_t di) const;
   // confine the pack / unpack kernels of the off-GPU transports (not the same-device translate) to at most n
   // 1024-thread blocks, i.e. n CUs (0 = one block per work item, the whole GPU). Used while an overlapped compute
@@ -213,6 +281,14 @@ private:
   bool backendSet_ = false;
   bool realized_ = false;
   bool pad_ = true;
+  TransportOptions topt_;
+  bool selfTest_ = false;
+  std::string selfTestReport_;
+  // set when an exchange failed fatally (device wait timed out, RCCL error/timeout): every later exchange refuses to
+  // run instead of handing a torn-down transport to the GPU
+  std::string poisoned_;
+  void poison(const std::string &why);
+  void init_rccl(const std::function<bool(int, int)> &sharedDev); // realize(): communicator or staged fallback
   std::string planPrefix_ = "plan";
   std::unique_ptr<Placement> placement_;
   std::vector<LocalDomain> domains_;

@@ -66,6 +66,13 @@ struct StencilTune {
   // segment mode: the grid is that many blocks short of the resident slots); reserveCUs is what one launch uses
   int x2reserve = 8;
   int reserveCUs = 0;
+  // whole-row fused pairs with fewer resident blocks than 4 per row group (CUs reserved for the transports): four
+  // blocks per column march lockstep z quarters, so y-adjacent blocks share their halo rows in L2 (512^3 local
+  // interior beside the slab kernels 276 -> 252 us); false = the balanced (column, plane) split
+  bool x2lockstep = true;
+  // overlapped fused pairs: the z slabs of periodic 512-cell rows go through the whole-row kernel with the slab as its
+  // z chunk (true) or through the thin slab kernel (false); both time the same within 2 % (r2s3)
+  bool zslabRow = true;
   bool xcdRemap = true;
   bool nontemporal = true;
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous

@@ -56,6 +56,15 @@ struct StencilModelConfig {
   // pair, mostly the strided x faces). Single steps do the same when they do not overlap or forward (the
   // exchange then leaves out every self copy). Off: every halo is copied.
   bool wrapSelf = true;
+  int wrapAxesMask = 7;       // axes (1 = x, 2 = y, 4 = z) in-kernel wrap may use at most (experiments restrict it)
+  // overlapped single steps with remote halos sweep get_local_interior(1) during the transfers (false: the classic
+  // interior / exterior split of the reference, get_interior + get_exterior)
+  bool localInterior = true;
+  // overlapped fused pairs: where the slabs at the remote faces run at first (set_overlap_mode: 1 beside the
+  // interior sweep on the comm stream, 2 after it on the compute stream)
+  int overlapMode = 1;
+  TransportOptions transport; // DistributedDomain::set_transport_options
+  bool selfTest = false;      // DistributedDomain::set_self_test (multi-rank: verified transport ladder)
   bool setBackend = false;
   Backend backend = Backend::Device;
   StencilTune tune;

@@ -8,10 +8,12 @@
 #include <cstring>
 
 #include "stencil/comm/proc_group.hpp"
+#include "stencil/comm/rccl_comm.hpp"
 #include "stencil/domain/distributed_domain.hpp"
 #include "stencil/kernels/copy.hpp"
 #include "stencil/kernels/stencil_ops.hpp"
 #include "stencil/models/stencil_model.hpp"
+#include "stencil/rt/build_info.hpp"
 #include "stencil/rt/statistics.hpp"
 #include "stencil/topo/gpu_topology.hpp"
 #include "stencil/topo/partition.hpp"
@@ -448,6 +450,47 @@ PYBIND11_MODULE(_C, m) {
       .def("fill_bytes", &LocalDomain::fill_bytes);
 
   // ---------------- DistributedDomain ----------------
+  py::class_<TransportOptions> topt(m, "TransportOptions");
+  py::enum_<TransportOptions::Inbox>(topt, "Inbox")
+      .value("Uncached", TransportOptions::Inbox::Uncached)
+      .value("Fine", TransportOptions::Inbox::Fine)
+      .value("Coarse", TransportOptions::Inbox::Coarse);
+  py::enum_<TransportOptions::Copy>(topt, "Copy")
+      .value("Store", TransportOptions::Copy::Store)
+      .value("Engine", TransportOptions::Copy::Engine);
+  py::enum_<TransportOptions::Completion>(topt, "Completion")
+      .value("Kernel", TransportOptions::Completion::Kernel)
+      .value("StreamOp", TransportOptions::Completion::StreamOp);
+  topt.def(py::init<>())
+      .def_readwrite("inbox", &TransportOptions::inbox)
+      .def_readwrite("colo_copy", &TransportOptions::coloCopy)
+      .def_readwrite("peer_copy", &TransportOptions::peerCopy)
+      .def_readwrite("completion", &TransportOptions::completion)
+      .def_readwrite("wait_timeout", &TransportOptions::waitTimeout)
+      .def_readwrite("fake_remote_axes", &TransportOptions::fakeRemoteAxes)
+      .def_readwrite("ipc_probe", &TransportOptions::ipcProbe)
+      .def_readwrite("fail_ipc_probe", &TransportOptions::failIpcProbe)
+      .def_readwrite("fail_rccl_init", &TransportOptions::failRcclInit)
+      .def_readwrite("jitter_us", &TransportOptions::jitterUs)
+      .def("__repr__", [](const TransportOptions &o) {
+        return std::string("TransportOptions(inbox=") + to_string(o.inbox) + ", colo_copy=" + to_string(o.coloCopy) +
+               ", peer_copy=" + to_string(o.peerCopy) + ", completion=" + to_string(o.completion) +
+               ", wait_timeout=" + std::to_string(o.waitTimeout) + ")";
+      });
+  m.def("build_info", []() {
+    const BuildInfo &b = build_info();
+    py::dict d;
+    d["git_sha"] = b.gitSha;
+    d["use_rccl"] = b.useRccl;
+    d["setup_stats"] = b.setupStats;
+    d["exchange_stats"] = b.exchangeStats;
+    d["output_level"] = b.outputLevel;
+    d["offload_arch"] = b.offloadArch;
+    return d;
+  });
+  m.def("build_info_string", &build_info_string);
+  m.def("rccl_compiled", &rccl::compiled);
+
   py::class_<ExchangePlanEntry>(m, "ExchangePlanEntry")
       .def_readonly("method", &ExchangePlanEntry::method)
       .def_readonly("src_idx", &ExchangePlanEntry::srcIdx)
@@ -484,6 +527,15 @@ PYBIND11_MODULE(_C, m) {
       .def("backend", &DistributedDomain::backend)
       .def("set_plan_file", &DistributedDomain::set_plan_file)
       .def("set_padding", &DistributedDomain::set_padding)
+      .def("set_transport_options", &DistributedDomain::set_transport_options)
+      .def("transport_options", &DistributedDomain::transport_options)
+      .def("set_colo_copy", &DistributedDomain::set_colo_copy, py::call_guard<py::gil_scoped_release>())
+      .def("set_completion", &DistributedDomain::set_completion, py::call_guard<py::gil_scoped_release>())
+      .def("poisoned", &DistributedDomain::poisoned)
+      .def("set_self_test", &DistributedDomain::set_self_test)
+      .def("self_test_report", &DistributedDomain::self_test_report)
+      .def("probe_transports", &DistributedDomain::probe_transports, py::call_guard<py::gil_scoped_release>())
+      .def_readwrite("exchange_stats", &DistributedDomain::exchangeStats_)
       .def("realize", &DistributedDomain::realize, py::call_guard<py::gil_scoped_release>())
       .def("realized", &DistributedDomain::realized)
       .def("size", &DistributedDomain::size)
@@ -568,6 +620,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("x2sched", &StencilTune::x2sched)
       .def_readwrite("x2reserve", &StencilTune::x2reserve)
       .def_readwrite("wrap", &StencilTune::wrap)
+      .def_readwrite("x2lockstep", &StencilTune::x2lockstep)
+      .def_readwrite("zslab_row", &StencilTune::zslabRow)
       .def_readwrite("x2xfast", &StencilTune::x2xfast);
   py::class_<StencilModelConfig>(m, "StencilModelConfig")
       .def(py::init<>())
@@ -587,6 +641,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("forward", &StencilModelConfig::forward)
       .def_readwrite("temporal", &StencilModelConfig::temporal)
       .def_readwrite("wrap_self", &StencilModelConfig::wrapSelf)
+      .def_readwrite("wrap_axes_mask", &StencilModelConfig::wrapAxesMask)
+      .def_readwrite("local_interior", &StencilModelConfig::localInterior)
+      .def_readwrite("overlap_mode", &StencilModelConfig::overlapMode)
+      .def_readwrite("transport", &StencilModelConfig::transport)
+      .def_readwrite("self_test", &StencilModelConfig::selfTest)
       .def_property(
           "backend", [](const StencilModelConfig &c) { return c.backend; },
           [](StencilModelConfig &c, Backend b) {

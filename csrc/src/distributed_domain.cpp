@@ -3,10 +3,11 @@
 #include "stencil/domain/distributed_domain.hpp"
 
 #include <hip/hip_runtime_api.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -16,15 +17,17 @@
 #include <sstream>
 #include <thread>
 
+#include "stencil/comm/rccl_comm.hpp"
 #include "stencil/comm/tags.hpp"
+#include "stencil/rt/env.hpp"
 #include "stencil/rt/hip_check.hpp"
 #include "stencil/rt/trace.hpp"
 #include "stencil/topo/gpu_topology.hpp"
 
-#define NCCL_CHECK(stmt)                                                                                           \
+#define RCCL_CHECK(stmt)                                                                                           \
   do {                                                                                                             \
-    ncclResult_t _r = (stmt);                                                                                      \
-    if (_r != ncclSuccess) LOG_FATAL("RCCL error " << int(_r) << " (" << ncclGetErrorString(_r) << ") in `" #stmt "`"); \
+    const std::string _e = (stmt);                                                                                 \
+    if (!_e.empty()) LOG_FATAL("RCCL error (" << _e << ") in `" #stmt "`");                                        \
   } while (0)
 
 namespace stencil {
@@ -124,9 +127,11 @@ struct Channel {
   char *dbuf = nullptr; // device staging buffer (Rccl, Staged)
   char *hbuf = nullptr; // pinned host (Staged, device backend)
   std::vector<char> hostBuf; // host backend
-  // Colocated (IPC)
-  char *ownBlock = nullptr;    // recv: [arrived flag | slot0 | slot1]; send: [credit flag]
-  char *remoteBlock = nullptr; // opened IPC mapping of the peer's block
+  // Colocated (IPC): the receiver owns a flag block [arrived word] and a data block [slot0 | slot1] (memory kind
+  // TransportOptions::inbox), the sender a flag block [credit word]; flag blocks are always uncached. remote* are
+  // the opened IPC mappings of the peer's blocks. Engine copies stage the packed message in dbuf (sender's GPU).
+  char *ownFlag = nullptr, *ownData = nullptr;
+  char *remoteFlag = nullptr, *remoteData = nullptr;
   int64_t slotStride = 0;
 };
 
@@ -141,9 +146,10 @@ struct DevCtx {
   std::set<int> peerWriters;      // devices whose translate writes into this device
   std::vector<int> coloSend, coloRecv, rcclSend, rcclRecv, stagedSend, stagedRecv;
   SegList coloPack, coloUnpack;   // variant = parity*2 + slot
+  SegList coloPackLocal;          // Engine copies: pack into the channels' local staging buffers (variant = parity)
   SegList rcclPack, rcclUnpack;   // variant = parity
   SegList stagedPack, stagedUnpack;
-  ncclComm_t nccl = nullptr;
+  rccl::Comm nccl = nullptr;
 };
 
 struct DistributedDomain::Impl {
@@ -155,7 +161,6 @@ struct DistributedDomain::Impl {
   uint64_t epoch = 0;
   int *errHost = nullptr; // host-mapped timeout word
   int *errDev = nullptr;
-  double waitTimeout = 60.0;
   // host backend
   SegList hostTranslate, hostStagedPack, hostStagedUnpack;
   bool rccl = false;
@@ -167,6 +172,7 @@ struct DistributedDomain::Impl {
   Event callerDone;
   bool callerPending = false; // callerDone marks a caller-stream exchange not yet joined by sync_exchange
   bool commPending = false;   // the comm stream holds an exchange (devs[0].done) a caller stream has not waited for
+  bool engineRefused = false; // hipMemcpyDeviceToDeviceNoCU not accepted by the runtime (warned once)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -175,45 +181,73 @@ struct DistributedDomain::Impl {
 DistributedDomain::DistributedDomain(int64_t x, int64_t y, int64_t z, std::shared_ptr<comm::ProcGroup> pg)
     : size_(x, y, z), pg_(pg ? pg : comm::default_group()), impl_(new Impl) {
   radius_ = Radius::constant(0);
-  if (const char *e = std::getenv("STENCIL_EXCHANGE_STATS")) exchangeStats_ = std::atoi(e) != 0;
-  if (const char *e = std::getenv("STENCIL_PLAN_FILE"))
-    if (std::atoi(e) == 0) planPrefix_.clear();
-  if (const char *e = std::getenv("STENCIL_WAIT_TIMEOUT")) impl_->waitTimeout = std::atof(e);
+#ifdef STENCIL_EXCHANGE_STATS
+  exchangeStats_ = STENCIL_EXCHANGE_STATS != 0;
+#endif
+  topt_.waitTimeout = env_wait_timeout(60.0);
+  if (env::get_int("STENCIL_PLAN_FILE", 1) == 0) planPrefix_.clear();
+}
+
+void DistributedDomain::set_transport_options(const TransportOptions &o) {
+  STENCIL_REQUIRE(!realized_, "set_transport_options after realize");
+  topt_ = o;
+  if (topt_.waitTimeout <= 0) topt_.waitTimeout = env_wait_timeout(60.0);
+}
+
+void DistributedDomain::poison(const std::string &why) {
+  if (poisoned_.empty()) poisoned_ = why;
 }
 
 DistributedDomain::~DistributedDomain() {
   if (!impl_) return;
-  try {
-    for (auto &d : impl_->devs) {
-      (void)HIP_TRY(hipSetDevice(d.dev));
-      (void)HIP_TRY(hipStreamSynchronize(d.comm));
+  Impl &I = *impl_;
+  // a poisoned domain may have work stuck behind a dead peer: do not block on it (the process is going down)
+  if (poisoned_.empty()) {
+    try {
+      for (auto &d : I.devs) {
+        (void)HIP_TRY(hipSetDevice(d.dev));
+        (void)HIP_TRY(hipStreamSynchronize(d.comm));
+      }
+    } catch (...) {
     }
-  } catch (...) {
   }
-  for (auto &c : impl_->chans) {
+  for (auto &c : I.chans) {
     if (c.dbuf) (void)hipFree(c.dbuf);
     if (c.hbuf) (void)hipHostFree(c.hbuf);
-    if (c.remoteBlock) (void)hipIpcCloseMemHandle(c.remoteBlock);
+    if (c.remoteFlag) (void)hipIpcCloseMemHandle(c.remoteFlag);
+    if (c.remoteData) (void)hipIpcCloseMemHandle(c.remoteData);
   }
-  // make sure peers closed their mappings of our blocks before freeing them
+  // make sure peers closed their mappings of our blocks before freeing them; bounded, so a dead or stalled peer
+  // cannot hold this rank in its destructor (the blocks then simply stay allocated until the process exits)
+  bool peersDone = true;
   try {
-    if (realized_ && pg_->size() > 1) pg_->barrier();
+    if (realized_ && pg_->size() > 1) peersDone = pg_->barrier_for(topt_.waitTimeout);
   } catch (...) {
+    peersDone = false;
   }
-  for (auto &c : impl_->chans)
-    if (c.ownBlock) (void)hipFree(c.ownBlock);
-  for (auto &d : impl_->devs) {
+  for (auto &c : I.chans) {
+    if (!peersDone) break;
+    if (c.ownFlag) (void)hipFree(c.ownFlag);
+    if (c.ownData) (void)hipFree(c.ownData);
+  }
+  for (auto &d : I.devs) {
     d.translate.release();
     d.translateSkip.release();
     d.coloPack.release();
+    d.coloPackLocal.release();
     d.coloUnpack.release();
     d.rcclPack.release();
     d.rcclUnpack.release();
     d.stagedPack.release();
     d.stagedUnpack.release();
-    if (d.nccl) ncclCommDestroy(d.nccl);
+    if (d.nccl) {
+      if (poisoned_.empty())
+        rccl::destroy(d.nccl);
+      else
+        rccl::abort(d.nccl);
+    }
   }
-  if (impl_->errHost) (void)hipHostFree(impl_->errHost);
+  if (I.errHost) (void)hipHostFree(I.errHost);
 }
 
 int64_t DistributedDomain::add_data(int64_t elemSize, const std::string &name, DType dtype) {
@@ -242,6 +276,197 @@ static void build_translate(const LocalDomain &src, const LocalDomain &dst, cons
 }
 
 // ------------------------------------------------------------------------------------------------
+// transport self-test (opt-in): coordinate oracle on a probe domain, ladder Colocated -> Rccl -> Staged
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int32_t kProbePoison = -1;
+int32_t probe_key(int64_t gx, int64_t gy, int64_t gz, const Dim3 &L, int32_t offset) {
+  return int32_t((gx + L.x * (gy + L.y * gz)) % 1000000007) + offset;
+}
+} // namespace
+
+int64_t DistributedDomain::probe_transports(MethodFlags m) {
+  // same group, radius, boundary, placement, cut costs, devices, backend and transport options; every axis
+  // shrunk ~16x (at least 6 cells per stencil reach) so the probe is cheap but spans the same rank pairs
+  int64_t rmax = 1;
+  for (int i = 0; i < 27; ++i) rmax = std::max<int64_t>(rmax, radius_.dir(dir_from_index(i)));
+  auto shrink = [&](int64_t n) { return std::min<int64_t>(n, std::max<int64_t>((n + 15) / 16, 6 * rmax + 2)); };
+  DistributedDomain p(shrink(size_.x), shrink(size_.y), shrink(size_.z), pg_);
+  p.set_radius(radius_);
+  p.set_boundary(boundary_);
+  p.set_methods(m);
+  p.set_placement(strategy_);
+  p.set_axis_cost(axisCost_);
+  if (!gpus_.empty()) p.set_gpus(gpus_);
+  if (backendSet_) p.set_backend(backend_);
+  p.set_transport_options(topt_);
+  p.set_plan_file("");
+  p.add_data(4, "probe", DType::I32);
+  int64_t bad = 0;
+  try {
+    p.realize();
+    const Dim3 L = p.size();
+    for (int it = 0; it < 2; ++it) {
+      const int32_t off = 7 * it;
+      for (auto &d : p.domains_) {
+        const Dim3 raw = d.raw_size(), org = d.accessor_origin();
+        std::vector<int32_t> v(size_t(raw.flatten()), kProbePoison);
+        const Rect3 cr = d.get_compute_region();
+        for (int64_t z = 0; z < raw.z; ++z)
+          for (int64_t y = 0; y < raw.y; ++y)
+            for (int64_t x = 0; x < raw.x; ++x)
+              if (cr.contains(Dim3(org.x + x, org.y + y, org.z + z)))
+                v[size_t(x + raw.x * (y + raw.y * z))] = probe_key(org.x + x, org.y + y, org.z + z, L, off);
+        d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), true);
+        d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), false);
+      }
+      p.exchange();
+      for (auto &d : p.domains_) {
+        const Dim3 raw = d.raw_size(), org = d.accessor_origin();
+        const Rect3 cr = d.get_compute_region();
+        const auto bytes = d.region_to_host(Dim3(0, 0, 0), raw, 0, true);
+        const int32_t *got = reinterpret_cast<const int32_t *>(bytes.data());
+        for (int64_t z = 0; z < raw.z; ++z)
+          for (int64_t y = 0; y < raw.y; ++y)
+            for (int64_t x = 0; x < raw.x; ++x) {
+              const int64_t g[3] = {org.x + x, org.y + y, org.z + z};
+              const int64_t lo[3] = {cr.lo.x, cr.lo.y, cr.lo.z}, hi[3] = {cr.hi.x, cr.hi.y, cr.hi.z};
+              const int64_t n[3] = {L.x, L.y, L.z};
+              int dd[3];
+              bool crossesClosed = false;
+              for (int a = 0; a < 3; ++a) {
+                dd[a] = g[a] >= hi[a] ? 1 : (g[a] < lo[a] ? -1 : 0);
+                if ((g[a] < 0 || g[a] >= n[a]) &&
+                    !boundary_.face_periodic(a == 0 ? dd[a] : 0, a == 1 ? dd[a] : 0, a == 2 ? dd[a] : 0))
+                  crossesClosed = true;
+              }
+              const bool filled = (dd[0] == 0 && dd[1] == 0 && dd[2] == 0) ||
+                                  (radius_.dir(Dim3(dd[0], dd[1], dd[2])) != 0 && !crossesClosed);
+              const int32_t want =
+                  filled ? probe_key(((g[0] % n[0]) + n[0]) % n[0], ((g[1] % n[1]) + n[1]) % n[1],
+                                     ((g[2] % n[2]) + n[2]) % n[2], L, off)
+                         : kProbePoison;
+              bad += got[size_t(x + raw.x * (y + raw.y * z))] != want;
+            }
+      }
+      p.swap();
+    }
+  } catch (const std::exception &e) {
+    LOG_WARN("rank " << rank() << ": transport probe with " << to_string(m) << " failed: " << e.what());
+    bad += int64_t(1) << 40;
+  }
+  return int64_t(pg_->allreduce_sum_u64(uint64_t(bad)));
+}
+
+// ------------------------------------------------------------------------------------------------
+// RCCL communicator (or the host-staged fallback)
+// ------------------------------------------------------------------------------------------------
+void DistributedDomain::init_rccl(const std::function<bool(int, int)> &sharedDev) {
+  Impl &I = *impl_;
+  comm::ProcGroup &pg = *pg_;
+  const int myRank = pg.rank();
+  int64_t rcclChans = 0;
+  for (auto &c : I.chans) rcclChans += c.method == MethodFlags::Rccl;
+  if (pg.allreduce_sum_u64(uint64_t(rcclChans)) == 0) return;
+  TraceRange trr("rccl init");
+  // members: every (rank, device) whose GPU no other rank drives (pairs touching a shared GPU are staged)
+  const int nLocal = int(I.devs.size());
+  std::vector<int> counts(size_t(pg.size()));
+  pg.allgather(&nLocal, sizeof(int), counts.data());
+  int maxN = 0;
+  for (int c : counts) maxN = std::max(maxN, c);
+  std::vector<int> padded(size_t(maxN), -1), allDevs(size_t(maxN) * size_t(pg.size()));
+  for (int k = 0; k < nLocal; ++k)
+    if (!sharedDev(myRank, I.devs[size_t(k)].dev)) padded[size_t(k)] = I.devs[size_t(k)].dev;
+  pg.allgather(padded.data(), sizeof(int) * size_t(maxN), allDevs.data());
+  // RCCL rank of (rank r, slot k) = number of members before it
+  std::vector<int> ncclRankOf(allDevs.size(), -1);
+  int total = 0, root = -1;
+  for (int r = 0; r < pg.size(); ++r)
+    for (int k = 0; k < maxN; ++k)
+      if (allDevs[size_t(r) * size_t(maxN) + size_t(k)] >= 0) {
+        ncclRankOf[size_t(r) * size_t(maxN) + size_t(k)] = total++;
+        if (root < 0) root = r;
+      }
+  STENCIL_REQUIRE(root >= 0, "RCCL channels planned but no rank owns an exclusive GPU");
+
+  // every failure is collected and agreed on before anyone falls back, so no rank is left blocked in a
+  // communicator the others abandoned. The unique id travels with the root's status.
+  std::string why;
+  struct {
+    int ok;
+    rccl::UniqueId id;
+  } boot{1, {}};
+  if (myRank == root) {
+    why = rccl::get_unique_id(&boot.id);
+    boot.ok = why.empty();
+  }
+  pg.bcast(&boot, sizeof(boot), root);
+  int ok = boot.ok && !topt_.failRcclInit;
+  if (!boot.ok && why.empty()) why = "the root rank could not create an RCCL id";
+  if (topt_.failRcclInit) why = "TransportOptions::failRcclInit";
+  if (ok) {
+    // a communicator that never forms (a rank died between the bcast and here) blocks in RCCL itself: say so
+    // with the plan after the wait timeout instead of hanging silently
+    std::mutex mu;
+    std::condition_variable cv;
+    bool initDone = false;
+    std::thread watch([&] {
+      std::unique_lock<std::mutex> lk(mu);
+      if (!cv.wait_for(lk, std::chrono::duration<double>(topt_.waitTimeout), [&] { return initDone; }))
+        LOG_ERROR("RCCL communicator creation still running after " << topt_.waitTimeout << " s; plan:\n"
+                                                                      << plan_summary());
+    });
+    std::vector<int> ranks, devices, slots;
+    for (int k = 0; k < nLocal; ++k) {
+      const int nr = ncclRankOf[size_t(myRank) * size_t(maxN) + size_t(k)];
+      if (nr < 0) continue;
+      ranks.push_back(nr);
+      devices.push_back(I.devs[size_t(k)].dev);
+      slots.push_back(k);
+    }
+    std::vector<rccl::Comm> comms;
+    why = rccl::init_ranks(&comms, total, boot.id, ranks, devices);
+    for (size_t j = 0; j < slots.size(); ++j) I.devs[size_t(slots[j])].nccl = comms[j];
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      initDone = true;
+    }
+    cv.notify_all();
+    watch.join();
+    ok = why.empty();
+  }
+  if (!ok) LOG_WARN("rank " << myRank << ": RCCL unavailable (" << why << ")");
+  if (pg.allreduce_min_i64(ok) == 1) {
+    // translate remote (rank, device) into RCCL ranks
+    for (auto &c : I.chans) {
+      if (c.method != MethodFlags::Rccl) continue;
+      int peer = -1;
+      for (int k = 0; k < maxN; ++k)
+        if (allDevs[size_t(c.remoteRank) * size_t(maxN) + size_t(k)] == c.remoteDev)
+          peer = ncclRankOf[size_t(c.remoteRank) * size_t(maxN) + size_t(k)];
+      STENCIL_REQUIRE(peer >= 0, "RCCL peer device not found");
+      STENCIL_REQUIRE(I.devs[size_t(I.devIndex[c.localDev])].nccl != nullptr, "RCCL channel on a shared GPU");
+      c.ncclPeer = peer;
+    }
+    I.rccl = true;
+    return;
+  }
+  // fallback: every RCCL channel (and plan entry) becomes host-staged on every rank
+  for (auto &d : I.devs)
+    if (d.nccl) {
+      rccl::abort(d.nccl);
+      d.nccl = nullptr;
+    }
+  if (myRank == 0) LOG_WARN("RCCL communicator creation failed on some rank; RCCL halos are host-staged instead");
+  for (auto &c : I.chans)
+    if (c.method == MethodFlags::Rccl) c.method = MethodFlags::Staged;
+  for (auto &e : plan_)
+    if (e.method == MethodFlags::Rccl) e.method = MethodFlags::Staged;
+  flags_ = MethodFlags((int(flags_) & ~int(MethodFlags::Rccl)) | int(MethodFlags::Staged));
+}
+
+// ------------------------------------------------------------------------------------------------
 // realize
 // ------------------------------------------------------------------------------------------------
 void DistributedDomain::realize() {
@@ -251,16 +476,40 @@ void DistributedDomain::realize() {
   Impl &I = *impl_;
   comm::ProcGroup &pg = *pg_;
   const int myRank = pg.rank();
+  // setup timers (reference STENCIL_SETUP_STATS, stencil.cu:31-538): max over ranks, or local and collective-free
+  // when the option is compiled out
+  auto setup_time = [&](double local) { return STENCIL_SETUP_STATS ? pg.allreduce_max(local) : local; };
 
   if (!backendSet_) backend_ = gpu_topo::device_count() > 0 ? Backend::Device : Backend::Host;
   const bool dev = backend_ == Backend::Device;
+  if (selfTest_ && pg.size() > 1) {
+    // ladder: as configured -> without Colocated -> without Rccl (host-staged); the last rung always runs
+    TraceRange trs("transport self-test");
+    std::vector<MethodFlags> ladder{flags_};
+    if (flags_ && MethodFlags::Colocated) ladder.push_back(MethodFlags(int(ladder.back()) & ~int(MethodFlags::Colocated)));
+    if (ladder.back() && MethodFlags::Rccl)
+      ladder.push_back(MethodFlags((int(ladder.back()) & ~int(MethodFlags::Rccl)) | int(MethodFlags::Staged)));
+    std::ostringstream rep;
+    bool found = false;
+    for (size_t k = 0; k < ladder.size() && !found; ++k) {
+      const int64_t bad = probe_transports(ladder[k]);
+      rep << (k ? "; " : "") << to_string(ladder[k]) << ": " << (bad == 0 ? "ok" : std::to_string(bad) + " bad");
+      if (bad == 0) {
+        found = true;
+        flags_ = ladder[k];
+      }
+    }
+    selfTestReport_ = rep.str();
+    if (myRank == 0) LOG_INFO("transport self-test: " << selfTestReport_);
+    STENCIL_REQUIRE(found, "no transport set passed the self-test: " << selfTestReport_);
+  }
   if (dev) STENCIL_REQUIRE(gpu_topo::device_count() > 0, "Device backend requested but no GPU is visible");
 
   // ---- node topology / GPU selection (reference stencil.hpp:158-245) ----
   double t0 = now_s();
   const int coloSize = pg.colocated_size();
   const int coloRank = pg.colocated_rank();
-  timeMpiTopo_ = pg.allreduce_max(now_s() - t0);
+  timeMpiTopo_ = setup_time(now_s() - t0);
   t0 = now_s();
   if (gpus_.empty()) {
     if (dev) {
@@ -275,14 +524,14 @@ void DistributedDomain::realize() {
       gpus_ = {0};
     }
   }
-  timeNodeGpus_ = pg.allreduce_max(now_s() - t0);
+  timeNodeGpus_ = setup_time(now_s() - t0);
   t0 = now_s();
   if (dev) {
     for (int a : gpus_)
       for (int b : gpus_)
         if (a != b) gpu_topo::enable_peer(a, b);
   }
-  timePeerEn_ = pg.allreduce_max(now_s() - t0);
+  timePeerEn_ = setup_time(now_s() - t0);
 
   // ---- placement ----
   t0 = now_s();
@@ -296,7 +545,7 @@ void DistributedDomain::realize() {
       placement_.reset(new TrivialPlacement(size_, pg, gpus_));
     }
   }
-  timePlacement_ = pg.allreduce_max(now_s() - t0);
+  timePlacement_ = setup_time(now_s() - t0);
 
   // ---- local domains ----
   t0 = now_s();
@@ -313,12 +562,11 @@ void DistributedDomain::realize() {
                      << " device " << device);
   }
   for (auto &d : domains_) d.realize();
-  timeRealize_ = pg.allreduce_max(now_s() - t0);
+  timeRealize_ = setup_time(now_s() - t0);
 
   // ---- HIP-IPC pre-flight: every rank maps a small uncached block of every co-located rank and reads it back.
   // If any mapping fails anywhere, Colocated is disabled on all ranks (they then agree on RCCL/staged). ----
-  if (dev && any_methods(MethodFlags::Colocated) && pg.size() > 1 && pg.colocated_size() > 1 &&
-      std::getenv("STENCIL_SKIP_IPC_PROBE") == nullptr) {
+  if (dev && any_methods(MethodFlags::Colocated) && pg.size() > 1 && pg.colocated_size() > 1 && topt_.ipcProbe) {
     TraceRange trp("ipc probe");
     // up to 3 collective attempts with a growing pause between them (50, 200 ms): a transient open/map failure on a
     // busy node must not cost the transport. Every failed attempt logs the call that failed on this rank.
@@ -369,7 +617,7 @@ void DistributedDomain::realize() {
         }
         (void)hipIpcCloseMemHandle(peer);
       }
-      if (std::getenv("STENCIL_IPC_PROBE_FAIL")) { // rehearses the fallback (tests)
+      if (topt_.failIpcProbe) { // rehearses the fallback (tests)
         ok = 0;
         failed = "STENCIL_IPC_PROBE_FAIL";
       }
@@ -478,7 +726,6 @@ void DistributedDomain::realize() {
         int64_t bytes = 0;
         for (int64_t q = 0; q < domains_[di].num_data(); ++q) bytes += domains_[di].halo_bytes(-dir, q);
         plan_.push_back({m, myIdx, dstIdx, myRank, dstRank, myDev, dstDev, dir, bytes});
-        bytesPerMethod_[method_slot(m)] += uint64_t(bytes);
         if (m == MethodFlags::Kernel || m == MethodFlags::PeerCopy) {
           localTranslates.emplace_back(int(di), dstId, dir);
         } else {
@@ -549,13 +796,7 @@ void DistributedDomain::realize() {
     std::sort(c.msgs.begin(), c.msgs.end());
     c.bytes = packed_size(domains_[c.localDom], c.msgs);
   }
-  for (int s = 0; s < 5; ++s) bytesPerMethod_[s] = pg.allreduce_sum_u64(bytesPerMethod_[s]);
-  timePlan_ = pg.allreduce_max(now_s() - t0);
-
-  if (!planPrefix_.empty()) {
-    std::ofstream f(planPrefix_ + "_" + std::to_string(myRank) + ".txt");
-    f << plan_summary();
-  }
+  timePlan_ = setup_time(now_s() - t0);
 
   // ---- create transports ----
   t0 = now_s();
@@ -601,6 +842,11 @@ void DistributedDomain::realize() {
     *I.errHost = 0;
     HIP_CHECK(hipHostGetDevicePointer((void **)&I.errDev, I.errHost, 0));
 
+    // RCCL communicator over all (rank, device) pairs, created only if some rank needs it. An init error on any
+    // rank (or TransportOptions::failRcclInit) is agreed on collectively and every RCCL channel falls back to the
+    // host-staged transport (the reference's ladder also ends at the MPI path, src/stencil.cu:185-194).
+    init_rccl(shared_dev);
+
     // same-process direct stores
     I.localTranslates = localTranslates;
     for (const auto &t : localTranslates) {
@@ -624,38 +870,55 @@ void DistributedDomain::realize() {
         HIP_CHECK(hipMalloc(&c.dbuf, nb));
         (c.send ? ctx.rcclSend : ctx.rcclRecv).push_back(ci);
       } else if (c.method == MethodFlags::Colocated) {
-        // receiver owns [arrived flag (256 B) | slot0 | slot1] in uncached memory; sender owns [credit flag]
+        // flag words (arrival on the receiver, credit on the sender) in uncached memory: polled across processes
+        // and GPUs, written remotely
+        HIP_CHECK(hipExtMallocWithFlags((void **)&c.ownFlag, 256, hipDeviceMallocUncached));
+        HIP_CHECK(hipMemset(c.ownFlag, 0, 256));
         c.slotStride = round_up(int64_t(nb), 256);
-        const size_t blockBytes = c.send ? 256 : size_t(256 + 2 * c.slotStride);
-        hipError_t e = hipExtMallocWithFlags((void **)&c.ownBlock, blockBytes, hipDeviceMallocUncached);
-        if (e != hipSuccess) {
-          (void)hipGetLastError();
-          LOG_WARN("uncached allocation failed (" << hipGetErrorString(e) << "), using fine-grained memory");
-          HIP_CHECK(hipExtMallocWithFlags((void **)&c.ownBlock, blockBytes, hipDeviceMallocFinegrained));
+        if (!c.send) {
+          const size_t dataBytes = size_t(2 * c.slotStride);
+          switch (topt_.inbox) {
+          case TransportOptions::Inbox::Uncached:
+            HIP_CHECK(hipExtMallocWithFlags((void **)&c.ownData, dataBytes, hipDeviceMallocUncached));
+            break;
+          case TransportOptions::Inbox::Fine:
+            HIP_CHECK(hipExtMallocWithFlags((void **)&c.ownData, dataBytes, hipDeviceMallocFinegrained));
+            break;
+          case TransportOptions::Inbox::Coarse:
+            HIP_CHECK(hipMalloc((void **)&c.ownData, dataBytes));
+            break;
+          }
+          HIP_CHECK(hipMemset(c.ownData, 0, dataBytes));
+        } else {
+          HIP_CHECK(hipMalloc(&c.dbuf, nb)); // Engine copies: the packed message before the DMA copy
         }
-        HIP_CHECK(hipMemset(c.ownBlock, 0, blockBytes));
         (c.send ? ctx.coloSend : ctx.coloRecv).push_back(ci);
       }
     }
     HIP_CHECK(hipDeviceSynchronize());
 
-    // IPC handshake for colocated channels: every side sends its handle first (non-blocking), then receives
+    // IPC handshake for colocated channels: every side sends its handles first (non-blocking), then receives.
+    // receiver -> sender: {arrival flag block, data block}; sender -> receiver: {credit flag block}
     {
       TraceRange tri("ipc handshake");
       for (auto &c : I.chans) {
         if (c.method != MethodFlags::Colocated) continue;
-        hipIpcMemHandle_t h;
+        hipIpcMemHandle_t h[2] = {};
         HIP_CHECK(hipSetDevice(c.localDev));
-        HIP_CHECK(hipIpcGetMemHandle(&h, c.ownBlock));
-        pg.send(c.remoteRank, retag(c.tag, c.send ? comm::MsgKind::IpcCredit : comm::MsgKind::IpcInbox), &h, sizeof(h));
+        HIP_CHECK(hipIpcGetMemHandle(&h[0], c.ownFlag));
+        if (!c.send) HIP_CHECK(hipIpcGetMemHandle(&h[1], c.ownData));
+        pg.send(c.remoteRank, retag(c.tag, c.send ? comm::MsgKind::IpcCredit : comm::MsgKind::IpcInbox), h,
+                c.send ? sizeof(h[0]) : sizeof(h));
       }
       for (auto &c : I.chans) {
         if (c.method != MethodFlags::Colocated) continue;
-        hipIpcMemHandle_t h;
-        // a sender needs the receiver's inbox, a receiver the sender's credit block
-        pg.recv(c.remoteRank, retag(c.tag, c.send ? comm::MsgKind::IpcInbox : comm::MsgKind::IpcCredit), &h, sizeof(h));
+        hipIpcMemHandle_t h[2] = {};
+        // a sender needs the receiver's flag + data blocks, a receiver the sender's credit block
+        pg.recv(c.remoteRank, retag(c.tag, c.send ? comm::MsgKind::IpcInbox : comm::MsgKind::IpcCredit), h,
+                c.send ? sizeof(h) : sizeof(h[0]));
         HIP_CHECK(hipSetDevice(c.localDev));
-        HIP_CHECK(hipIpcOpenMemHandle((void **)&c.remoteBlock, h, hipIpcMemLazyEnablePeerAccess));
+        HIP_CHECK(hipIpcOpenMemHandle((void **)&c.remoteFlag, h[0], hipIpcMemLazyEnablePeerAccess));
+        if (c.send) HIP_CHECK(hipIpcOpenMemHandle((void **)&c.remoteData, h[1], hipIpcMemLazyEnablePeerAccess));
       }
       pg.barrier();
     }
@@ -665,16 +928,18 @@ void DistributedDomain::realize() {
       for (int ci : ctx.coloSend) {
         Channel &c = I.chans[ci];
         const LocalDomain &dom = domains_[c.localDom];
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < 2; ++p) {
           for (int slot = 0; slot < 2; ++slot)
-            build_pack(dom, c.msgs, c.remoteBlock + 256 + slot * c.slotStride, p == 0, ctx.coloPack.host[p * 2 + slot]);
+            build_pack(dom, c.msgs, c.remoteData + slot * c.slotStride, p == 0, ctx.coloPack.host[p * 2 + slot]);
+          build_pack(dom, c.msgs, c.dbuf, p == 0, ctx.coloPackLocal.host[p]);
+        }
       }
       for (int ci : ctx.coloRecv) {
         Channel &c = I.chans[ci];
         const LocalDomain &dom = domains_[c.localDom];
         for (int p = 0; p < 2; ++p)
           for (int slot = 0; slot < 2; ++slot)
-            build_unpack(dom, c.msgs, c.ownBlock + 256 + slot * c.slotStride, p == 0, ctx.coloUnpack.host[p * 2 + slot]);
+            build_unpack(dom, c.msgs, c.ownData + slot * c.slotStride, p == 0, ctx.coloUnpack.host[p * 2 + slot]);
       }
       for (int ci : ctx.rcclSend)
         for (int p = 0; p < 2; ++p)
@@ -691,6 +956,7 @@ void DistributedDomain::realize() {
                        ctx.stagedUnpack.host[p]);
       ctx.translate.upload(ctx.dev);
       ctx.coloPack.upload(ctx.dev);
+      ctx.coloPackLocal.upload(ctx.dev);
       ctx.coloUnpack.upload(ctx.dev);
       ctx.rcclPack.upload(ctx.dev);
       ctx.rcclUnpack.upload(ctx.dev);
@@ -702,56 +968,16 @@ void DistributedDomain::realize() {
       std::sort(ctx.rcclRecv.begin(), ctx.rcclRecv.end(), byKey);
     }
 
-    // RCCL communicator over all (rank, device) pairs, created only if some rank needs it
-    int64_t rcclChans = 0;
-    for (auto &c : I.chans) rcclChans += c.method == MethodFlags::Rccl;
-    if (pg.allreduce_sum_u64(uint64_t(rcclChans)) > 0) {
-      TraceRange trr("rccl init");
-      // members: every (rank, device) whose GPU no other rank drives (pairs touching a shared GPU are staged)
-      const int nLocal = int(I.devs.size());
-      std::vector<int> counts(pg.size());
-      pg.allgather(&nLocal, sizeof(int), counts.data());
-      int maxN = 0;
-      for (int c : counts) maxN = std::max(maxN, c);
-      std::vector<int> padded(size_t(maxN), -1), allDevs(size_t(maxN) * pg.size());
-      for (int k = 0; k < nLocal; ++k)
-        if (!shared_dev(myRank, I.devs[size_t(k)].dev)) padded[size_t(k)] = I.devs[size_t(k)].dev;
-      pg.allgather(padded.data(), sizeof(int) * size_t(maxN), allDevs.data());
-      // RCCL rank of (rank r, slot k) = number of members before it
-      std::vector<int> ncclRankOf(allDevs.size(), -1);
-      int total = 0, root = -1;
-      for (int r = 0; r < pg.size(); ++r)
-        for (int k = 0; k < maxN; ++k)
-          if (allDevs[size_t(r) * maxN + k] >= 0) {
-            ncclRankOf[size_t(r) * maxN + k] = total++;
-            if (root < 0) root = r;
-          }
-      STENCIL_REQUIRE(root >= 0, "RCCL channels planned but no rank owns an exclusive GPU");
-      ncclUniqueId id;
-      if (myRank == root) NCCL_CHECK(ncclGetUniqueId(&id));
-      pg.bcast(&id, sizeof(id), root);
-      NCCL_CHECK(ncclGroupStart());
-      for (int k = 0; k < nLocal; ++k) {
-        const int nr = ncclRankOf[size_t(myRank) * maxN + k];
-        if (nr < 0) continue;
-        HIP_CHECK(hipSetDevice(I.devs[size_t(k)].dev));
-        NCCL_CHECK(ncclCommInitRank(&I.devs[size_t(k)].nccl, total, id, nr));
-      }
-      NCCL_CHECK(ncclGroupEnd());
-      // translate remote (rank, device) into RCCL ranks
-      for (auto &c : I.chans) {
-        if (c.method != MethodFlags::Rccl) continue;
-        int peer = -1;
-        for (int k = 0; k < maxN; ++k)
-          if (allDevs[size_t(c.remoteRank) * maxN + k] == c.remoteDev) peer = ncclRankOf[size_t(c.remoteRank) * maxN + k];
-        STENCIL_REQUIRE(peer >= 0, "RCCL peer device not found");
-        STENCIL_REQUIRE(I.devs[size_t(I.devIndex[c.localDev])].nccl != nullptr, "RCCL channel on a shared GPU");
-        c.ncclPeer = peer;
-      }
-      I.rccl = true;
-    }
   }
-  timeCreate_ = pg.allreduce_max(now_s() - t0);
+  // bytes per method (after any RCCL -> staged fallback) and the plan file
+  bytesPerMethod_ = {};
+  for (const auto &e : plan_) bytesPerMethod_[size_t(method_slot(e.method))] += uint64_t(e.bytes);
+  for (int m = 0; m < 5; ++m) bytesPerMethod_[size_t(m)] = pg.allreduce_sum_u64(bytesPerMethod_[size_t(m)]);
+  if (!planPrefix_.empty()) {
+    std::ofstream f(planPrefix_ + "_" + std::to_string(myRank) + ".txt");
+    f << plan_summary();
+  }
+  timeCreate_ = setup_time(now_s() - t0);
   realized_ = true;
   pg.barrier();
 }
@@ -862,9 +1088,9 @@ std::vector<Rect3> DistributedDomain::get_local_interior(int reach) const {
     }
     // measurement knob: treat the faces of these axes (mask 1=x, 2=y, 4=z) as remote, so one GPU runs the split
     // (local interior during the transfers, slabs after) of a multi-GPU decomposition
-    if (const char *e = std::getenv("STENCIL_FAKE_REMOTE_AXES"))
+    if (topt_.fakeRemoteAxes != 0)
       for (int a = 0; a < 3; ++a)
-        if (std::atoi(e) >> a & 1)
+        if (topt_.fakeRemoteAxes >> a & 1)
           for (int s = 0; s < 2; ++s) {
             const Dim3 d(a == 0 ? 2 * s - 1 : 0, a == 1 ? 2 * s - 1 : 0, a == 2 ? 2 * s - 1 : 0);
             sh[a][s] = std::max<int64_t>(sh[a][s], std::min<int64_t>(reach, radius_.dir(d)));
@@ -946,70 +1172,112 @@ hipStream_t DistributedDomain::comm_stream(size_t di) const {
   return impl_->devs[impl_->devIndex.at(domains_.at(di).gpu())].comm;
 }
 
-void DistributedDomain::sync_exchange() {
+void DistributedDomain::sync_exchange() { sync_streams({}); }
+
+void DistributedDomain::sync_streams(const std::vector<hipStream_t> &extra) {
   if (backend_ != Backend::Device) return;
   Impl &I = *impl_;
-  if (I.rccl) {
-    // RCCL watchdog: poll the streams that carry RCCL work, check every communicator's asynchronous
-    // error, and give up after the wait timeout with the plan on stderr (a peer that died or never posted its
-    // matching send/recv would otherwise block here forever)
+  STENCIL_REQUIRE(poisoned_.empty(), "halo exchange unusable after an earlier failure: " << poisoned_);
+  auto fail = [&](const std::string &why) {
+    poison(why);
+    for (auto &d : I.devs)
+      if (d.nccl) {
+        rccl::abort(d.nccl);
+        d.nccl = nullptr;
+      }
+    I.rccl = false;
+    LOG_FATAL(why);
+  };
+  // Every device-side wait of the IPC path is bounded by default (spin kernels stop after waitTimeout and report
+  // through errHost), so a blocking synchronize always returns. RCCL operations and command-processor waits are
+  // not: then poll the streams, check every communicator's asynchronous error, and give up after the wait timeout
+  // with the plan on stderr (a peer that died or never posted its matching send/recv would otherwise block here
+  // forever) -- including the caller's compute streams, which join the exchange.
+  const bool unbounded = I.rccl || topt_.completion == TransportOptions::Completion::StreamOp;
+  if (unbounded) {
     const double t0 = now_s();
+    auto pending = [&](hipError_t q) {
+      if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        return true;
+      }
+      HIP_CHECK(q);
+      return false;
+    };
     auto done = [&]() {
-      bool all = true;
+      for (hipStream_t st : extra)
+        if (pending(hipStreamQuery(st))) return false;
       for (auto &d : I.devs) {
         HIP_CHECK(hipSetDevice(d.dev));
-        const hipError_t q = hipStreamQuery(d.comm);
-        if (q == hipErrorNotReady) {
-          (void)hipGetLastError();
-          all = false;
-        } else {
-          HIP_CHECK(q);
-        }
+        if (pending(hipStreamQuery(d.comm))) return false;
       }
-      if (I.callerPending) {
-        const hipError_t q = hipEventQuery(I.callerDone);
-        if (q == hipErrorNotReady) {
-          (void)hipGetLastError();
-          all = false;
-        } else {
-          HIP_CHECK(q);
-        }
-      }
-      return all;
+      return !(I.callerPending && pending(hipEventQuery(I.callerDone)));
     };
     while (!done()) {
       for (auto &d : I.devs) {
         if (!d.nccl) continue;
-        ncclResult_t r = ncclSuccess;
-        if (ncclCommGetAsyncError(d.nccl, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress) {
-          LOG_ERROR("RCCL asynchronous error on device " << d.dev << ": " << ncclGetErrorString(r) << "\n"
+        const std::string ae = rccl::async_error(d.nccl);
+        if (!ae.empty()) {
+          LOG_ERROR("RCCL " << ae << " error on device " << d.dev << "\n"
                                                           << plan_summary());
-          LOG_FATAL("halo exchange failed in RCCL (epoch " << I.epoch << ")");
+          fail("halo exchange failed in RCCL (epoch " + std::to_string(I.epoch) + ")");
         }
       }
-      if (now_s() - t0 > I.waitTimeout) {
-        LOG_ERROR("halo exchange still running after " << I.waitTimeout << " s (epoch " << I.epoch
+      if (*I.errHost) break; // a bounded device wait gave up: reported below
+      if (now_s() - t0 > topt_.waitTimeout) {
+        LOG_ERROR("halo exchange still running after " << topt_.waitTimeout << " s (epoch " << I.epoch
                                                         << "); plan:\n" << plan_summary());
-        for (auto &d : I.devs)
-          if (d.nccl) (void)ncclCommAbort(d.nccl), d.nccl = nullptr;
-        LOG_FATAL("halo exchange timed out in RCCL; a peer rank is stalled or dead");
+        fail("halo exchange timed out; a peer rank is stalled or dead");
       }
       std::this_thread::yield();
     }
   }
-  for (auto &d : I.devs) {
-    HIP_CHECK(hipSetDevice(d.dev));
-    HIP_CHECK(hipStreamSynchronize(d.comm));
-  }
-  if (I.callerPending) {
-    I.callerDone.sync();
-    I.callerPending = false;
+  if (!*I.errHost) {
+    for (hipStream_t st : extra) HIP_CHECK(hipStreamSynchronize(st));
+    for (auto &d : I.devs) {
+      HIP_CHECK(hipSetDevice(d.dev));
+      HIP_CHECK(hipStreamSynchronize(d.comm));
+    }
+    if (I.callerPending) {
+      I.callerDone.sync();
+      I.callerPending = false;
+    }
   }
   if (*I.errHost) {
     const int code = *I.errHost;
-    LOG_FATAL("halo exchange timed out waiting for a colocated peer (code " << code << ", epoch " << I.epoch
-                                                                           << "); a peer rank is stalled or dead");
+    LOG_ERROR("halo exchange timed out waiting for a colocated peer (" << (code == 1 ? "inbox credit" : "arrival")
+                                                                      << ", epoch " << I.epoch << "); plan:\n"
+                                                                      << plan_summary());
+    fail("halo exchange timed out waiting for a colocated peer; a peer rank is stalled or dead");
   }
+}
+
+void DistributedDomain::set_colo_copy(TransportOptions::Copy c) {
+  if (c == topt_.coloCopy) return;
+  if (realized_) sync_exchange(); // the staging buffers and inbox slots of the exchanges in flight
+  topt_.coloCopy = c;
+}
+
+void DistributedDomain::set_completion(TransportOptions::Completion c) {
+  if (c == topt_.completion) return;
+  if (realized_) sync_exchange(); // flag words are monotonic epochs: either method continues where the other left off
+  topt_.completion = c;
+}
+
+const char *to_string(TransportOptions::Inbox v) {
+  switch (v) {
+  case TransportOptions::Inbox::Uncached:
+    return "uncached";
+  case TransportOptions::Inbox::Fine:
+    return "fine";
+  case TransportOptions::Inbox::Coarse:
+    return "coarse";
+  }
+  return "?";
+}
+const char *to_string(TransportOptions::Copy v) { return v == TransportOptions::Copy::Engine ? "engine" : "store"; }
+const char *to_string(TransportOptions::Completion v) {
+  return v == TransportOptions::Completion::StreamOp ? "streamop" : "kernel";
 }
 
 void DistributedDomain::exchange() {
@@ -1060,6 +1328,7 @@ void DistributedDomain::prepare_skip_wrapped(int axes) {
 
 void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   STENCIL_REQUIRE(realized_, "exchange before realize");
+  STENCIL_REQUIRE(poisoned_.empty(), "halo exchange unusable after an earlier failure: " << poisoned_);
   TraceRange tr("DD::exchange()");
   Impl &I = *impl_;
   STENCIL_REQUIRE(skipAxes == 0 || backend_ == Backend::Host || skipAxes == I.skipAxes,
@@ -1127,12 +1396,37 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
 
   const int slot = int(I.epoch & 1);
   const int cv = parity * 2 + slot;
+  // Colocated completion (TransportOptions::completion): bounded spin / release kernels, or command-processor
+  // stream operations on the same flag words
+  const bool streamOps = topt_.completion == TransportOptions::Completion::StreamOp;
+  auto wait_flags = [&](const std::vector<uint64_t *> &flags, uint64_t target, int code, hipStream_t st) {
+    if (!streamOps) {
+      wait_flags_device(flags, target, I.errDev, code, topt_.waitTimeout, st);
+      return;
+    }
+    for (uint64_t *f : flags) HIP_CHECK(hipStreamWaitValue64(st, f, target, hipStreamWaitValueGte));
+  };
+  auto signal_flags = [&](const std::vector<uint64_t *> &flags, uint64_t value, hipStream_t st) {
+    if (!streamOps) {
+      signal_flags_device(flags, value, st);
+      return;
+    }
+    for (uint64_t *f : flags) HIP_CHECK(hipStreamWriteValue64(st, f, value, 0));
+  };
+  // DMA-engine copy (no CUs); falls back to an ordinary device copy if the runtime refuses the NoCU kind
+  auto engine_copy = [&](void *dst, const void *src, size_t n, hipStream_t st) {
+    if (!I.engineRefused) {
+      const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, st);
+      if (e == hipSuccess) return;
+      (void)hipGetLastError();
+      I.engineRefused = true;
+      LOG_WARN("hipMemcpyDeviceToDeviceNoCU refused (" << hipGetErrorString(e) << "); engine copies use hipMemcpyDeviceToDevice");
+    }
+    HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st));
+  };
   // STENCIL_JITTER_US=N: sleep a random 0..N us between transport phases (reference's unused rand_sleep(),
   // packer.cuh:17-20) to shake out ordering assumptions between ranks and streams
-  static const int jitterUs = [] {
-    const char *e = std::getenv("STENCIL_JITTER_US");
-    return e ? std::atoi(e) : 0;
-  }();
+  const int jitterUs = topt_.jitterUs;
   auto jitter = [&] {
     if (jitterUs > 0) std::this_thread::sleep_for(std::chrono::microseconds(std::rand() % (jitterUs + 1)));
   };
@@ -1148,21 +1442,34 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   }
 
   jitter();
-  // (2) colocated sends: wait for inbox credit (slot reuse distance 2), pack into the peer's inbox over xGMI,
-  //     then raise the peer's arrival flag
+  // (2) colocated sends: wait for inbox credit (slot reuse distance 2), move the packed message into the peer's
+  //     inbox over xGMI, then raise the peer's arrival flag.
+  //     Store:  the pack kernel stores straight into the IPC-mapped inbox slot.
+  //     Engine: pack into the local staging buffer (before the credit wait: it does not touch the inbox), then one
+  //             DMA-engine copy per channel into the slot, leaving the CUs to the compute sweep.
   for (auto &ctx : I.devs) {
     if (ctx.coloSend.empty()) continue;
     HIP_CHECK(hipSetDevice(ctx.dev));
     TraceRange t("colo send");
+    const bool engine = topt_.coloCopy == TransportOptions::Copy::Engine;
+    if (engine) ctx.coloPackLocal.run_device(parity, S(ctx), commBlocks_);
     if (I.epoch > 2) {
       std::vector<uint64_t *> credits;
-      for (int ci : ctx.coloSend) credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownBlock));
-      wait_flags_device(credits, I.epoch - 2, I.errDev, 1, I.waitTimeout, S(ctx));
+      for (int ci : ctx.coloSend) credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownFlag));
+      wait_flags(credits, I.epoch - 2, 1, S(ctx));
     }
-    ctx.coloPack.run_device(cv, S(ctx), commBlocks_);
+    if (engine) {
+      for (int ci : ctx.coloSend) {
+        const Channel &c = I.chans[ci];
+        if (c.bytes > 0)
+          engine_copy(c.remoteData + slot * c.slotStride, c.dbuf, size_t(c.bytes), S(ctx));
+      }
+    } else {
+      ctx.coloPack.run_device(cv, S(ctx), commBlocks_);
+    }
     std::vector<uint64_t *> arrived;
-    for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
-    signal_flags_device(arrived, I.epoch, S(ctx));
+    for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteFlag));
+    signal_flags(arrived, I.epoch, S(ctx));
   }
 
   jitter();
@@ -1174,16 +1481,14 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       HIP_CHECK(hipSetDevice(ctx.dev));
       ctx.rcclPack.run_device(parity, S(ctx), commBlocks_);
     }
-    NCCL_CHECK(ncclGroupStart());
+    RCCL_CHECK(rccl::group_start());
     for (auto &ctx : I.devs) {
       for (int ci : ctx.rcclSend)
-        NCCL_CHECK(ncclSend(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, I.chans[ci].ncclPeer, ctx.nccl,
-                            S(ctx)));
+        RCCL_CHECK(rccl::send(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), I.chans[ci].ncclPeer, ctx.nccl, S(ctx)));
       for (int ci : ctx.rcclRecv)
-        NCCL_CHECK(ncclRecv(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), ncclUint8, I.chans[ci].ncclPeer, ctx.nccl,
-                            S(ctx)));
+        RCCL_CHECK(rccl::recv(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), I.chans[ci].ncclPeer, ctx.nccl, S(ctx)));
     }
-    NCCL_CHECK(ncclGroupEnd());
+    RCCL_CHECK(rccl::group_end());
     for (auto &ctx : I.devs) {
       if (ctx.rcclRecv.empty()) continue;
       HIP_CHECK(hipSetDevice(ctx.dev));
@@ -1232,12 +1537,12 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     TraceRange t("colo recv");
     std::vector<uint64_t *> arrived, credits;
     for (int ci : ctx.coloRecv) {
-      arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownBlock));
-      credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteBlock));
+      arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownFlag));
+      credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteFlag));
     }
-    wait_flags_device(arrived, I.epoch, I.errDev, 2, I.waitTimeout, S(ctx));
+    wait_flags(arrived, I.epoch, 2, S(ctx));
     ctx.coloUnpack.run_device(cv, S(ctx), commBlocks_);
-    signal_flags_device(credits, I.epoch, S(ctx));
+    signal_flags(credits, I.epoch, S(ctx));
   }
 
   // (6) halos written by peer devices of this process

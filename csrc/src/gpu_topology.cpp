@@ -1,4 +1,5 @@
 #include "stencil/topo/gpu_topology.hpp"
+#include "stencil/rt/env.hpp"
 
 #include <hip/hip_runtime_api.h>
 
@@ -36,7 +37,7 @@ template <typename F> static bool sym(void *lib, const char *name, F *out) {
 const Smi &smi() {
   static Smi s = [] {
     Smi r;
-    if (std::getenv("STENCIL_NO_AMDSMI")) return r;
+    if (env::get_int("STENCIL_NO_AMDSMI", 0) != 0) return r;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
       (void)hipGetLastError();

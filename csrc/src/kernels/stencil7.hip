@@ -930,7 +930,7 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
     launch_lds<T, 2, 8, KIND, true>(a, tune, stream);
     return;
   }
-  if (alignedLayout && fits && (fwd || std::getenv("STENCIL_GENERIC_KERNEL") == nullptr)) {
+  if (alignedLayout && fits) {
     if (fwd) {
       // the forwarding epilogue needs registers: 2 rows per lane keeps it spill-free at >= 4 waves/SIMD
       launch_lds<T, 2, 8, KIND>(a, tune, stream);
@@ -1029,9 +1029,8 @@ static void apply_regions_t(const LocalDomain &dom, int64_t qi, const std::vecto
   std::vector<Rect3> rs;
   for (const auto &r : regions)
     if (!r.empty()) rs.push_back(Rect3(r.lo - org, r.hi - org));
-  STENCIL_REQUIRE(wrap == 0 || (aligned && std::getenv("STENCIL_GENERIC_EXTERIOR") == nullptr),
-                  "in-kernel wrap of exterior slabs needs the aligned layout");
-  if (aligned && std::getenv("STENCIL_GENERIC_EXTERIOR") == nullptr) {
+  STENCIL_REQUIRE(wrap == 0 || aligned, "in-kernel wrap of exterior slabs needs the aligned layout");
+  if (aligned) {
     for (size_t k0 = 0; k0 < rs.size(); k0 += kMaxShell) {
       ShellTable st{};
       for (size_t k = k0; k < rs.size() && st.n < kMaxShell; ++k) {
@@ -1089,7 +1088,7 @@ static void apply_regions_t(const LocalDomain &dom, int64_t qi, const std::vecto
 
 void stencil7_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
                             const Spheres &sph, hipStream_t stream, const StencilTune &tune) {
-  if (dom.backend() == Backend::Host || std::getenv("STENCIL_EXTERIOR_PER_REGION")) {
+  if (dom.backend() == Backend::Host) {
     STENCIL_REQUIRE(tune.wrap == 0 || dom.backend() == Backend::Device, "in-kernel wrap needs a device sub-domain");
     for (const auto &r : regions) stencil7_apply(dom, qi, r, kind, sph, stream, tune);
     return;

@@ -112,7 +112,7 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy && cvalid;
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1; // outer waves: garbage u1, never consumed
   // wave-uniform: u1 only on rows 1 .. NW-2, u2 only on the output rows (see stencil7x2_row_kernel)
-  const bool needU1 = !a.edgeskip || (w >= 1 && w < NW - 1), needU2 = !a.edgeskip || (w >= 2 && w < NW - 2);
+  const bool needU1 = w >= 1 && w < NW - 1, needU2 = w >= 2 && w < NW - 2; // edge waves: source rows only
 
   // y-wrapped rows read their periodic image (one conditional shift: rows reach 2 beyond the region, ny >= 2)
   const int yw =
@@ -338,17 +338,12 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
     // (4 apart, one XCD after the remap) march the same planes together and their shared y-halo rows meet in L2;
     // the columns left over (grids of fewer than 4 x columns blocks) spread over all blocks as short second segments
     const uint32_t cm = nb / 4;
-    uint32_t col, qq;
-    if (a.seg2q) { // quarter-major: consecutive blocks (one XCD after the remap) take y-adjacent columns of one
-      qq = lb / cm; //   quarter, so an XCD's blocks share every interior y-halo row through its L2
-      col = lb % cm;
-    } else {
-      col = lb / 4;
-      qq = lb % 4;
-    }
+    // quarter-major: consecutive blocks (one XCD after the remap) take y-adjacent columns of one quarter, so an
+    // XCD's blocks share every interior y-halo row through its L2 (column-major: 1146 vs 1164 Gcells/s, r2s3)
+    const uint32_t qq = lb / cm, col = lb % cm;
     s = col * nzt + qq * nzt / 4;
     e = col * nzt + (qq + 1) * nzt / 4;
-    if (a.seg2q) qodd = int(qq & 1);
+    qodd = int(qq & 1);
     const uint64_t LW = uint64_t(uint32_t(a.gy) - cm) * nzt;
     s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
     e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
@@ -385,7 +380,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy;
   // wave-uniform: u1 is needed on rows 1 .. NW-2 of the block (the y-neighbours of the output rows), u2 only on the
   // output rows; the edge waves only load and publish their source rows
-  const bool needU1 = !a.edgeskip || (w >= 1 && w < NW - 1), needU2 = !a.edgeskip || (w >= 2 && w < NW - 2);
+  const bool needU1 = w >= 1 && w < NW - 1, needU2 = w >= 2 && w < NW - 2; // edge waves: source rows only
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
   const bool lane0 = lane == 0, lane63 = lane == 63;
   // ragged rows: the last cell x = nx-1 sits in chunk H-1 of lane Lr, element kr
@@ -623,7 +618,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   const int y = yblk - 2 + w;
   if (yblk >= a.hiy) continue;
   const bool outRow = w >= 2 && w < NW - 2 && y < a.hiy;
-  const bool needU1 = !a.edgeskip || (w >= 1 && w < NW - 1), needU2 = !a.edgeskip || (w >= 2 && w < NW - 2);
+  const bool needU1 = w >= 1 && w < NW - 1, needU2 = w >= 2 && w < NW - 2; // edge waves: source rows only
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
   const bool lane0 = lane == 0, lane63 = lane == 63;
 
@@ -973,15 +968,6 @@ __global__ __launch_bounds__(256) void stencil7x2_thin_kernel(StencilArgs<T> a, 
 // ---------------------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------------------
-// STENCIL_X2_EDGE_SKIP=0: every wave computes u1 and u2 (A/B of the edge-wave skip)
-static int x2_edge_skip() {
-  static const int v = [] {
-    const char *e = std::getenv("STENCIL_X2_EDGE_SKIP");
-    return e == nullptr || std::atoi(e) != 0 ? 1 : 0;
-  }();
-  return v;
-}
-
 static int64_t x2_resident_blocks(const void *kernel, int threads) {
   static std::map<const void *, int64_t> cache;
   static std::mutex mu;
@@ -1065,7 +1051,6 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.gx = (a.nchunks + 63) / 64;
   a.gy = (ny + YO - 1) / YO;
   a.remap = tune.xcdRemap ? 1 : 0;
-  a.edgeskip = x2_edge_skip();
   const void *kern = (const void *)stencil7x2_kernel<T, NW, PF, KIND, 0>;
   const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x2_resident_blocks(kern, 64 * NW);
@@ -1115,7 +1100,6 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   a.x0 = a.lox;
   a.nchunks = 128;
   a.remap = tune.xcdRemap ? 1 : 0;
-  a.edgeskip = x2_edge_skip();
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = 1;
   a.gy = (ny + YO - 1) / YO;
@@ -1135,19 +1119,10 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     // lockstep quarters (a.seg = 2) when the resident blocks cover at most four per column and the quarters stay
     // long: with 8 CUs left to the transports (248 blocks) the balanced split puts y-adjacent blocks 16 planes apart
     // and their halo rows miss L2 (512^3 local interior: 276 vs 237 us at 256 blocks)
-    static const bool lockstep = [] {
-      const char *e = std::getenv("STENCIL_X2_LOCKSTEP");
-      return e == nullptr || std::atoi(e) != 0;
-    }();
     const int64_t q4 = slots / 4 * 4;
-    if (lockstep && q4 >= 4 && q4 / 4 <= cols && nz >= 64) {
+    if (tune.x2lockstep && q4 >= 4 && q4 / 4 <= cols && nz >= 64) {
       a.seg = 2;
       blocks = uint32_t(q4);
-      static const int qmajor = [] {
-        const char *e = std::getenv("STENCIL_X2_QMAJOR");
-        return e == nullptr || std::atoi(e) != 0 ? 1 : 0;
-      }();
-      a.seg2q = qmajor;
     }
   } else {
     int zc = tune.zchunk;
@@ -1173,7 +1148,6 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
   a.wrapm = tune.wrap;
   a.xfast = tune.x2xfast;
   a.remap = tune.xcdRemap ? 1 : 0;
-  a.edgeskip = x2_edge_skip();
   a.x0 = a.lox; // 16-B aligned (checked by the caller)
   a.nchunks = (a.hix - a.x0) / 4;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
@@ -1431,8 +1405,7 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
   // z slabs (whole x-y planes) of periodic 512-cell rows: the whole-row kernel, one block per 8 output rows of a
   // slab (fixed z chunk = the slab: every block marches only its slab's planes)
   bool zDone = false;
-  const char *zr = std::getenv("STENCIL_ZSLAB_ROW"); // read per call: tests switch it within one process
-  if (f32 && tune.x2row && (tune.wrap & 1) && (zr == nullptr || std::atoi(zr) != 0) && lo.z <= 4 && hi.z <= 4) {
+  if (f32 && tune.x2row && tune.zslabRow && (tune.wrap & 1) && lo.z <= 4 && hi.z <= 4) {
     StencilTune tz = tune;
     tz.x2sched = 0;
     tz.reserveCUs = 0;

@@ -48,10 +48,8 @@ template <typename T> struct StencilArgs {
   int zc;                           // planes per block
   int gx, gy, gz;                   // logical grid
   int seg;                          // stencil7x2: 1 = balanced (column, plane) segments over gridDim.x blocks, 2 = lockstep quarters
-  int seg2q;                        // stencil7x2 lockstep quarters: 1 = quarter-major block order
   int xfast;                        // stencil7x2: 1 = column index x-major (x-adjacent columns on one XCD)
   int remap;                        // stencil7x2: 1 = XCD-aware block remap
-  int edgeskip;                     // stencil7x2 row kernel: 1 = the block's edge waves skip the unused u1 / u2
   // spheres, raw coordinates
   int hx, hy, hz, cx, cy, cz;
   int r1sq; // (radius+1)^2, 0 = disabled

@@ -11,9 +11,7 @@
 namespace stencil {
 
 LocalDomain::LocalDomain(const Dim3 &sz, const Dim3 &origin, int dev, Backend backend)
-    : sz_(sz), origin_(origin), dev_(dev), backend_(backend) {
-  if (const char *e = std::getenv("STENCIL_PAD")) pad_ = std::atoi(e) != 0;
-}
+    : sz_(sz), origin_(origin), dev_(dev), backend_(backend) {}
 
 LocalDomain::LocalDomain(LocalDomain &&o) noexcept
     : sz_(o.sz_), origin_(o.origin_), radius_(o.radius_), dev_(o.dev_), backend_(o.backend_), pad_(o.pad_),

@@ -21,6 +21,7 @@
 #include <set>
 #include <thread>
 
+#include "stencil/rt/env.hpp"
 #include "stencil/rt/logging.hpp"
 
 namespace stencil {
@@ -29,10 +30,7 @@ static std::atomic<int> g_rank{0};
 int rank() { return g_rank.load(); }
 void set_rank(int r) { g_rank.store(r); }
 int runtime_level() {
-  static int lvl = [] {
-    const char *e = std::getenv("STENCIL_LOG_LEVEL");
-    return e ? std::atoi(e) : 2;
-  }();
+  static int lvl = int(env::get_int("STENCIL_LOG_LEVEL", 2));
   return lvl;
 }
 } // namespace log
@@ -40,7 +38,7 @@ int runtime_level() {
 namespace comm {
 
 static std::string local_hostname() {
-  if (const char *h = std::getenv("STENCIL_HOSTNAME")) return h;
+  if (env::has("STENCIL_HOSTNAME")) return env::get_str("STENCIL_HOSTNAME", "");
   char buf[256] = {0};
   gethostname(buf, sizeof(buf) - 1);
   return buf;
@@ -316,11 +314,20 @@ class TcpGroup : public ProcGroup {
   }
 
   std::vector<char> recv_raw(int src, uint32_t tag) {
-    std::unique_lock<std::mutex> lk(mu_);
-    auto pred = [&] { return !mailbox_[src][tag].empty() || closed_[src] || !error_.empty(); };
-    if (!cv_.wait_for(lk, std::chrono::duration<double>(timeout_s_), pred))
+    bool ok = false;
+    std::vector<char> m = recv_raw_for(src, tag, timeout_s_, &ok);
+    if (!ok)
       LOG_FATAL("recv from rank " << src << " tag " << std::hex << tag << std::dec << " timed out after " << timeout_s_
                                   << " s");
+    return m;
+  }
+
+  // *ok = false on timeout (nothing consumed)
+  std::vector<char> recv_raw_for(int src, uint32_t tag, double timeout_s, bool *ok) {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto pred = [&] { return !mailbox_[src][tag].empty() || closed_[src] || !error_.empty(); };
+    *ok = cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred);
+    if (!*ok) return {};
     auto &q = mailbox_[src][tag];
     if (q.empty()) LOG_FATAL("rank " << src << " closed its connection (" << error_ << ")");
     std::vector<char> m = std::move(q.front());
@@ -330,8 +337,11 @@ class TcpGroup : public ProcGroup {
 
 public:
   TcpGroup(int rank, int size, const std::string &master, int port, double timeout_s)
-      : rank_(rank), size_(size), timeout_s_(timeout_s), hosts_(size), fds_(size, -1), mailbox_(size),
-        closed_(size, false) {
+      : rank_(rank), size_(size), timeout_s_(std::max(timeout_s, 600.0)), hosts_(size), fds_(size, -1),
+        mailbox_(size), closed_(size, false) {
+    // the rendezvous waits for every rank to start (a fresh node may take minutes to load torch): at least 600 s;
+    // the configured timeout applies from the first barrier on
+    const double bootTimeout = timeout_s_;
     log::set_rank(rank);
     for (int i = 0; i < size; ++i) sendMu_.emplace_back(new std::mutex);
     const std::string myHost = local_hostname();
@@ -349,7 +359,7 @@ public:
       names[0] = myHost;
       std::vector<int> bootFds(size, -1);
       for (int k = 1; k < size; ++k) {
-        int fd = accept_one(lfd, timeout_s);
+        int fd = accept_one(lfd, bootTimeout);
         int32_t r = -1;
         STENCIL_REQUIRE(read_all(fd, &r, sizeof(r)), "bootstrap peer closed");
         STENCIL_REQUIRE(r > 0 && r < size && bootFds[r] < 0, "bad/duplicate bootstrap rank " << r);
@@ -371,7 +381,7 @@ public:
       // rank 0's bootstrap connections double as its links to every other rank
       for (int r = 1; r < size; ++r) fds_[r] = bootFds[r];
     } else {
-      int fd = connect_to(master, port, timeout_s);
+      int fd = connect_to(master, port, bootTimeout);
       int32_t r = rank;
       write_all(fd, &r, sizeof(r));
       // our address as seen on the route to the master
@@ -394,13 +404,13 @@ public:
       fds_[0] = fd;
       // connect to ranks 1..rank-1, accept from rank+1..size-1
       for (int k = 1; k < rank; ++k) {
-        int cfd = connect_to(ips[k], ports[k], timeout_s);
+        int cfd = connect_to(ips[k], ports[k], bootTimeout);
         int32_t me = rank;
         write_all(cfd, &me, sizeof(me));
         fds_[k] = cfd;
       }
       for (int k = rank + 1; k < size; ++k) {
-        int afd = accept_one(lfd, timeout_s);
+        int afd = accept_one(lfd, bootTimeout);
         int32_t who = -1;
         STENCIL_REQUIRE(read_all(afd, &who, sizeof(who)), "mesh peer closed");
         STENCIL_REQUIRE(who > rank && who < size && fds_[who] < 0, "bad mesh rank " << who);
@@ -412,6 +422,7 @@ public:
     for (int k = 0; k < size; ++k)
       if (k != rank) readers_.emplace_back(&TcpGroup::reader, this, k);
     barrier();
+    timeout_s_ = timeout_s;
   }
 
   ~TcpGroup() override {
@@ -454,6 +465,22 @@ public:
     std::vector<char> all(size_);
     allgather(&c, 1, all.data());
   }
+  bool barrier_for(double timeout_s) override {
+    const uint32_t tag = next_coll_tag();
+    const char c = 0;
+    bool ok = true;
+    if (rank_ == 0) {
+      for (int k = 1; k < size_ && ok; ++k) (void)recv_raw_for(k, tag, timeout_s, &ok);
+      if (ok)
+        for (int k = 1; k < size_; ++k) send_raw(k, tag, &c, 1);
+    } else {
+      send_raw(0, tag, &c, 1);
+      (void)recv_raw_for(0, tag, timeout_s, &ok);
+    }
+    return ok;
+  }
+  void set_timeout(double timeout_s) override { timeout_s_ = timeout_s; }
+  double timeout() const override { return timeout_s_; }
   void bcast(void *buf, size_t n, int root) override {
     const uint32_t tag = next_coll_tag();
     if (rank_ == root) {
@@ -506,25 +533,17 @@ std::shared_ptr<ProcGroup> make_tcp_group(int rank, int size, const std::string 
 }
 
 static int env_int(const char *a, const char *b, int dflt) {
-  if (const char *e = std::getenv(a)) return std::atoi(e);
-  if (b)
-    if (const char *e = std::getenv(b)) return std::atoi(e);
-  return dflt;
+  return int(env::get_int(a, b ? env::get_int(b, dflt) : dflt));
 }
 
 std::shared_ptr<ProcGroup> make_group_from_env() {
   const int size = env_int("STENCIL_WORLD_SIZE", "WORLD_SIZE", 1);
   const int rank = env_int("STENCIL_RANK", "RANK", 0);
   if (size <= 1) return make_single_group();
-  std::string addr = "127.0.0.1";
-  if (const char *e = std::getenv("STENCIL_MASTER_ADDR"))
-    addr = e;
-  else if (const char *e2 = std::getenv("MASTER_ADDR"))
-    addr = e2;
+  const std::string addr = env::get_str("STENCIL_MASTER_ADDR", env::get_str("MASTER_ADDR", "127.0.0.1"));
   int port = env_int("STENCIL_MASTER_PORT", nullptr, -1);
   if (port < 0) port = env_int("MASTER_PORT", nullptr, 29500) + 1; // MASTER_PORT is held by torch's store
-  double timeout = 600;
-  if (const char *e = std::getenv("STENCIL_COMM_TIMEOUT")) timeout = std::atof(e);
+  const double timeout = env::get_double("STENCIL_COMM_TIMEOUT", env_wait_timeout(600.0));
   return make_tcp_group(rank, size, addr, port, timeout);
 }
 

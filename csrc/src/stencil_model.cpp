@@ -31,6 +31,8 @@ StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::
   dd_->set_axis_cost(cfg.axisCost);
   if (!cfg.gpus.empty()) dd_->set_gpus(cfg.gpus);
   if (cfg.setBackend) dd_->set_backend(cfg.backend);
+  dd_->set_transport_options(cfg.transport);
+  dd_->set_self_test(cfg.selfTest);
   for (int q = 0; q < cfg.quantities; ++q) {
     const std::string name = cfg.kind == StencilKind::Jacobi && cfg.quantities == 1 ? "d" : "d" + std::to_string(q);
     if (cfg.fp64)
@@ -66,11 +68,11 @@ void StencilModel::init() {
   const Rect3 cReg = dd_->get_compute_region();
   sph_ = cfg_.kind == StencilKind::Jacobi ? Spheres::jacobi(cReg) : Spheres();
   overlap_ = cfg_.overlap;
-  if (cfg_.overlap && cfg_.autoOverlap && std::getenv("STENCIL_FAKE_REMOTE_AXES") == nullptr &&
+  if (cfg_.overlap && cfg_.autoOverlap && cfg_.transport.fakeRemoteAxes == 0 &&
       dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All))
     overlap_ = false;
   auto &doms0 = dd_->domains();
-  forward_ = cfg_.forward && std::getenv("STENCIL_NO_FORWARD") == nullptr && dd_->world_size() == 1 &&
+  forward_ = cfg_.forward && dd_->world_size() == 1 &&
              dd_->all_direct() && !doms0.empty();
   for (const auto &d : doms0)
     for (int64_t q = 0; q < d.num_data() && forward_; ++q) forward_ = HaloForwarder::supported(d, q);
@@ -119,8 +121,8 @@ void StencilModel::init() {
   // overlapped and whole-region pairs can be switched at run time when both would wrap the same axes: the local
   // interior is shrunk only along axes cut across GPUs, which are never self-wrapped (set_overlap)
   bool sameWrap = true;
-  if (pairs_ && cfg_.wrapSelf && std::getenv("STENCIL_NO_WRAP") == nullptr) {
-    int w = dd_->self_wrap_axes();
+  if (pairs_ && cfg_.wrapSelf) {
+    int w = dd_->self_wrap_axes() & cfg_.wrapAxesMask;
     for (size_t di = 0; di < doms0.size(); ++di) {
       const auto &d = doms0[di];
       for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7x2_wrappable_axes(d, q, cfg_.tune.x2row);
@@ -136,7 +138,6 @@ void StencilModel::init() {
     }
     sameWrap = wOn == w;
     if (overlap_) w = wOn;
-    if (const char *e = std::getenv("STENCIL_WRAP_AXES")) w &= std::atoi(e); // restrict (experiments)
     pairTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
@@ -160,7 +161,7 @@ void StencilModel::init() {
   localSteps_ = false;
   const bool stepDevice = !doms0.empty() && doms0[0].backend() == Backend::Device;
   if (!pairs_ && !forward_ && overlap_ && stepDevice && cfg_.wrapSelf && cfg_.tune.variant != StencilTune::kMfma &&
-      std::getenv("STENCIL_NO_LOCAL_INTERIOR") == nullptr) {
+      cfg_.localInterior) {
     const auto li = dd_->get_local_interior(1);
     bool remote = false, ok = true;
     for (size_t di = 0; di < doms0.size(); ++di) {
@@ -187,9 +188,8 @@ void StencilModel::init() {
     }
   }
   if (!pairs_ && !forward_ && (!overlap_ || localSteps_) && stepDevice && cfg_.wrapSelf &&
-      cfg_.tune.variant != StencilTune::kMfma && std::getenv("STENCIL_NO_WRAP") == nullptr) {
-    int w = dd_->self_wrap_axes();
-    if (const char *e = std::getenv("STENCIL_WRAP_AXES")) w &= std::atoi(e);
+      cfg_.tune.variant != StencilTune::kMfma) {
+    int w = dd_->self_wrap_axes() & cfg_.wrapAxesMask;
     for (size_t di = 0; di < doms0.size(); ++di) {
       const auto &d = doms0[di];
       for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7_wrappable_axes(d, q);
@@ -203,12 +203,12 @@ void StencilModel::init() {
     stepTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
-  // experiments: overlapped pairs with the slabs after the interior sweep (set_overlap_mode(2)) from the start
-  if (const char *e = std::getenv("STENCIL_OVERLAP_MODE")) slabsAfter_ = pairs_ && overlap_ && std::atoi(e) == 2;
+  // overlapped pairs with the slabs after the interior sweep (set_overlap_mode(2)) from the start
+  slabsAfter_ = pairs_ && overlap_ && cfg_.overlapMode == 2;
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
-            dd_->world_size() == 1 && std::getenv("STENCIL_NO_GRAPH") == nullptr;
+            dd_->world_size() == 1;
   interiors_ = dd_->get_interior();
   exteriors_ = dd_->get_exterior();
   auto &doms = dd_->domains();
@@ -467,8 +467,14 @@ void StencilModel::set_comm_reserve(int cus) {
 }
 
 void StencilModel::synchronize() {
-  for (auto &s : compute_) s.sync();
-  if (dd_->realized()) dd_->sync_exchange();
+  // the compute streams join the exchange (wait_exchange / exteriorDone_ / the exchange enqueued on them), so a
+  // stalled peer stalls them too: DistributedDomain polls them with its watchdog instead of blocking on them first
+  std::vector<hipStream_t> streams;
+  for (auto &s : compute_) streams.push_back(s.get());
+  if (dd_->realized())
+    dd_->sync_streams(streams);
+  else
+    for (auto &s : compute_) s.sync();
 }
 
 } // namespace stencil

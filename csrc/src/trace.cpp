@@ -1,4 +1,5 @@
 #include "stencil/rt/trace.hpp"
+#include "stencil/rt/env.hpp"
 
 #include <dlfcn.h>
 
@@ -16,8 +17,7 @@ struct Roctx {
   PopFn pop = nullptr;
   bool on = false;
   Roctx() {
-    const char *e = std::getenv("STENCIL_TRACE");
-    if (!e || std::atoi(e) == 0) return;
+    if (env::get_int("STENCIL_TRACE", 0) == 0) return;
     const char *libs[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4",
                           "libroctx64.so"};
     for (const char *l : libs) {

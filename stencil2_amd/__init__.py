@@ -42,7 +42,10 @@ from ._C import (  # noqa: E402,F401
     StencilKind,
     StencilModelConfig,
     StencilTune,
+    TransportOptions,
     TrivialPlacement,
+    build_info,
+    build_info_string,
     device_count,
     find_free_port,
     gpu_bandwidth,
@@ -65,5 +68,5 @@ from .models.stencil_model import Jacobi3D, AstarothSim, StencilModel  # noqa: E
 __all__ = [
     "Backend", "Boundary", "Dim3", "DType", "MethodFlags", "PlacementStrategy", "Radius", "Rect3", "Statistics", "StencilKind",
     "DistributedDomain", "Jacobi3D", "AstarothSim", "StencilModel", "init_process_group", "get_group",
-    "RankPartition", "NodePartition", "TrivialPlacement", "NodeAwarePlacement", "qap_solve", "qap_solve_catch",
+    "TransportOptions", "build_info", "RankPartition", "NodePartition", "TrivialPlacement", "NodeAwarePlacement", "qap_solve", "qap_solve_catch",
 ]

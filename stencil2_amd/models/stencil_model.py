@@ -22,7 +22,9 @@ class StencilModel:
                  quantities: int = 1, fp64: bool = False, methods=_C.MethodFlags.All,
                  placement=_C.PlacementStrategy.NodeAware, gpus=None, overlap: bool = True, auto_overlap: bool = True,
                  use_graph: bool = True, forward: bool = False, temporal: int = 1, backend=None,
-                 tune: _C.StencilTune | None = None, group=None, axis_cost=None, wrap_self: bool = True):
+                 tune: _C.StencilTune | None = None, group=None, axis_cost=None, wrap_self: bool = True,
+                 transport: _C.TransportOptions | None = None, wrap_axes_mask: int = 7, local_interior: bool = True,
+                 overlap_mode: int = 1, self_test: bool = False):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
         cfg.kind = kind
@@ -40,6 +42,12 @@ class StencilModel:
         cfg.forward = forward
         cfg.temporal = temporal
         cfg.wrap_self = wrap_self
+        cfg.wrap_axes_mask = wrap_axes_mask
+        cfg.local_interior = local_interior
+        cfg.overlap_mode = overlap_mode
+        cfg.self_test = self_test  # multi-rank: verify the transports on a probe domain, ladder to what works
+        if transport is not None:  # DistributedDomain.set_transport_options (inbox memory, DMA copies, completion)
+            cfg.transport = transport
         if backend is not None:
             cfg.backend = backend
         if tune is not None:

@@ -1,4 +1,5 @@
 """Worker for multi-process tests (launched by conftest.run_ranks). argv[1] = scenario."""
+import faulthandler
 import os
 import sys
 
@@ -7,6 +8,20 @@ import torch
 import stencil2_amd as st
 from stencil2_amd.ops import jacobi_step_reference
 from stencil2_amd.utils.testing import check_exchange, fill_coords
+
+
+def transport_from_env():
+    """TransportOptions of a test scenario (MP_* variables set by the launching test)."""
+    t = st.TransportOptions()
+    e = os.environ
+    t.inbox = getattr(st.TransportOptions.Inbox, e.get("MP_INBOX", "Uncached"))
+    t.colo_copy = getattr(st.TransportOptions.Copy, e.get("MP_COLO_COPY", "Store"))
+    t.peer_copy = getattr(st.TransportOptions.Copy, e.get("MP_PEER_COPY", "Store"))
+    t.completion = getattr(st.TransportOptions.Completion, e.get("MP_COMPLETION", "Kernel"))
+    t.jitter_us = int(e.get("MP_JITTER_US", "0"))
+    t.fail_ipc_probe = e.get("MP_IPC_PROBE_FAIL") == "1"
+    t.fail_rccl_init = e.get("MP_RCCL_INIT_FAIL") == "1"
+    return t
 
 
 def scenario_exchange(backend, methods, radius_name, size):
@@ -23,6 +38,7 @@ def scenario_exchange(backend, methods, radius_name, size):
     radius = pats[radius_name]
     dd = st.DistributedDomain(*size, group=g)
     dd.set_backend(backend)
+    dd.set_transport_options(transport_from_env())
     dd.set_radius(radius)
     if backend == st.Backend.Device:
         dd.set_gpus([0])
@@ -34,6 +50,7 @@ def scenario_exchange(backend, methods, radius_name, size):
     for it in range(3):
         fill_coords(dd, q)
         fill_coords(dd, q2)
+        print(f"rank {g.rank()} epoch {it} exchange", flush=True)
         dd.exchange()
         bad += check_exchange(dd, q, radius) + check_exchange(dd, q2, radius)
         dd.swap()
@@ -49,6 +66,7 @@ def scenario_canary(backend, methods, radius_name, size, iters=12):
     radius = {"r1": st.Radius.constant(1), "fec": st.Radius.face_edge_corner(2, 1, 1)}[radius_name]
     dd = st.DistributedDomain(*size, group=g)
     dd.set_backend(backend)
+    dd.set_transport_options(transport_from_env())
     dd.set_radius(radius)
     if backend == st.Backend.Device:
         dd.set_gpus([0])
@@ -67,7 +85,9 @@ def scenario_canary(backend, methods, radius_name, size, iters=12):
             t.fill_(float("nan"))
             dd.curr_interior(di, qf).copy_(inner)
         before = [dd.curr_interior(di, q).clone() for di in range(dd.num_domains())]
+        print(f"rank {g.rank()} epoch {it} exchange", flush=True)
         dd.exchange()
+        print(f"rank {g.rank()} epoch {it} check", flush=True)
         bad += check_exchange(dd, q, radius, offset=off) + check_exchange(dd, qf, radius, offset=off)
         for di in range(dd.num_domains()):
             bad += int((dd.curr_interior(di, q) != before[di]).sum())
@@ -88,10 +108,11 @@ def scenario_jacobi(backend, methods, size):
     if kind == "astaroth":
         from stencil2_amd.ops import astaroth_step_reference as ref
         m = st.AstarothSim(size, quantities=1, gpus=gpus, backend=backend, methods=methods, group=g,
-                           temporal=temporal, **kw)
+                           temporal=temporal, transport=transport_from_env(), **kw)
     else:
         ref = jacobi_step_reference
-        m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g, temporal=temporal, **kw)
+        m = st.Jacobi3D(size, gpus=gpus, backend=backend, methods=methods, group=g, temporal=temporal,
+                        transport=transport_from_env(), **kw)
     m.init()
     L = m.domain.size()
     if kind == "astaroth":
@@ -144,6 +165,31 @@ def scenario_jacobi(backend, methods, size):
     return bad
 
 
+def scenario_selftest(backend, methods, size):
+    """realize() with the transport self-test ladder, then the coordinate oracle on the verified transports."""
+    g = st.init_process_group()
+    r = st.Radius.face_edge_corner(2, 1, 1)
+    dd = st.DistributedDomain(*size, group=g)
+    dd.set_backend(backend)
+    dd.set_transport_options(transport_from_env())
+    dd.set_radius(r)
+    dd.set_methods(methods)
+    dd.set_self_test(True)
+    if backend == st.Backend.Device:
+        dd.set_gpus([0])
+    q = dd.add_data("c", torch.int32)
+    dd.realize()
+    bad = 0
+    for it in range(2):
+        fill_coords(dd, q, offset=it)
+        dd.exchange()
+        bad += check_exchange(dd, q, r, offset=it)
+        dd.swap()
+    print(f"rank {g.rank()} selftest bad {bad} report [{dd.self_test_report()}] methods "
+          f"{st.methods_to_string(dd.methods())}", flush=True)
+    return bad
+
+
 def scenario_localint(backend, methods, size):
     """get_local_interior: shrunk by the stencil reach (2) exactly at the faces whose halo comes from another rank,
     untouched along axes that wrap onto the same rank; always a superset of get_interior()."""
@@ -175,6 +221,10 @@ def scenario_localint(backend, methods, size):
 
 
 def main():
+    # a stalled rank dumps every thread's Python stack (its C++ frames show as the native call it is in) so a hang
+    # names its rank, scenario and phase; repeated, in case the first dump lands before the stall
+    faulthandler.enable()
+    faulthandler.dump_traceback_later(float(os.environ.get("MP_STALL_DUMP_S", "40")), repeat=True)
     sc = sys.argv[1]
     backend = st.Backend.Device if os.environ.get("MP_DEVICE") == "1" else st.Backend.Host
     methods = st.MethodFlags.None_
@@ -184,6 +234,8 @@ def main():
         bad = scenario_exchange(backend, methods, sys.argv[2], tuple(int(v) for v in sys.argv[3].split(",")))
     elif sc == "canary":
         bad = scenario_canary(backend, methods, sys.argv[2], tuple(int(v) for v in sys.argv[3].split(",")))
+    elif sc == "selftest":
+        bad = scenario_selftest(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "localint":
         bad = scenario_localint(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "jacobi":

@@ -449,17 +449,20 @@ def test_temporal2_overlapped(st, methods, size, gpus, kind):
                                                  ((512, 112, 120), [0, 0, 0, 0], 6, "jacobi"),
                                                  ((512, 20, 26), [0, 0], 6, "astaroth"),
                                                  ((645, 132, 136), [0, 0], 4, "jacobi")])
-def test_temporal2_overlapped_zslab_row_kernel(st, monkeypatch, zrow, mode, size, gpus, fake, kind):
+def test_temporal2_overlapped_zslab_row_kernel(st, zrow, mode, size, gpus, fake, kind):
     """Overlapped fused pairs with periodic 512-cell (and ragged) rows whose z (and y) faces are treated as remote
-    (STENCIL_FAKE_REMOTE_AXES: the multi-GPU split on one GPU): the z slabs go through the whole-row kernel with the
-    slab as its z chunk (STENCIL_ZSLAB_ROW=1, default) or the thin kernel (0); both bitwise equal to single steps."""
+    (TransportOptions.fake_remote_axes: the multi-GPU split on one GPU): the z slabs go through the whole-row kernel
+    with the slab as its z chunk (StencilTune.zslab_row, default) or the thin kernel; both bitwise equal to single
+    steps. mode 2: the slabs after the interior sweep."""
     from stencil2_amd.ops import astaroth_step_reference
-    monkeypatch.setenv("STENCIL_ZSLAB_ROW", zrow)
-    monkeypatch.setenv("STENCIL_FAKE_REMOTE_AXES", str(fake))
-    monkeypatch.setenv("STENCIL_OVERLAP_MODE", mode)  # 2: the slabs after the interior sweep
+    t = st.StencilTune()
+    t.zslab_row = zrow == "1"
+    tr = st.TransportOptions()
+    tr.fake_remote_axes = fake
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
-    m = cls(size, gpus=gpus, temporal=2, overlap=True, axis_cost=(64, 3, 2), **kw)
+    m = cls(size, gpus=gpus, temporal=2, overlap=True, axis_cost=(64, 3, 2), tune=t, transport=tr,
+            overlap_mode=int(mode), **kw)
     m.init()
     assert m.temporal_blocking() and m.overlapping() and m.wrap_axes() == (1 if fake == 6 else 3)
     assert m.domain.placement_dim().x == 1 and m.overlap_mode() == int(mode)
@@ -474,18 +477,19 @@ def test_temporal2_overlapped_zslab_row_kernel(st, monkeypatch, zrow, mode, size
 @pytest.mark.parametrize("fake,reserve,lockstep", [(None, 8, "1"), ("4", 8, "1"), ("4", 4, "1"), ("4", 8, "0"),
                                                     ("6", 8, "1")])
 @pytest.mark.parametrize("alt", [False, True])
-def test_temporal2_row_kernel_lockstep_quarters(st, monkeypatch, fake, reserve, lockstep, alt):
+def test_temporal2_row_kernel_lockstep_quarters(st, fake, reserve, lockstep, alt):
     """Whole-row fused pairs over 64 row groups: the lockstep schedule (four blocks per column for the first
     blocks/4 columns, the rest as short second segments: 256 / 248 / 252 resident blocks) and the balanced one are
     bitwise equal to single steps (Astaroth proxy: no spheres, any grid thickness)."""
     from stencil2_amd.ops import astaroth_step_reference
-    monkeypatch.setenv("STENCIL_X2_LOCKSTEP", lockstep)
-    if fake:
-        monkeypatch.setenv("STENCIL_FAKE_REMOTE_AXES", fake)
     t = st.StencilTune()
+    t.x2lockstep = lockstep == "1"
     t.x2reserve = reserve
     t.alternate_z = alt  # per-step z-direction flip (off by default)
-    m = st.AstarothSim((512, 512, 72), quantities=1, gpus=[0], temporal=2, tune=t, axis_cost=(64, 3, 2))
+    tr = st.TransportOptions()
+    tr.fake_remote_axes = int(fake or 0)
+    m = st.AstarothSim((512, 512, 72), quantities=1, gpus=[0], temporal=2, tune=t, axis_cost=(64, 3, 2),
+                       transport=tr)
     m.init()
     assert m.temporal_blocking() and m.overlapping() == bool(fake)
     u = _gather(m)
@@ -556,6 +560,54 @@ def test_colocated_ipc_two_ranks_one_gpu(radius):
         assert rc == 0, out[-3000:]
 
 
+@pytest.mark.parametrize("inbox,copy,completion", [("Uncached", "Engine", "Kernel"), ("Coarse", "Store", "Kernel"),
+                                                   ("Coarse", "Engine", "Kernel"), ("Fine", "Store", "Kernel"),
+                                                   ("Uncached", "Store", "StreamOp"), ("Coarse", "Engine", "StreamOp")])
+def test_colocated_transport_variants_two_ranks(inbox, copy, completion):
+    """Every TransportOptions variant of the HIP IPC transport (receive-slot memory, kernel stores vs DMA-engine
+    copies, spin kernels vs stream wait/write operations): coordinate oracle over faces, edges and corners, then
+    fused Jacobi pairs vs the torch oracle, two ranks sharing one GPU."""
+    env = {"MP_DEVICE": "1", "MP_METHODS": "Colocated|Kernel", "STENCIL_WAIT_TIMEOUT": "20", "MP_INBOX": inbox,
+           "MP_COLO_COPY": copy, "MP_COMPLETION": completion}
+    for rc, out in run_ranks(2, WORKER, ["exchange", "fec", "20,12,10"], env_extra=env):
+        assert rc == 0, out[-3000:]
+    env.update({"MP_METHODS": "All", "MP_TEMPORAL": "2", "MP_EXPECT_OVERLAP": "1"})
+    for rc, out in run_ranks(2, WORKER, ["jacobi", "48,48,48"], env_extra=env):
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out
+
+
+def test_rccl_init_failure_falls_back_to_staged(st):
+    """An RCCL communicator that cannot be created (forced) turns every RCCL channel into a host-staged one
+    (agreed on by all ranks) instead of aborting; the fused pairs stay exact."""
+    tr = st.TransportOptions()
+    tr.fail_rccl_init = True
+    m = st.Jacobi3D((40, 36, 44), gpus=[0, 0], methods=st.MethodFlags.Rccl, temporal=2, transport=tr)
+    m.init()
+    dd = m.domain
+    assert dd.exchange_bytes_for_method(st.MethodFlags.Rccl) == 0
+    assert dd.exchange_bytes_for_method(st.MethodFlags.Staged) > 0
+    u = _gather(m)
+    m.run(4)
+    for _ in range(4):
+        u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
+def test_self_test_ladder_two_ranks():
+    """DistributedDomain.set_self_test: the probe exchange passes with the co-located IPC transport (nothing dropped);
+    with the IPC probe forced to fail, Colocated is dropped and the shared-GPU pairs are host-staged, still exact."""
+    for fail in ("0", "1"):
+        outs = run_ranks(2, WORKER, ["selftest", "48,40,36"],
+                         env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                    "MP_IPC_PROBE_FAIL": fail})
+        for rc, out in outs:
+            assert rc == 0, out[-3000:]
+            assert "selftest bad 0" in out, out[-2000:]
+            assert ("colo" in out.split("methods ")[-1].split()[0]) == (fail == "0"), out[-2000:]
+
+
 @pytest.mark.parametrize("temporal,ranks", [("1", 2), ("2", 2), ("2", 4), ("2", 8)])
 def test_colocated_ipc_jacobi_two_ranks(temporal, ranks):
     """Jacobi over HIP IPC between ranks sharing one GPU. Fused pairs overlap automatically here (the split axes
@@ -616,7 +668,7 @@ def test_ipc_probe_failure_falls_back_on_shared_gpu():
     one device): the runtime drops Colocated and Rccl and stages through the host; results stay exact."""
     outs = run_ranks(2, WORKER, ["jacobi", "48,48,48"],
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
-                                "MP_TEMPORAL": "2", "STENCIL_IPC_PROBE_FAIL": "1"})
+                                "MP_TEMPORAL": "2", "MP_IPC_PROBE_FAIL": "1"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out
@@ -624,12 +676,15 @@ def test_ipc_probe_failure_falls_back_on_shared_gpu():
         assert "bytes_Rccl=0 " in out and "bytes_Colocated=0 " in out and "bytes_Staged=0 " not in out, out[-2000:]
 
 
-@pytest.mark.parametrize("methods", ["Colocated|Kernel", "Staged|Kernel"])
-def test_race_canary_two_ranks_one_gpu(methods):
-    """Race canary over HIP IPC (double-buffered inboxes + credits) and the staged path, with jitter."""
+@pytest.mark.parametrize("methods,copy", [("Colocated|Kernel", "Store"), ("Colocated|Kernel", "Engine"),
+                                          ("Staged|Kernel", "Store")])
+def test_race_canary_two_ranks_one_gpu(methods, copy):
+    """Race canary over HIP IPC (double-buffered inboxes + credits; pack-kernel stores or DMA-engine copies) and the
+    staged path, with jitter. Every host wait on a peer is bounded by STENCIL_WAIT_TIMEOUT and a stalled rank dumps
+    its stacks (MP_STALL_DUMP_S), so a stall fails with every rank's phase instead of hanging."""
     outs = run_ranks(2, WORKER, ["canary", "fec", "20,12,10"],  # ~2.5 s normally; 90 s: rank outputs on a hang
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20",
-                                "STENCIL_JITTER_US": "200"}, timeout=90)
+                                "MP_JITTER_US": "200", "MP_COLO_COPY": copy, "MP_STALL_DUMP_S": "30"}, timeout=90)
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 

@@ -34,10 +34,20 @@ def test_jacobi_ranks_match_oracle():
 @pytest.mark.parametrize("n,radius", [(2, "r1"), (3, "fec")])
 def test_race_canary_staged(n, radius):
     """NaN-poisoned halos, iteration-tagged interiors, back-to-back exchanges with random transport jitter."""
-    _ok(run_ranks(n, WORKER, ["canary", radius, "14,10,9"], env_extra={"STENCIL_JITTER_US": "300"}))
+    _ok(run_ranks(n, WORKER, ["canary", radius, "14,10,9"], env_extra={"MP_JITTER_US": "300"}))
 
 
 @pytest.mark.parametrize("n", [1, 2, 4])
 def test_local_interior_ranks(n):
     """the overlap interior of fused pairs: shrunk only at faces whose halo crosses ranks"""
     _ok(run_ranks(n, WORKER, ["localint", "24,20,18"]))
+
+
+def test_self_test_ladder_host_backend():
+    """realize() with the transport self-test on the host backend (staged over TCP): the probe passes and the
+    methods are kept."""
+    outs = run_ranks(2, WORKER, ["selftest", "24,20,18"], env_extra={"MP_METHODS": "All"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "selftest bad 0" in out and "report [all" not in out, out[-2000:]
+        assert ": ok]" in out, out[-2000:]
