@@ -126,30 +126,48 @@ def scenario_jacobi(backend, methods, size):
             m.interior(di).copy_(u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x].to(m.interior(di).device))
         if backend == st.Backend.Device:
             torch.cuda.synchronize()
+    elif os.environ.get("MP_RANDOM") == "1":  # same random global field on every rank (CPU generator, fixed seed)
+        u = torch.rand((L.z, L.y, L.x), generator=torch.Generator().manual_seed(1234))
+        for di in range(m.domain.num_domains()):
+            d = m.domain.domain(di)
+            o, s = d.origin(), d.size()
+            m.interior(di).copy_(u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x].to(m.interior(di).device))
+        if backend == st.Backend.Device:
+            torch.cuda.synchronize()
     else:
         u = torch.full((L.z, L.y, L.x), 0.5)
-    for _ in range(3):
+    if backend == st.Backend.Device and u.numel() > 1 << 24:  # big grids: the oracle runs on the GPU too
+        u = u.cuda()
+    if os.environ.get("MP_PREPARE") == "1":
+        m.prepare()
+    first = int(os.environ.get("MP_SINGLE_STEPS", "3"))
+    for _ in range(first):
         m.step()
         u = ref(u)
-    m.run(5)  # fused pairs when temporal blocking is on
-    for _ in range(5):
+    pairs = int(os.environ.get("MP_RUN_STEPS", "5"))
+    m.run(pairs)  # fused pairs when temporal blocking is on
+    for _ in range(pairs):
         u = ref(u)
     bad = 0
     if os.environ.get("MP_TOGGLE_OVERLAP"):  # whole-region pairs, then back to overlapped ones (set_overlap)
         bad += int(not m.can_toggle_overlap())
         if m.can_toggle_overlap():
-            for mode, reserve in ((0, 8), (2, 8), (1, 16), (1, 8)):
+            modes = ((0, 8), (2, 8), (1, 16), (1, 8))
+            if os.environ.get("MP_TOGGLE_MODES"):  # e.g. "2": only that mode, with the default reserve
+                modes = tuple((int(c), 8) for c in os.environ["MP_TOGGLE_MODES"])
+            k = int(os.environ.get("MP_TOGGLE_STEPS", "4" if len(modes) > 1 else "16"))
+            for mode, reserve in modes:
                 m.set_overlap_mode(mode)
                 m.set_comm_reserve(reserve)
                 bad += int(m.overlap_mode() != mode or m.comm_reserve() != reserve)
-                m.run(4)
-                for _ in range(4):
+                m.run(k)
+                for _ in range(k):
                     u = ref(u)
     m.synchronize()
     for di in range(m.domain.num_domains()):
         d = m.domain.domain(di)
         o, s = d.origin(), d.size()
-        got = m.interior(di).cpu()
+        got = m.interior(di).to(u.device)
         bad += int((got != u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x]).sum())
     if os.environ.get("MP_EXPECT_WRAP") is not None:  # axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
         bad += int(m.wrap_axes() != int(os.environ["MP_EXPECT_WRAP"]))

@@ -707,6 +707,41 @@ def test_staged_two_ranks_one_gpu():
         assert rc == 0, out[-3000:]
 
 
+def test_headline_config_bitwise(st):
+    """BASELINE config 2 exactly as bench.py runs it: 512^3 Jacobi3D fp32 on one GPU, bench.py's default StencilTune
+    (whole-row fused pairs, lockstep quarter-major schedule, x/y/z wrapped in-kernel so no halo is copied),
+    prepare()'d hipGraph blocks of 16 steps, 20 steps from a random field; bitwise vs the torch oracle on GPU
+    tensors (reference test style: test/test_exchange.cu:135-201)."""
+    m = st.Jacobi3D((512, 512, 512), gpus=[0], temporal=2, tune=st.StencilTune())
+    m.init()
+    assert m.temporal_blocking() and m.wrap_axes() == 7 and not m.overlapping()
+    m.prepare()
+    u = torch.rand((512, 512, 512), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+    m.interior(0).copy_(u)
+    torch.cuda.synchronize()
+    m.run(20)
+    m.synchronize()
+    for _ in range(20):
+        u = jacobi_step_reference(u)
+    got = m.interior(0)
+    assert torch.equal(got, u), f"{int((got != u).sum())} cells differ"
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_headline_two_rank_exact_grid_bitwise(mode):
+    """bench.py's 2-GPU weak-scaling grid (512x512x1024, cut 1x1x2, 512^3 per rank) with two ranks sharing one GPU
+    over HIP IPC: fused pairs overlapped with the slabs beside (1) or after (2) the interior sweep, or whole-region
+    (0), from a random field; bitwise vs the torch oracle (computed on the GPU) after 1 + 8 + 16 steps."""
+    outs = run_ranks(2, WORKER, ["jacobi", "512,512,1024"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "30",
+                                "MP_TEMPORAL": "2", "MP_RANDOM": "1", "MP_PREPARE": "1", "MP_SINGLE_STEPS": "1",
+                                "MP_RUN_STEPS": "8", "MP_TOGGLE_OVERLAP": "1", "MP_TOGGLE_MODES": mode,
+                                "MP_EXPECT_OVERLAP": "1"}, timeout=200)
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out and "dim (1, 1, 2)" in out.replace("Dim3", ""), out[-2000:]
+
+
 def test_smoke_entry():
     import __graft_entry__ as g
 
