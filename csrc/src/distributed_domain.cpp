@@ -135,6 +135,16 @@ struct Channel {
   int64_t slotStride = 0;
 };
 
+// PeerCopy over a DMA engine (TransportOptions::peerCopy == Engine): every message from one local sub-domain to
+// another (on a peer GPU of this process) is packed into sbuf on the source GPU, copied by hipMemcpyPeerAsync into
+// rbuf on the destination GPU and unpacked there (reference PeerCopySender, tx_cuda.cuh:106-170)
+struct PeerPipe {
+  int srcDom = -1, dstDom = -1, srcDev = -1, dstDev = -1;
+  std::vector<Message> msgs; // sorted by dir
+  char *sbuf = nullptr, *rbuf = nullptr;
+  int64_t bytes[2] = {0, 0}; // packed bytes: all messages / without the directions prepare_skip_wrapped leaves out
+};
+
 struct DevCtx {
   int dev = -1;
   Stream comm;
@@ -147,6 +157,10 @@ struct DevCtx {
   std::vector<int> coloSend, coloRecv, rcclSend, rcclRecv, stagedSend, stagedRecv;
   SegList coloPack, coloUnpack;   // variant = parity*2 + slot
   SegList coloPackLocal;          // Engine copies: pack into the channels' local staging buffers (variant = parity)
+  // PeerCopy pipes leaving / entering this device ([0] all messages, [1] the prepare_skip_wrapped subset)
+  std::vector<int> pipesOut, pipesIn;
+  SegList pipePack[2], pipeUnpack[2];
+  Event pipeSent, pipeUnpacked;
   SegList rcclPack, rcclUnpack;   // variant = parity
   SegList stagedPack, stagedUnpack;
   rccl::Comm nccl = nullptr;
@@ -165,6 +179,7 @@ struct DistributedDomain::Impl {
   SegList hostTranslate, hostStagedPack, hostStagedUnpack;
   bool rccl = false;
   std::vector<std::tuple<int, int, Dim3>> localTranslates; // (srcDom, dstDom, dir) of the Kernel/PeerCopy messages
+  std::vector<PeerPipe> pipes;                               // PeerCopy messages over DMA engines (see PeerPipe)
   int skipAxes = 0;                                         // axes translateSkip leaves out (0 = not prepared)
   // exchanges enqueued on a caller stream (single device) vs on the comm stream: each kind waits for the last
   // exchange of the other kind, so the two never race on the IPC inbox slots / flags, and sync_exchange() also
@@ -211,6 +226,10 @@ DistributedDomain::~DistributedDomain() {
     } catch (...) {
     }
   }
+  for (auto &pp : I.pipes) {
+    if (pp.sbuf) (void)hipFree(pp.sbuf);
+    if (pp.rbuf) (void)hipFree(pp.rbuf);
+  }
   for (auto &c : I.chans) {
     if (c.dbuf) (void)hipFree(c.dbuf);
     if (c.hbuf) (void)hipHostFree(c.hbuf);
@@ -235,6 +254,10 @@ DistributedDomain::~DistributedDomain() {
     d.translateSkip.release();
     d.coloPack.release();
     d.coloPackLocal.release();
+    for (int k = 0; k < 2; ++k) {
+      d.pipePack[k].release();
+      d.pipeUnpack[k].release();
+    }
     d.coloUnpack.release();
     d.rcclPack.release();
     d.rcclUnpack.release();
@@ -708,6 +731,7 @@ void DistributedDomain::realize() {
   // channel maps: (method, localDom, remoteLinear) -> channel index
   std::map<std::tuple<int, int, int64_t>, int> sendKey, recvKey;
   std::vector<std::tuple<int, int, Dim3>> localTranslates; // (srcDom, dstDom, dir)
+  std::map<std::pair<int, int>, std::vector<Message>> pipeMsgs; // PeerCopy over DMA engines: (srcDom, dstDom) -> msgs
   plan_.clear();
   remoteHalo_.assign(domains_.size(), std::array<uint8_t, 27>{});
   for (size_t di = 0; di < domains_.size(); ++di) {
@@ -726,7 +750,9 @@ void DistributedDomain::realize() {
         int64_t bytes = 0;
         for (int64_t q = 0; q < domains_[di].num_data(); ++q) bytes += domains_[di].halo_bytes(-dir, q);
         plan_.push_back({m, myIdx, dstIdx, myRank, dstRank, myDev, dstDev, dir, bytes});
-        if (m == MethodFlags::Kernel || m == MethodFlags::PeerCopy) {
+        if (m == MethodFlags::PeerCopy && topt_.peerCopy == TransportOptions::Copy::Engine && dstId != int(di) && dev) {
+          pipeMsgs[{int(di), dstId}].push_back(Message{dir, int(di), dstId});
+        } else if (m == MethodFlags::Kernel || m == MethodFlags::PeerCopy) {
           localTranslates.emplace_back(int(di), dstId, dir);
         } else {
           const auto key = std::make_tuple(int(m), int(di), linearize(dstIdx, gdim));
@@ -854,6 +880,37 @@ void DistributedDomain::realize() {
       DevCtx &ctx = I.devs[I.devIndex[s.gpu()]];
       for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, ctx.translate.host[p]);
       if (d.gpu() != s.gpu()) I.devs[I.devIndex[d.gpu()]].peerWriters.insert(s.gpu());
+    }
+    for (auto &kv : pipeMsgs) {
+      PeerPipe pp;
+      pp.srcDom = kv.first.first;
+      pp.dstDom = kv.first.second;
+      pp.srcDev = domains_[size_t(pp.srcDom)].gpu();
+      pp.dstDev = domains_[size_t(pp.dstDom)].gpu();
+      pp.msgs = kv.second;
+      std::sort(pp.msgs.begin(), pp.msgs.end());
+      pp.bytes[0] = pp.bytes[1] = packed_size(domains_[size_t(pp.srcDom)], pp.msgs);
+      const size_t nb = size_t(std::max<int64_t>(pp.bytes[0], 1));
+      HIP_CHECK(hipSetDevice(pp.srcDev));
+      HIP_CHECK(hipMalloc(&pp.sbuf, nb));
+      HIP_CHECK(hipSetDevice(pp.dstDev));
+      HIP_CHECK(hipMalloc(&pp.rbuf, nb));
+      const int k = int(I.pipes.size());
+      DevCtx &sc = I.devs[size_t(I.devIndex[pp.srcDev])];
+      DevCtx &dc = I.devs[size_t(I.devIndex[pp.dstDev])];
+      sc.pipesOut.push_back(k);
+      dc.pipesIn.push_back(k);
+      for (int p = 0; p < 2; ++p) {
+        build_pack(domains_[size_t(pp.srcDom)], pp.msgs, pp.sbuf, p == 0, sc.pipePack[0].host[p]);
+        build_unpack(domains_[size_t(pp.dstDom)], pp.msgs, pp.rbuf, p == 0, dc.pipeUnpack[0].host[p]);
+      }
+      I.pipes.push_back(std::move(pp));
+    }
+    for (auto &ctx : I.devs) {
+      ctx.pipePack[0].upload(ctx.dev);
+      ctx.pipeUnpack[0].upload(ctx.dev);
+      if (!ctx.pipesOut.empty()) ctx.pipeSent = Event(ctx.dev);
+      if (!ctx.pipesIn.empty()) ctx.pipeUnpacked = Event(ctx.dev);
     }
 
     // channel buffers
@@ -1323,6 +1380,33 @@ void DistributedDomain::prepare_skip_wrapped(int axes) {
     for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p]);
   }
   for (auto &ctx : I.devs) ctx.translateSkip.upload(ctx.dev);
+  // PeerCopy pipes: the same subset, packed compactly
+  for (auto &ctx : I.devs) {
+    ctx.pipePack[1].release();
+    ctx.pipePack[1] = SegList();
+    ctx.pipeUnpack[1].release();
+    ctx.pipeUnpack[1] = SegList();
+  }
+  for (auto &pp : I.pipes) {
+    std::vector<Message> keep;
+    for (const Message &mm : pp.msgs) {
+      const Dim3 dir = mm.dir;
+      if (((axes & 1) && dir.x != 0) || ((axes & 2) && dir.y != 0) || ((axes & 4) && dir.z != 0)) continue;
+      keep.push_back(mm);
+    }
+    pp.bytes[1] = keep.empty() ? 0 : packed_size(domains_[size_t(pp.srcDom)], keep);
+    if (keep.empty()) continue;
+    DevCtx &sc = I.devs[size_t(I.devIndex[pp.srcDev])];
+    DevCtx &dc = I.devs[size_t(I.devIndex[pp.dstDev])];
+    for (int p = 0; p < 2; ++p) {
+      build_pack(domains_[size_t(pp.srcDom)], keep, pp.sbuf, p == 0, sc.pipePack[1].host[p]);
+      build_unpack(domains_[size_t(pp.dstDom)], keep, pp.rbuf, p == 0, dc.pipeUnpack[1].host[p]);
+    }
+  }
+  for (auto &ctx : I.devs) {
+    ctx.pipePack[1].upload(ctx.dev);
+    ctx.pipeUnpack[1].upload(ctx.dev);
+  }
   I.skipAxes = axes;
 }
 
@@ -1439,6 +1523,43 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     ctx.translateEmpty = tl.host[parity].empty();
     if (!ctx.translateEmpty) tl.run_device(parity, S(ctx));
     if (!over) ctx.translated.record(S(ctx)); // events only matter across streams
+  }
+
+  // (1b) PeerCopy over DMA engines: pack on the source GPU, one peer copy per pipe, unpack on the destination
+  //      GPU once the copies into it have landed; a receive buffer is overwritten only after its previous unpack
+  if (!I.pipes.empty()) {
+    TraceRange t("peer copy (engine)");
+    const int pv = skipAxes != 0 ? 1 : 0;
+    for (auto &ctx : I.devs) {
+      if (ctx.pipesOut.empty()) continue;
+      HIP_CHECK(hipSetDevice(ctx.dev));
+      ctx.pipePack[pv].run_device(parity, S(ctx), commBlocks_);
+      std::set<int> dsts;
+      for (int k : ctx.pipesOut) dsts.insert(I.pipes[size_t(k)].dstDev);
+      if (!over && I.epoch > 1)
+        for (int d : dsts) I.devs[size_t(I.devIndex[d])].pipeUnpacked.wait_on(S(ctx));
+      for (int k : ctx.pipesOut) {
+        const PeerPipe &pp = I.pipes[size_t(k)];
+        const size_t nb = size_t(pp.bytes[pv]);
+        if (nb == 0) continue;
+        if (pp.srcDev == pp.dstDev)
+          engine_copy(pp.rbuf, pp.sbuf, nb, S(ctx));
+        else
+          HIP_CHECK(hipMemcpyPeerAsync(pp.rbuf, pp.dstDev, pp.sbuf, pp.srcDev, nb, S(ctx)));
+      }
+      if (!over) ctx.pipeSent.record(S(ctx));
+    }
+    for (auto &ctx : I.devs) {
+      if (ctx.pipesIn.empty()) continue;
+      HIP_CHECK(hipSetDevice(ctx.dev));
+      if (!over) {
+        std::set<int> srcs;
+        for (int k : ctx.pipesIn) srcs.insert(I.pipes[size_t(k)].srcDev);
+        for (int d : srcs) I.devs[size_t(I.devIndex[d])].pipeSent.wait_on(S(ctx));
+      }
+      ctx.pipeUnpack[pv].run_device(parity, S(ctx), commBlocks_);
+      if (!over) ctx.pipeUnpacked.record(S(ctx));
+    }
   }
 
   jitter();

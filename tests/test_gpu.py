@@ -14,9 +14,11 @@ pytestmark = pytest.mark.gpu
 WORKER = os.path.join(os.path.dirname(__file__), "mp_worker.py")
 
 
-def _dd(st, size, radius, gpus, methods, dtype=torch.int64):
+def _dd(st, size, radius, gpus, methods, dtype=torch.int64, transport=None):
     dd = st.DistributedDomain(*size, group=st.make_single_group())
     dd.set_backend(st.Backend.Device)
+    if transport is not None:
+        dd.set_transport_options(transport)
     dd.set_radius(radius)
     dd.set_gpus(gpus)
     dd.set_methods(methods)
@@ -36,11 +38,18 @@ def _radii(st):
 
 
 @pytest.mark.parametrize("method,gpus", [("Kernel", [0]), ("Kernel", [0, 0]), ("PeerCopy", [0, 0]),
+                                         ("PeerCopyEngine", [0, 0]), ("PeerCopyEngine", [0, 0, 0]),
                                          ("Rccl", [0, 0]), ("Staged", [0, 0]), ("All", [0, 0, 0])])
 @pytest.mark.parametrize("rname", ["r1", "r3", "asym", "fec", "mixed"])
 def test_device_exchange(st, method, gpus, rname):
+    """PeerCopyEngine: PeerCopy messages between sub-domains packed, copied by a DMA engine, unpacked
+    (TransportOptions.peer_copy = Engine; self-neighbour messages stay direct stores)."""
     radius = _radii(st)[rname]
-    dd, q = _dd(st, (19, 13, 11), radius, gpus, getattr(st.MethodFlags, method))
+    tr = st.TransportOptions()
+    if method == "PeerCopyEngine":
+        tr.peer_copy = st.TransportOptions.Copy.Engine
+        method = "PeerCopy"
+    dd, q = _dd(st, (19, 13, 11), radius, gpus, getattr(st.MethodFlags, method), transport=tr)
     for it in range(2):
         fill_coords(dd, q)
         dd.exchange()
@@ -500,10 +509,15 @@ def test_temporal2_row_kernel_lockstep_quarters(st, fake, reserve, lockstep, alt
     assert torch.equal(_gather(m), u)
 
 
-@pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy"])
+@pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy", "PeerCopyEngine"])
 def test_jacobi_temporal2_transports(st, methods):
-    """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs"""
-    m = st.Jacobi3D((40, 36, 44), gpus=[0, 0], methods=getattr(st.MethodFlags, methods), temporal=2)
+    """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs (PeerCopyEngine: the
+    peer messages over DMA-engine copies, including the in-kernel-wrap subset prepared by prepare_skip_wrapped)"""
+    tr = st.TransportOptions()
+    if methods == "PeerCopyEngine":
+        tr.peer_copy = st.TransportOptions.Copy.Engine
+        methods = "PeerCopy"
+    m = st.Jacobi3D((40, 36, 44), gpus=[0, 0], methods=getattr(st.MethodFlags, methods), temporal=2, transport=tr)
     m.init()
     assert m.temporal_blocking()
     u = _gather(m)
