@@ -107,6 +107,14 @@ struct TransportOptions {
   // sleep a random 0..jitterUs microseconds between transport phases of every exchange (race canary; reference's
   // unused rand_sleep(), packer.cuh:17-20)
   int jitterUs = 0;
+  // blocking exchange(): the last op of every comm stream stores the exchange's epoch into a host-mapped word and
+  // the host spins on it (bounded) before the stream synchronize, which then returns at once; false: block in
+  // hipStreamSynchronize right away (its wake-up comes several microseconds after the work completes)
+  bool spinWait = true;
+  // blocking exchange() without record_ready(): the producers of the fields are taken to be on the null stream or
+  // blocking streams (torch's default stream, synchronous copies) and the comm streams wait for an event recorded on
+  // the null stream; false: hipDeviceSynchronize (also covers non-blocking producer streams)
+  bool nullStreamProducers = false;
 };
 const char *to_string(TransportOptions::Inbox v);
 const char *to_string(TransportOptions::Copy v);
@@ -171,6 +179,9 @@ public:
   // switch how Colocated messages reach the peer inbox between exchanges (both paths are prepared by realize);
   // waits for the exchanges in flight first
   void set_colo_copy(TransportOptions::Copy c);
+  // change the run-time fields (colo copy, completion, spin wait, producer ordering, jitter, timeout) of a realized
+  // domain; the allocation-time fields (inbox, peer copy, probes) must stay as realized
+  void set_transport_options_live(const TransportOptions &o);
   void set_completion(TransportOptions::Completion c);
 
   void realize();

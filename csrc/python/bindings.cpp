@@ -472,6 +472,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fail_ipc_probe", &TransportOptions::failIpcProbe)
       .def_readwrite("fail_rccl_init", &TransportOptions::failRcclInit)
       .def_readwrite("jitter_us", &TransportOptions::jitterUs)
+      .def_readwrite("spin_wait", &TransportOptions::spinWait)
+      .def_readwrite("null_stream_producers", &TransportOptions::nullStreamProducers)
       .def("__repr__", [](const TransportOptions &o) {
         return std::string("TransportOptions(inbox=") + to_string(o.inbox) + ", colo_copy=" + to_string(o.coloCopy) +
                ", peer_copy=" + to_string(o.peerCopy) + ", completion=" + to_string(o.completion) +
@@ -531,6 +533,18 @@ PYBIND11_MODULE(_C, m) {
       .def("transport_options", &DistributedDomain::transport_options)
       .def("set_colo_copy", &DistributedDomain::set_colo_copy, py::call_guard<py::gil_scoped_release>())
       .def("set_completion", &DistributedDomain::set_completion, py::call_guard<py::gil_scoped_release>())
+      .def("set_spin_wait", [](DistributedDomain &d, bool on) {
+        TransportOptions o = d.transport_options();
+        o.spinWait = on;
+        d.set_transport_options_live(o);
+      })
+      .def("set_transport_options_live", &DistributedDomain::set_transport_options_live,
+           py::call_guard<py::gil_scoped_release>())
+      .def("set_null_stream_producers", [](DistributedDomain &d, bool on) {
+        TransportOptions o = d.transport_options();
+        o.nullStreamProducers = on;
+        d.set_transport_options_live(o);
+      })
       .def("poisoned", &DistributedDomain::poisoned)
       .def("set_self_test", &DistributedDomain::set_self_test)
       .def("self_test_report", &DistributedDomain::self_test_report)

@@ -175,6 +175,9 @@ struct DistributedDomain::Impl {
   uint64_t epoch = 0;
   int *errHost = nullptr; // host-mapped timeout word
   int *errDev = nullptr;
+  uint64_t *doneHost = nullptr; // host-mapped epoch word per device (TransportOptions::spinWait)
+  uint64_t *doneDev = nullptr;
+  Event nullReady;              // TransportOptions::nullStreamProducers
   // host backend
   SegList hostTranslate, hostStagedPack, hostStagedUnpack;
   bool rccl = false;
@@ -271,6 +274,7 @@ DistributedDomain::~DistributedDomain() {
     }
   }
   if (I.errHost) (void)hipHostFree(I.errHost);
+  if (I.doneHost) (void)hipHostFree(I.doneHost);
 }
 
 int64_t DistributedDomain::add_data(int64_t elemSize, const std::string &name, DType dtype) {
@@ -867,6 +871,10 @@ void DistributedDomain::realize() {
     HIP_CHECK(hipHostMalloc((void **)&I.errHost, sizeof(int), hipHostMallocMapped));
     *I.errHost = 0;
     HIP_CHECK(hipHostGetDevicePointer((void **)&I.errDev, I.errHost, 0));
+    HIP_CHECK(hipHostMalloc((void **)&I.doneHost, sizeof(uint64_t) * I.devs.size(), hipHostMallocMapped));
+    for (size_t k = 0; k < I.devs.size(); ++k) I.doneHost[k] = 0;
+    HIP_CHECK(hipHostGetDevicePointer((void **)&I.doneDev, I.doneHost, 0));
+    I.nullReady = Event(I.devs[0].dev);
 
     // RCCL communicator over all (rank, device) pairs, created only if some rank needs it. An init error on any
     // rank (or TransportOptions::failRcclInit) is agreed on collectively and every RCCL channel falls back to the
@@ -1315,6 +1323,22 @@ void DistributedDomain::set_colo_copy(TransportOptions::Copy c) {
   topt_.coloCopy = c;
 }
 
+void DistributedDomain::set_transport_options_live(const TransportOptions &o) {
+  if (!realized_) {
+    set_transport_options(o);
+    return;
+  }
+  STENCIL_REQUIRE(o.inbox == topt_.inbox && o.peerCopy == topt_.peerCopy,
+                  "inbox memory and the peer-copy path are fixed at realize()");
+  set_colo_copy(o.coloCopy);
+  set_completion(o.completion);
+  topt_.spinWait = o.spinWait;
+  topt_.nullStreamProducers = o.nullStreamProducers;
+  topt_.jitterUs = o.jitterUs;
+  if (o.waitTimeout > 0) topt_.waitTimeout = o.waitTimeout;
+  topt_.fakeRemoteAxes = o.fakeRemoteAxes;
+}
+
 void DistributedDomain::set_completion(TransportOptions::Completion c) {
   if (c == topt_.completion) return;
   if (realized_) sync_exchange(); // flag words are monotonic epochs: either method continues where the other left off
@@ -1344,6 +1368,20 @@ void DistributedDomain::exchange() {
     t0 = now_s();
   }
   exchange_async();
+  Impl &I = *impl_;
+  if (backend_ == Backend::Device && topt_.spinWait && I.doneHost) {
+    // every comm stream ends with a store of this epoch into a host-mapped word; spin (bounded) until all landed,
+    // so the synchronize below finds the streams complete instead of sleeping until its wake-up
+    for (size_t k = 0; k < I.devs.size(); ++k) {
+      HIP_CHECK(hipSetDevice(I.devs[k].dev));
+      signal_flags_device({I.doneDev + k}, I.epoch, I.devs[k].comm);
+    }
+    const double ts = now_s();
+    for (size_t k = 0; k < I.devs.size(); ++k)
+      while (__atomic_load_n(&I.doneHost[k], __ATOMIC_ACQUIRE) < I.epoch && *I.errHost == 0 &&
+             now_s() - ts < topt_.waitTimeout) {
+      }
+  }
   sync_exchange();
   if (exchangeStats_) timeExchange_ += pg_->allreduce_max(now_s() - t0);
 }
@@ -1462,7 +1500,12 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   if (!over) {
     bool anyMissing = false;
     for (size_t di = 0; di < domains_.size(); ++di) anyMissing |= !I.readyPending[di];
-    if (anyMissing) {
+    if (anyMissing && topt_.nullStreamProducers && I.devs.size() == 1) {
+      // producers on the null stream / blocking streams: order after them without a host round trip
+      HIP_CHECK(hipSetDevice(I.devs[0].dev));
+      I.nullReady.record(nullptr);
+      I.nullReady.wait_on(S(I.devs[0]));
+    } else if (anyMissing) {
       for (auto &d : I.devs) {
         HIP_CHECK(hipSetDevice(d.dev));
         HIP_CHECK(hipDeviceSynchronize());
