@@ -115,6 +115,9 @@ struct TransportOptions {
   // blocking streams (torch's default stream, synchronous copies) and the comm streams wait for an event recorded on
   // the null stream; false: hipDeviceSynchronize (also covers non-blocking producer streams)
   bool nullStreamProducers = false;
+  // device backend: when every GPU of this process sits on one NUMA node, realize() binds the calling thread to that
+  // node's CPUs and allocates the host-staged (pinned) buffers there
+  bool numaAffinity = true;
 };
 const char *to_string(TransportOptions::Inbox v);
 const char *to_string(TransportOptions::Copy v);
@@ -301,6 +304,12 @@ private:
   void poison(const std::string &why);
   void init_rccl(const std::function<bool(int, int)> &sharedDev); // realize(): communicator or staged fallback
   std::string planPrefix_ = "plan";
+  int numaNode_ = -1; // NUMA node the calling thread was bound to in realize() (-1: none)
+
+public:
+  int numa_node() const { return numaNode_; }
+
+private:
   std::unique_ptr<Placement> placement_;
   std::vector<LocalDomain> domains_;
   std::vector<ExchangePlanEntry> plan_;

@@ -34,8 +34,13 @@ struct LinkInfo {
   std::string source;                  // "amd-smi", "hip" or "none"
 };
 std::vector<LinkInfo> links();
-// NUMA node of a device (amd-smi), -1 if unknown; used to pin host-staged buffers / ranks
+// NUMA node of a device (amd-smi, else the PCI function's sysfs entry), -1 if unknown
 int numa_node(int dev);
+// CPUs of a NUMA node (sysfs cpulist), empty if unknown
+std::vector<int> numa_cpus(int node);
+// restrict the calling thread (and the threads it creates later) to the CPUs of `node` that this process may use;
+// false if the node or its CPUs are unknown. Host-staged buffers allocated afterwards are first touched there.
+bool bind_thread_to_numa(int node);
 // whether the amd-smi library was found and initialised
 bool smi_available();
 

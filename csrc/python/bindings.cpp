@@ -378,6 +378,7 @@ PYBIND11_MODULE(_C, m) {
     return l;
   });
   m.def("gpu_numa_node", &gpu_topo::numa_node);
+  m.def("numa_cpus", &gpu_topo::numa_cpus);
   m.def("amdsmi_available", &gpu_topo::smi_available);
 
   // ---------------- statistics ----------------
@@ -473,6 +474,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fail_rccl_init", &TransportOptions::failRcclInit)
       .def_readwrite("jitter_us", &TransportOptions::jitterUs)
       .def_readwrite("spin_wait", &TransportOptions::spinWait)
+      .def_readwrite("numa_affinity", &TransportOptions::numaAffinity)
       .def_readwrite("null_stream_producers", &TransportOptions::nullStreamProducers)
       .def("__repr__", [](const TransportOptions &o) {
         return std::string("TransportOptions(inbox=") + to_string(o.inbox) + ", colo_copy=" + to_string(o.coloCopy) +
@@ -546,6 +548,7 @@ PYBIND11_MODULE(_C, m) {
         d.set_transport_options_live(o);
       })
       .def("poisoned", &DistributedDomain::poisoned)
+      .def("numa_node", &DistributedDomain::numa_node)
       .def("set_self_test", &DistributedDomain::set_self_test)
       .def("self_test_report", &DistributedDomain::self_test_report)
       .def("probe_transports", &DistributedDomain::probe_transports, py::call_guard<py::gil_scoped_release>())

@@ -559,6 +559,17 @@ void DistributedDomain::realize() {
         if (a != b) gpu_topo::enable_peer(a, b);
   }
   timePeerEn_ = setup_time(now_s() - t0);
+  if (dev && topt_.numaAffinity) {
+    int node = -2;
+    for (int g : gpus_) {
+      const int n = gpu_topo::numa_node(g);
+      node = node == -2 ? n : (node == n ? node : -1);
+    }
+    if (node >= 0 && gpu_topo::bind_thread_to_numa(node)) {
+      numaNode_ = node;
+      LOG_DEBUG("rank " << myRank << " bound to NUMA node " << node << " of its GPU(s)");
+    }
+  }
 
   // ---- placement ----
   t0 = now_s();
@@ -929,7 +940,8 @@ void DistributedDomain::realize() {
       const size_t nb = size_t(std::max<int64_t>(c.bytes, 1));
       if (c.method == MethodFlags::Staged) {
         HIP_CHECK(hipMalloc(&c.dbuf, nb));
-        HIP_CHECK(hipHostMalloc((void **)&c.hbuf, nb, hipHostMallocDefault));
+        // pinned on the GPU's NUMA node when realize() bound this thread there (pages follow the thread's policy)
+        HIP_CHECK(hipHostMalloc((void **)&c.hbuf, nb, numaNode_ >= 0 ? hipHostMallocNumaUser : hipHostMallocDefault));
         (c.send ? ctx.stagedSend : ctx.stagedRecv).push_back(ci);
       } else if (c.method == MethodFlags::Rccl) {
         HIP_CHECK(hipMalloc(&c.dbuf, nb));

@@ -1,6 +1,12 @@
 #include "stencil/topo/gpu_topology.hpp"
 #include "stencil/rt/env.hpp"
 
+#include <sched.h>
+
+#include <cctype>
+#include <fstream>
+#include <sstream>
+
 #include <hip/hip_runtime_api.h>
 
 #include <amd_smi/amdsmi.h>
@@ -105,7 +111,55 @@ int numa_node(int dev) {
   amdsmi_processor_handle h = s.handle(dev);
   uint32_t n = 0;
   if (h && s.numa(h, &n) == AMDSMI_STATUS_SUCCESS) return int(n);
+  // sysfs: the PCI function's NUMA node
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  std::string b(bus);
+  for (auto &c : b) c = char(std::tolower(c));
+  std::ifstream f("/sys/bus/pci/devices/" + b + "/numa_node");
+  int node = -1;
+  if (f >> node) return node;
   return -1;
+}
+
+std::vector<int> numa_cpus(int node) {
+  std::vector<int> cpus;
+  if (node < 0) return cpus;
+  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!(f >> list)) return cpus;
+  std::stringstream ss(list);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    const size_t dash = part.find('-');
+    try {
+      const int a = std::stoi(part.substr(0, dash));
+      const int b = dash == std::string::npos ? a : std::stoi(part.substr(dash + 1));
+      for (int c = a; c <= b; ++c) cpus.push_back(c);
+    } catch (...) {
+      return {};
+    }
+  }
+  return cpus;
+}
+
+bool bind_thread_to_numa(int node) {
+  const std::vector<int> cpus = numa_cpus(node);
+  if (cpus.empty()) return false;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus)
+    if (c < CPU_SETSIZE) CPU_SET(c, &set);
+  // keep only CPUs this process may use at all (a container / cgroup cpuset may exclude some)
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
+    CPU_AND(&set, &set, &allowed);
+    if (CPU_COUNT(&set) == 0) return false;
+  }
+  return sched_setaffinity(0, sizeof(set), &set) == 0;
 }
 
 static constexpr uint32_t kLinkPcie = 2; // HSA_AMD_LINK_INFO_TYPE_PCIE
