@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "stencil/comm/rccl_comm.hpp"
 #include "stencil/comm/tags.hpp"
 #include "stencil/core/array.hpp"
 #include "stencil/core/boundary.hpp"
@@ -15,7 +16,9 @@
 #include "stencil/kernels/stencil_ops.hpp"
 #include "stencil/rt/stream.hpp"
 #include "stencil/rt/allocator.hpp"
+#include "stencil/rt/build_info.hpp"
 #include "stencil/rt/statistics.hpp"
+#include "stencil/topo/gpu_topology.hpp"
 #include "stencil/topo/partition.hpp"
 #include "stencil/topo/qap.hpp"
 
@@ -355,6 +358,54 @@ static void check_x2_split(StencilKind kind) {
 }
 TEST(gpu_x2_split_regions_jacobi, true) { check_x2_split(StencilKind::Jacobi); }
 TEST(gpu_x2_split_regions_astaroth, true) { check_x2_split(StencilKind::Astaroth); }
+
+TEST(transport_options_defaults, false) {
+  TransportOptions o;
+  CHECK(o.inbox == TransportOptions::Inbox::Uncached && o.coloCopy == TransportOptions::Copy::Store &&
+        o.peerCopy == TransportOptions::Copy::Store && o.completion == TransportOptions::Completion::Kernel);
+  CHECK(std::string(to_string(TransportOptions::Inbox::Coarse)) == "coarse");
+  CHECK(std::string(to_string(TransportOptions::Copy::Engine)) == "engine");
+  CHECK(std::string(to_string(TransportOptions::Completion::StreamOp)) == "streamop");
+  // waitTimeout <= 0 resolves to STENCIL_WAIT_TIMEOUT or 60 s at set_transport_options
+  DistributedDomain dd(8, 8, 8, comm::make_single_group());
+  dd.set_transport_options(o);
+  CHECK(dd.transport_options().waitTimeout > 0);
+}
+
+TEST(build_info_embedded, false) {
+  const BuildInfo &b = build_info();
+  CHECK(!b.gitSha.empty() && b.offloadArch == "gfx950");
+  CHECK(b.useRccl == rccl::compiled());
+  CHECK(build_info_string().find("git=") != std::string::npos);
+}
+
+TEST(rccl_unique_id_or_reason, false) {
+  // without a GPU RCCL may refuse; either way the wrapper reports instead of aborting
+  rccl::UniqueId id{};
+  const std::string e = rccl::get_unique_id(&id);
+  CHECK(e.empty() || e.find("nccl") != std::string::npos || e.find("RCCL") != std::string::npos);
+}
+
+TEST(numa_cpulist_parse, false) {
+  // node 0 exists on every Linux host with sysfs; unknown nodes give nothing
+  const auto c0 = gpu_topo::numa_cpus(0);
+  CHECK(gpu_topo::numa_cpus(-1).empty() && gpu_topo::numa_cpus(1 << 20).empty());
+  for (size_t i = 1; i < c0.size(); ++i) CHECK(c0[i] > c0[i - 1]);
+}
+
+TEST(host_self_test_ladder_single_rank, false) {
+  // a single rank has no ladder to climb; probe_transports still runs the coordinate oracle on the host backend
+  DistributedDomain dd(20, 16, 12, comm::make_single_group());
+  dd.set_backend(Backend::Host);
+  dd.set_radius(Radius::face_edge_corner(2, 1, 1));
+  dd.add_data<float>("d");
+  CHECK(dd.probe_transports(MethodFlags::All) == 0);
+}
+
+TEST(process_group_bounded_barrier, false) {
+  auto g = comm::make_single_group();
+  CHECK(g->barrier_for(0.1));
+}
 
 int main(int argc, char **argv) {
   bool cpu = true, gpu = false;
