@@ -63,6 +63,32 @@ def test_jacobi3d_csv():
     assert float(m.group(2)) > 0 and float(m.group(4)) > 0
 
 
+def _check_jacobi_dump(prefix, n, steps):
+    """The app's final ParaView dump vs the torch oracle after `steps` steps from the 0.5 initial field (the dump
+    prints 6 decimals: |err| <= 5e-7)."""
+    import torch
+
+    from stencil2_amd.ops import jacobi_step_reference
+    from stencil2_amd.utils.paraview import paraview_grid
+
+    got = paraview_grid(prefix, "d", (n, n, n))
+    u = torch.full((n, n, n), 0.5, dtype=torch.float32)
+    for _ in range(steps):
+        u = jacobi_step_reference(u)
+    err = (got - u.double()).abs().max().item()
+    assert err <= 5.01e-7, err
+
+
+@pytest.mark.parametrize("temporal", [1, 2])
+def test_jacobi3d_result_vs_oracle(tmp_path, temporal):
+    """The jacobi3d app's field (its final ParaView dump) equals the torch oracle, not just its CSV shape:
+    host backend (no fused pairs there: --temporal 2 runs single steps), warm-up + timed sweeps = 4 steps."""
+    n = 24
+    run_app("jacobi3d", n, n, n, "-n", 3, "--warmup", 1, "--temporal", temporal, "--paraview", "--prefix",
+            str(tmp_path) + "/")
+    _check_jacobi_dump(str(tmp_path / "jacobi3d_final"), n, 4)
+
+
 def test_jacobi3d_two_ranks_weak_scaled():
     """Two ranks: the global grid follows the reference weak-scaling rule (24 * 2^0.33333 -> 30), rank 0 prints."""
     outs = run_app_ranks(2, "jacobi3d", 24, 24, 24, "-n", 2)

@@ -34,6 +34,25 @@ def test_jacobi3d_device(temporal):
     assert float(m.group(4)) > 0
 
 
+@pytest.mark.parametrize("temporal", [1, 2])
+def test_jacobi3d_device_result_vs_oracle(tmp_path, temporal):
+    """The jacobi3d app on the GPU: its final ParaView dump equals the torch oracle (warm-up + timed sweeps =
+    4 x temporal steps; the dump prints 6 decimals)."""
+    import torch
+
+    from stencil2_amd.ops import jacobi_step_reference
+    from stencil2_amd.utils.paraview import paraview_grid
+
+    n = 48
+    run_app("jacobi3d", n, n, n, "-n", 3, "--warmup", 1, "--temporal", temporal, "--paraview", "--prefix",
+            str(tmp_path) + "/")
+    got = paraview_grid(str(tmp_path / "jacobi3d_final"), "d", (n, n, n))
+    u = torch.full((n, n, n), 0.5, dtype=torch.float32)
+    for _ in range(4 * temporal):
+        u = jacobi_step_reference(u)
+    assert (got - u.double()).abs().max().item() <= 5.01e-7
+
+
 def test_astaroth_sim_device():
     out = run_app("astaroth_sim", "--x", 96, "--y", 96, "--z", 96, "--q", 2, "-n", 2)
     assert re.search(rf"^astaroth,[a-z/]+,1,96,96,96,2,{NUM},{NUM},{NUM},{NUM}$", out, re.M), out[-2000:]
