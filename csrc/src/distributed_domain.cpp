@@ -161,6 +161,11 @@ struct DevCtx {
   std::vector<int> pipesOut, pipesIn;
   SegList pipePack[2], pipeUnpack[2];
   Event pipeSent, pipeUnpacked;
+  // DMA-engine copies to different peers run concurrently: copies on one stream would execute one after another,
+  // so each peer's copy is forked onto its own copy stream (copy k of an exchange on copyStreams[k % n]) and joined
+  Event copyFork;
+  std::vector<Stream> copyStreams;
+  std::vector<Event> copyJoin;
   SegList rcclPack, rcclUnpack;   // variant = parity
   SegList stagedPack, stagedUnpack;
   rccl::Comm nccl = nullptr;
@@ -931,6 +936,21 @@ void DistributedDomain::realize() {
       if (!ctx.pipesOut.empty()) ctx.pipeSent = Event(ctx.dev);
       if (!ctx.pipesIn.empty()) ctx.pipeUnpacked = Event(ctx.dev);
     }
+    // copy streams for DMA-engine copies (Colocated sends and outgoing pipes of a device: at most 4 streams)
+    {
+      std::map<int, int> coloOut;
+      for (auto &c : I.chans)
+        if (c.method == MethodFlags::Colocated && c.send) ++coloOut[c.localDev];
+      for (auto &ctx : I.devs) {
+        const int n = std::min(4, std::max(coloOut[ctx.dev], int(ctx.pipesOut.size())));
+        if (n < 2) continue;
+        ctx.copyFork = Event(ctx.dev);
+        for (int k = 0; k < n; ++k) {
+          ctx.copyStreams.emplace_back(ctx.dev, Priority::HIGH);
+          ctx.copyJoin.emplace_back(ctx.dev);
+        }
+      }
+    }
 
     // channel buffers
     for (int ci = 0; ci < int(I.chans.size()); ++ci) {
@@ -1563,6 +1583,23 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     }
     HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st));
   };
+  // run copies[k] (k = 0..n-1) behind the work on `st`, on the device's copy streams when it has them (concurrent
+  // DMA engines / links), and make `st` wait for all of them
+  auto forked_copies = [&](DevCtx &ctx, hipStream_t st, int n, const std::function<void(int, hipStream_t)> &copy) {
+    const bool fork = !over && ctx.copyStreams.size() > 1 && n > 1;
+    if (!fork) {
+      for (int k = 0; k < n; ++k) copy(k, st);
+      return;
+    }
+    ctx.copyFork.record(st);
+    const int ns = std::min(n, int(ctx.copyStreams.size()));
+    for (int j = 0; j < ns; ++j) ctx.copyFork.wait_on(ctx.copyStreams[size_t(j)]);
+    for (int k = 0; k < n; ++k) copy(k, ctx.copyStreams[size_t(k % ns)]);
+    for (int j = 0; j < ns; ++j) {
+      ctx.copyJoin[size_t(j)].record(ctx.copyStreams[size_t(j)]);
+      ctx.copyJoin[size_t(j)].wait_on(st);
+    }
+  };
   // STENCIL_JITTER_US=N: sleep a random 0..N us between transport phases (reference's unused rand_sleep(),
   // packer.cuh:17-20) to shake out ordering assumptions between ranks and streams
   const int jitterUs = topt_.jitterUs;
@@ -1593,15 +1630,15 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       for (int k : ctx.pipesOut) dsts.insert(I.pipes[size_t(k)].dstDev);
       if (!over && I.epoch > 1)
         for (int d : dsts) I.devs[size_t(I.devIndex[d])].pipeUnpacked.wait_on(S(ctx));
-      for (int k : ctx.pipesOut) {
-        const PeerPipe &pp = I.pipes[size_t(k)];
+      forked_copies(ctx, S(ctx), int(ctx.pipesOut.size()), [&](int j, hipStream_t cs) {
+        const PeerPipe &pp = I.pipes[size_t(ctx.pipesOut[size_t(j)])];
         const size_t nb = size_t(pp.bytes[pv]);
-        if (nb == 0) continue;
+        if (nb == 0) return;
         if (pp.srcDev == pp.dstDev)
-          engine_copy(pp.rbuf, pp.sbuf, nb, S(ctx));
+          engine_copy(pp.rbuf, pp.sbuf, nb, cs);
         else
-          HIP_CHECK(hipMemcpyPeerAsync(pp.rbuf, pp.dstDev, pp.sbuf, pp.srcDev, nb, S(ctx)));
-      }
+          HIP_CHECK(hipMemcpyPeerAsync(pp.rbuf, pp.dstDev, pp.sbuf, pp.srcDev, nb, cs));
+      });
       if (!over) ctx.pipeSent.record(S(ctx));
     }
     for (auto &ctx : I.devs) {
@@ -1635,11 +1672,10 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       wait_flags(credits, I.epoch - 2, 1, S(ctx));
     }
     if (engine) {
-      for (int ci : ctx.coloSend) {
-        const Channel &c = I.chans[ci];
-        if (c.bytes > 0)
-          engine_copy(c.remoteData + slot * c.slotStride, c.dbuf, size_t(c.bytes), S(ctx));
-      }
+      forked_copies(ctx, S(ctx), int(ctx.coloSend.size()), [&](int k, hipStream_t cs) {
+        const Channel &c = I.chans[size_t(ctx.coloSend[size_t(k)])];
+        if (c.bytes > 0) engine_copy(c.remoteData + slot * c.slotStride, c.dbuf, size_t(c.bytes), cs);
+      });
     } else {
       ctx.coloPack.run_device(cv, S(ctx), commBlocks_);
     }
