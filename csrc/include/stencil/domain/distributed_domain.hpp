@@ -118,6 +118,9 @@ struct TransportOptions {
   // device backend: when every GPU of this process sits on one NUMA node, realize() binds the calling thread to that
   // node's CPUs and allocates the host-staged (pinned) buffers there
   bool numaAffinity = true;
+  // same-GPU x faces (translates) copied as whole 64-B sectors (4 lanes per row, the extra cells land in the
+  // receiver's row padding) instead of w-cell pieces of one sector per lane (build_translate_segs_q)
+  bool xFaceSectors = false;
 };
 const char *to_string(TransportOptions::Inbox v);
 const char *to_string(TransportOptions::Copy v);

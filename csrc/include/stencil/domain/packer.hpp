@@ -28,12 +28,13 @@ void build_pack_segs(const LocalDomain &dom, const std::vector<Message> &sortedM
                      std::vector<CopySeg> &out);
 void build_unpack_segs(const LocalDomain &dom, const std::vector<Message> &sortedMsgs, char *buf, bool curr,
                        std::vector<CopySeg> &out);
-// direct same-process translate: src interior slab -> dst -dir halo
+// direct same-process translate: src interior slab -> dst -dir halo. xSectors: copy x faces as whole 64-B sectors
+// where both layouts allow it (the extra cells land in the receiver's row padding), see build_translate_segs_q
 void build_translate_segs(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
-                          std::vector<CopySeg> &out);
+                          std::vector<CopySeg> &out, bool xSectors = false);
 // same for one quantity
 void build_translate_segs_q(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr, int64_t q,
-                            std::vector<CopySeg> &out);
+                            std::vector<CopySeg> &out, bool xSectors = false);
 
 class PackerBase {
 public:

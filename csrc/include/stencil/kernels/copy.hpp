@@ -38,7 +38,7 @@ struct CopySeg {
   uint32_t row_units; // vector units per row
   uint32_t ny;        // rows per z-plane
   uint32_t vec;       // bytes per unit (16, 8, 4, 2 or 1)
-  uint32_t pad_;
+  uint32_t flags;     // kSegWide: always one unit per item, even for rows of <= kNarrowMaxUnits units
   uint64_t unit_begin; // exclusive prefix sum of units over previous segments
   uint64_t units;      // row_units * ny * nz
   // device plans only: a second copy of the same shape and strides done by the same items (make_copy_plan pairs
@@ -62,6 +62,9 @@ void copy_segs_host(const std::vector<CopySeg> &segs);
 // Rows of at most this many vector units are copied one row per item (narrow rows, e.g. x faces); wider rows one
 // unit per item. make_copy_plan and the kernel's per-row template dispatch share this bound.
 constexpr uint32_t kNarrowMaxUnits = 4;
+// rows of whole 64-B sectors (x faces widened to sectors): 4 consecutive lanes move one row, so every wave
+// instruction reads / writes 16 complete sectors instead of 64 partial ones
+constexpr uint32_t kSegWide = 1;
 struct CopyWork {
   uint32_t seg;
   uint32_t first;

@@ -303,8 +303,8 @@ static void build_unpack(const LocalDomain &dom, const std::vector<Message> &msg
   build_unpack_segs(dom, msgs, buf, curr, out);
 }
 static void build_translate(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
-                            std::vector<CopySeg> &out) {
-  build_translate_segs(src, dst, dir, curr, out);
+                            std::vector<CopySeg> &out, bool xSectors = false) {
+  build_translate_segs(src, dst, dir, curr, out, xSectors);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -851,7 +851,8 @@ void DistributedDomain::realize() {
     // host backend: translate + staged only, all executed on the host
     for (const auto &t : localTranslates) {
       const LocalDomain &s = domains_[std::get<0>(t)], &d = domains_[std::get<1>(t)];
-      for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, I.hostTranslate.host[p]);
+      for (int p = 0; p < 2; ++p)
+        build_translate(s, d, std::get<2>(t), p == 0, I.hostTranslate.host[p], topt_.xFaceSectors);
     }
     for (auto &c : I.chans) {
       STENCIL_REQUIRE(c.method == MethodFlags::Staged, "host backend supports only Kernel/Staged transports");
@@ -902,7 +903,7 @@ void DistributedDomain::realize() {
     for (const auto &t : localTranslates) {
       const LocalDomain &s = domains_[std::get<0>(t)], &d = domains_[std::get<1>(t)];
       DevCtx &ctx = I.devs[I.devIndex[s.gpu()]];
-      for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, ctx.translate.host[p]);
+      for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, ctx.translate.host[p], topt_.xFaceSectors);
       if (d.gpu() != s.gpu()) I.devs[I.devIndex[d.gpu()]].peerWriters.insert(s.gpu());
     }
     for (auto &kv : pipeMsgs) {
@@ -1447,7 +1448,7 @@ void DistributedDomain::prepare_skip_wrapped(int axes) {
     if (((axes & 1) && dir.x != 0) || ((axes & 2) && dir.y != 0) || ((axes & 4) && dir.z != 0)) continue;
     const LocalDomain &sd = domains_[std::get<0>(t)], &dd = domains_[std::get<1>(t)];
     DevCtx &ctx = I.devs[I.devIndex[sd.gpu()]];
-    for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p]);
+    for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p], topt_.xFaceSectors);
   }
   for (auto &ctx : I.devs) ctx.translateSkip.upload(ctx.dev);
   // PeerCopy pipes: the same subset, packed compactly

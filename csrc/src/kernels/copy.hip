@@ -209,7 +209,9 @@ __global__ __launch_bounds__(1024) void copy_plan_kernel_narrow(const CopySeg *_
 static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
   std::vector<CopySeg> out;
   std::vector<bool> used(in.size(), false);
-  auto narrow = [](const CopySeg &s) { return s.units && s.row_units <= kNarrowMaxUnits && !s.src2; };
+  auto narrow = [](const CopySeg &s) {
+    return s.units && s.row_units <= kNarrowMaxUnits && !s.src2 && !(s.flags & kSegWide);
+  };
   for (size_t i = 0; i < in.size(); ++i) {
     if (used[i]) continue;
     CopySeg a = in[i];
@@ -241,7 +243,7 @@ CopyPlan make_copy_plan(const std::vector<CopySeg> &segsIn, int device) {
     const CopySeg &s = segs[si];
     if (!s.units) continue;
     p.bytes += s.units * s.vec * (s.src2 ? 2 : 1);
-    const bool rows = s.row_units <= kNarrowMaxUnits;
+    const bool rows = s.row_units <= kNarrowMaxUnits && !(s.flags & kSegWide);
     const uint64_t items = rows ? s.units / s.row_units : s.units;
     STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
     for (uint64_t f = 0; f < items; f += perBlockUnits)

@@ -62,18 +62,53 @@ void build_unpack_segs(const LocalDomain &dom, const std::vector<Message> &msgs,
     }
 }
 
+// An x face (dir = (+-1, 0, 0)) is a strided column of w-cell row pieces: each row touches one 64-B sector of the
+// source and one of the receiver, the latter only partly written. Widened to whole sectors (S = 64 B / element)
+// the copy reads the same sectors and writes whole ones (the extra S - w cells land in the receiver's x padding in
+// front of its -x halo or behind its +x halo, which nothing reads). Needs both rows 64-B aligned at the interior (the
+// padded layout), interiors a multiple of S long and at least S long, and room for the sector in the receiver's row.
+static bool widen_x_face(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, int64_t q, Dim3 *sp, Dim3 *dp,
+                         Dim3 *ext) {
+  if (dir.y != 0 || dir.z != 0 || dir.x == 0) return false;
+  const int64_t es = src.elem_size(q);
+  if (es != dst.elem_size(q) || 64 % es != 0) return false;
+  const int64_t S = 64 / es, w = ext->x;
+  if (w > S || src.size().x % S || dst.size().x % S || src.size().x < S) return false;
+  const int64_t srxm = src.radius().x(-1), drxm = dst.radius().x(-1);
+  if ((src.pad_x(q) + srxm) % S || (dst.pad_x(q) + drxm) % S) return false; // interiors not sector aligned
+  const int64_t dRowEnd = dst.pitch(q).x - dst.pad_x(q);                      // raw x one past the dst row
+  if (dir.x > 0) { // +x face -> the receiver's -x halo: sector [nx - S, nx) -> [-S, 0) (global x)
+    sp->x -= S - w;
+    dp->x -= S - w;
+    if (dp->x < -dst.pad_x(q)) return false;
+  } else { // -x face -> the receiver's +x halo: [0, S) -> [nx, nx + S)
+    if (dp->x + S > dRowEnd) return false;
+  }
+  ext->x = S;
+  return true;
+}
+
 // direct translate src interior slab -> dst halo (same process)
 void build_translate_segs_q(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr, int64_t q,
-                            std::vector<CopySeg> &out) {
+                            std::vector<CopySeg> &out, bool xSectors) {
   const int64_t es = src.elem_size(q);
-  const Dim3 ext = src.halo_extent(-dir);
-  out.push_back(make_copy_seg(src.box(q, curr, src.halo_pos(dir, false)), dst.box(q, curr, dst.halo_pos(-dir, true)),
-                              ext, es));
+  Dim3 ext = src.halo_extent(-dir);
+  Dim3 sp = src.halo_pos(dir, false), dp = dst.halo_pos(-dir, true);
+  Dim3 wsp = sp, wdp = dp, wext = ext;
+  const bool wide = xSectors && widen_x_face(src, dst, dir, q, &wsp, &wdp, &wext);
+  if (wide) {
+    sp = wsp;
+    dp = wdp;
+    ext = wext;
+  }
+  CopySeg sg = make_copy_seg(src.box(q, curr, sp), dst.box(q, curr, dp), ext, es);
+  if (wide && sg.vec == 16) sg.flags |= kSegWide;
+  out.push_back(sg);
 }
 
 void build_translate_segs(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, bool curr,
-                          std::vector<CopySeg> &out) {
-  for (int64_t q = 0; q < src.num_data(); ++q) build_translate_segs_q(src, dst, dir, curr, q, out);
+                          std::vector<CopySeg> &out, bool xSectors) {
+  for (int64_t q = 0; q < src.num_data(); ++q) build_translate_segs_q(src, dst, dir, curr, q, out, xSectors);
 }
 
 

@@ -43,6 +43,15 @@ def _sphere_masks(shape_zyx, size_xyz, device):
     return dh < r1, dc < r1
 
 
+def _div6(val: torch.Tensor) -> torch.Tensor:
+    """IEEE val / 6 on any device. PyTorch's GPU kernel turns a division by a Python / CPU scalar into a
+    multiplication by its (rounded) reciprocal, which differs in the last bit; a divisor tensor on the same device
+    keeps the true division the kernels implement."""
+    if val.device.type == "cpu":
+        return _div6(val)
+    return val / torch.full((), 6, dtype=val.dtype, device=val.device)
+
+
 def jacobi_step_reference(u: torch.Tensor) -> torch.Tensor:
     """One Jacobi3D iteration on a periodic global (z, y, x) grid."""
     Z, Y, X = u.shape
@@ -58,7 +67,7 @@ def jacobi_step_reference(u: torch.Tensor) -> torch.Tensor:
     val = val + my
     val = val + pz
     val = val + mz
-    val = val / 6
+    val = _div6(val)
     hot, cold = _sphere_masks(u.shape, (X, Y, Z), u.device)
     val = torch.where(hot, torch.ones_like(val), val)
     val = torch.where(cold & ~hot, torch.zeros_like(val), val)
@@ -79,7 +88,7 @@ def astaroth_step_reference(u: torch.Tensor) -> torch.Tensor:
     val = val + px
     val = val + py
     val = val + pz
-    return val / 6
+    return _div6(val)
 
 
 def astaroth_init_reference(size_xyz, radius: int, period: float, dtype=torch.float32) -> torch.Tensor:

@@ -23,9 +23,11 @@ def radius_patterns(st):
     return pats
 
 
-def make_dd(st, size, radius, gpus, methods=None, dtype=torch.int64, nq=1, backend=None):
+def make_dd(st, size, radius, gpus, methods=None, dtype=torch.int64, nq=1, backend=None, transport=None):
     dd = st.DistributedDomain(*size, group=st.make_single_group())
     dd.set_backend(backend or st.Backend.Host)
+    if transport is not None:
+        dd.set_transport_options(transport)
     dd.set_radius(radius)
     dd.set_gpus(gpus)
     if methods is not None:
@@ -196,3 +198,21 @@ def test_select_method_priority_and_shared_gpu(st):
     assert sel(M.All, device=False, same_rank=True, same_device=True) == M.Kernel
     assert sel(M.All, device=False) == M.Staged
     assert sel(M.Kernel, device=False) == M.None_
+
+
+@pytest.mark.parametrize("name", ["r1", "r2", "+x2", "-x1", "+x2-x1", "fec", "mixed"])
+@pytest.mark.parametrize("size,gpus", [((64, 12, 10), [0]), ((64, 12, 10), [0, 0]), ((32, 10, 9), [0, 0, 0]),
+                                       ((30, 10, 9), [0])])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_exchange_x_face_sectors(st, name, size, gpus, dtype):
+    """TransportOptions.x_face_sectors: same-process x faces copied as whole 64-B sectors (the extra cells go to the
+    receiver's row padding) give exactly the same halos; x extents that are no multiple of a sector fall back."""
+    radius = radius_patterns(st)[name]
+    tr = st.TransportOptions()
+    tr.x_face_sectors = True
+    dd, (q,) = make_dd(st, size, radius, gpus, dtype=dtype, transport=tr)
+    for it in range(2):
+        fill_coords(dd, q, offset=it)
+        dd.exchange()
+        assert check_exchange(dd, q, radius, offset=it) == 0
+        dd.swap()
