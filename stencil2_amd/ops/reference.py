@@ -48,7 +48,7 @@ def _div6(val: torch.Tensor) -> torch.Tensor:
     multiplication by its (rounded) reciprocal, which differs in the last bit; a divisor tensor on the same device
     keeps the true division the kernels implement."""
     if val.device.type == "cpu":
-        return _div6(val)
+        return val / 6
     return val / torch.full((), 6, dtype=val.dtype, device=val.device)
 
 
