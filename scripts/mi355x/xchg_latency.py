@@ -27,15 +27,25 @@ r = st.Radius.constant(0)
 r.set_face(2)
 if a.radius == "bench":
     r.set_edge(1)
-dd = st.DistributedDomain(a.size, a.size, a.size, group=st.make_single_group())
-dd.set_radius(r)
-dd.set_gpus([0])
-q = dd.add_data("d", torch.float32)
-dd.realize()
-xb = dd.exchange_bytes_for_method(st.MethodFlags.All)
 
 
-def setmode(spin, null):
+def make(sectors):
+    d = st.DistributedDomain(a.size, a.size, a.size, group=st.make_single_group())
+    d.set_radius(r)
+    d.set_gpus([0])
+    tr = st.TransportOptions()
+    tr.x_face_sectors = sectors
+    d.set_transport_options(tr)
+    d.add_data("d", torch.float32)
+    d.realize()
+    return d
+
+
+doms = {"": make(False), "sect/": make(True)}
+xb = doms[""].exchange_bytes_for_method(st.MethodFlags.All)
+
+
+def setmode(dd, spin, null):
     o = dd.transport_options()
     o.spin_wait = spin
     o.null_stream_producers = null
@@ -44,9 +54,11 @@ def setmode(spin, null):
 
 res = {}
 for rnd in range(a.rounds):
+  for pre, dd in doms.items():
     for name, spin, null in (("block", False, False), ("spin", True, False), ("null", False, True),
                              ("spin+null", True, True)):
-        setmode(spin, null)
+        name = pre + name
+        setmode(dd, spin, null)
         for _ in range(5):
             dd.exchange()
             dd.swap()
@@ -68,7 +80,7 @@ for rnd in range(a.rounds):
         dd.swap()
     s.synchronize()
     dd.sync_exchange()
-    res.setdefault("async", []).append((time.perf_counter() - t) / a.iters)
+    res.setdefault(pre + "async", []).append((time.perf_counter() - t) / a.iters)
 
 out = {"size": a.size, "radius": a.radius, "bytes": xb}
 for k, v in res.items():
