@@ -749,11 +749,12 @@ def test_headline_two_rank_exact_grid_bitwise(mode):
     outs = run_ranks(2, WORKER, ["jacobi", "512,512,1024"],
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "30",
                                 "MP_TEMPORAL": "2", "MP_RANDOM": "1", "MP_PREPARE": "1", "MP_SINGLE_STEPS": "1",
-                                "MP_RUN_STEPS": "8", "MP_TOGGLE_OVERLAP": "1", "MP_TOGGLE_MODES": mode,
-                                "MP_EXPECT_OVERLAP": "1"}, timeout=200)
+                                "MP_RUN_STEPS": "8", "MP_TOGGLE_OVERLAP": "1", "MP_TOGGLE_MODES": mode},
+                     timeout=200)
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out and "dim (1, 1, 2)" in out.replace("Dim3", ""), out[-2000:]
+        assert f"overlap {mode != '0'}" in out, out[-2000:]
 
 
 def test_smoke_entry():
