@@ -108,18 +108,22 @@ struct TransportOptions {
   // unused rand_sleep(), packer.cuh:17-20)
   int jitterUs = 0;
   // blocking exchange(): the last op of every comm stream stores the exchange's epoch into a host-mapped word and
-  // the host spins on it (bounded) before the stream synchronize, which then returns at once; false: block in
-  // hipStreamSynchronize right away (its wake-up comes several microseconds after the work completes)
-  bool spinWait = true;
+  // the host spins on it (bounded) before the stream synchronize, which then returns at once; false (default):
+  // block in hipStreamSynchronize right away. Measured on one MI355X (512^3, faces 2, scripts/mi355x/xchg_latency.py,
+  // profiles/r3/xchg_latency_*.json): 45.2 us with the spin vs 37.8 us without -- the extra one-wave signal kernel
+  // costs more than the synchronize's wake-up
+  bool spinWait = false;
   // blocking exchange() without record_ready(): the producers of the fields are taken to be on the null stream or
   // blocking streams (torch's default stream, synchronous copies) and the comm streams wait for an event recorded on
-  // the null stream; false: hipDeviceSynchronize (also covers non-blocking producer streams)
+  // the null stream; false (default): hipDeviceSynchronize, which also covers non-blocking producer streams and
+  // measured faster on an idle GPU (37.8 vs 44.2 us per blocking exchange, same probe)
   bool nullStreamProducers = false;
   // device backend: when every GPU of this process sits on one NUMA node, realize() binds the calling thread to that
   // node's CPUs and allocates the host-staged (pinned) buffers there
   bool numaAffinity = true;
   // same-GPU x faces (translates) copied as whole 64-B sectors (4 lanes per row, the extra cells land in the
-  // receiver's row padding) instead of w-cell pieces of one sector per lane (build_translate_segs_q)
+  // receiver's row padding) instead of w-cell pieces of one sector per lane (build_translate_segs_q). Measured no
+  // gain (same probe: stream-ordered 26.2 vs 24.9 us for faces 2, 26.8 vs 27.8 us with depth-1 edges): off
   bool xFaceSectors = false;
 };
 const char *to_string(TransportOptions::Inbox v);
