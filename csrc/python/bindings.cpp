@@ -495,6 +495,22 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("build_info_string", &build_info_string);
   m.def("rccl_compiled", &rccl::compiled);
+  // host wait policy of this process's HIP device contexts (hipSetDeviceFlags): call before the process first uses
+  // the GPU. "spin" busy-waits in synchronize (lowest wake-up latency), "yield", "blocking", "auto" (HIP default)
+  m.def("set_device_schedule", [](const std::string &mode) {
+    unsigned f = hipDeviceScheduleAuto;
+    if (mode == "spin")
+      f = hipDeviceScheduleSpin;
+    else if (mode == "yield")
+      f = hipDeviceScheduleYield;
+    else if (mode == "blocking")
+      f = hipDeviceScheduleBlockingSync;
+    else if (mode != "auto")
+      throw std::invalid_argument("schedule mode " + mode);
+    const hipError_t e = hipSetDeviceFlags(f);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return std::string(e == hipSuccess ? "" : hipGetErrorString(e));
+  });
 
   py::class_<ExchangePlanEntry>(m, "ExchangePlanEntry")
       .def_readonly("method", &ExchangePlanEntry::method)

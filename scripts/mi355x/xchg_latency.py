@@ -21,7 +21,12 @@ ap.add_argument("--size", type=int, default=512)
 ap.add_argument("--radius", default="faces2")
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--schedule", default="", help="hipSetDeviceFlags host wait policy before the GPU is used: spin/yield/blocking/auto")
+ap.add_argument("--only", default="", help="comma list of modes (block,spin,null,spin+null); sector A/B off")
 a = ap.parse_args()
+if a.schedule:
+    err = st._C.set_device_schedule(a.schedule)
+    print("schedule", a.schedule, err or "ok")
 
 r = st.Radius.constant(0)
 r.set_face(2)
@@ -41,7 +46,7 @@ def make(sectors):
     return d
 
 
-doms = {"": make(False), "sect/": make(True)}
+doms = {"": make(False)} if a.only else {"": make(False), "sect/": make(True)}
 xb = doms[""].exchange_bytes_for_method(st.MethodFlags.All)
 
 
@@ -57,6 +62,8 @@ for rnd in range(a.rounds):
   for pre, dd in doms.items():
     for name, spin, null in (("block", False, False), ("spin", True, False), ("null", False, True),
                              ("spin+null", True, True)):
+        if a.only and name not in a.only.split(","):
+            continue
         name = pre + name
         setmode(dd, spin, null)
         for _ in range(5):
@@ -82,7 +89,7 @@ for rnd in range(a.rounds):
     dd.sync_exchange()
     res.setdefault(pre + "async", []).append((time.perf_counter() - t) / a.iters)
 
-out = {"size": a.size, "radius": a.radius, "bytes": xb}
+out = {"size": a.size, "radius": a.radius, "bytes": xb, "schedule": a.schedule or "default"}
 for k, v in res.items():
     out[k] = {"us": round(min(v) * 1e6, 2), "us_all": [round(x * 1e6, 2) for x in v], "GBps": round(xb / min(v) / 1e9, 1)}
 print(json.dumps(out))
