@@ -848,8 +848,9 @@ static void launch_lds(StencilArgs<T> a, const StencilTune &tune, hipStream_t st
                                            : (const void *)stencil7_lds_kernel<T, TY, NW, KIND, true, true, false>;
     int64_t targetBlocks = resident_blocks(kern, 64 * NW);
     if (tune.reserveCUs > 0) { // leave that many CUs to the comm stream's kernels (overlapped steps)
-      int cus = 256;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
+      int cus = 256, dev = 0; // the device the launch goes to (the caller set it: dom.set_device())
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
       const int64_t perCU = std::max<int64_t>(1, targetBlocks / std::max(1, cus));
       targetBlocks = std::max<int64_t>(perCU, targetBlocks - perCU * std::min(tune.reserveCUs, cus / 2));
     }
