@@ -15,10 +15,12 @@ Steps:
     bench[:<args>]        python bench.py <args> on the one GPU
     mp:<n>:<args>         torch.distributed.run with n ranks sharing the GPU: bench.py --gpus n <args>
     app:<name>:<args>     build/bin/<name> <args>
-    prof:<name>:<cmd>     rocprofv3 --kernel-trace --stats around `python3 <cmd>` (kernel_stats.csv under <out>/<name>)
+    prof:<name>:<cmd>     rocprofv3 --kernel-trace --stats around `python3 <cmd>` (one CSV set per process under
+                          <out>/<name>)
     mpprof:<name>:<n>:<args>  same around an n-rank bench.py run
     pmc:<name>:<ctrs>:<cmd>   rocprofv3 --pmc <ctrs> (comma separated) around `python3 <cmd>`
     py:<script>:<args>    python3 <script> <args>
+A step may start with environment assignments: "GPU_MAX_HW_QUEUES=2,STENCIL_LOG_LEVEL=3@mp:8:--per-gpu 128".
 """
 from __future__ import annotations
 
@@ -75,10 +77,10 @@ def step_cmd(step: str, out: str, k: int):
         os.makedirs(d, exist_ok=True)
         if kind == "pmc":
             ctrs, _, cmd = rest2.partition(":")
-            pre = ["rocprofv3", "--pmc", *ctrs.split(","), "--kernel-trace", "-d", d, "-o", "run",
+            pre = ["rocprofv3", "--pmc", *ctrs.split(","), "--kernel-trace", "-d", d, "-o", "run_%pid%",
                    "--output-format", "csv", "--"]
             return f"pmc_{name}", pre + [PY, *shlex.split(cmd)], 300
-        pre = ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv", "--"]
+        pre = ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "run_%pid%", "--output-format", "csv", "--"]
         if kind == "prof":
             return f"prof_{name}", pre + [PY, *shlex.split(rest2)], 420
         n, _, args = rest2.partition(":")
@@ -94,16 +96,20 @@ def main():
     os.makedirs(a.out, exist_ok=True)
     os.chdir(REPO)
     for k, step in enumerate(a.steps):
+        extra = {}
+        if "@" in step.split(":")[0]:
+            assigns, step = step.split("@", 1)
+            extra = dict(kv.split("=", 1) for kv in assigns.split(","))
         name, cmd, limit = step_cmd(step, a.out, k)
         log = os.path.join(a.out, f"{k:02d}_{name}.log")
-        print(f"[{time.strftime('%H:%M:%S')}] step {k}: {step}  (limit {limit} s) -> {log}", flush=True)
+        print(f"[{time.strftime('%H:%M:%S')}] step {k}: {step} {extra or ''} (limit {limit} s) -> {log}", flush=True)
         t0 = time.time()
         with open(log, "w") as f:
             f.write(" ".join(shlex.quote(c) for c in cmd) + "\n")
             f.flush()
             try:
                 rc = subprocess.run(["timeout", "-k", "10", str(limit), *cmd], stdout=f, stderr=subprocess.STDOUT,
-                                    env=env(), cwd=REPO).returncode
+                                    env={**env(), **extra}, cwd=REPO).returncode
             except Exception as e:  # noqa: BLE001
                 rc = 99
                 f.write(f"\nrunner error: {e}\n")
