@@ -42,7 +42,33 @@ def weak_grid(st, per_gpu: int, n: int, rule: str, axis_cost) -> tuple:
     return grid
 
 
+def _gpus_sysfs() -> int:
+    """GPUs of this node from the KFD topology (no HIP call: the HIP runtime must not start before the queue limit
+    below is set)."""
+    import glob
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            n += int(open(f).read().strip() or 0) != 0
+        except (OSError, ValueError):
+            pass
+    return n
+
+
+def _limit_queues_when_sharing():
+    """Ranks sharing one GPU (a rehearsal of the multi-GPU run on a smaller box): keep ranks x hardware queues per
+    process <= 8. Beyond that the GPU time-slices the processes' queues and every cross-process hand-off waits a
+    scheduling quantum: one MI355X, 8 ranks x 128^3, 39.3 / 6.0 / 2.0 ms per step with 4 / 2 / 1 queues per
+    process, 4 ranks 12.4 vs 0.30 ms with 4 vs 2 (profiles/r3/cliff/). One process per GPU is left alone."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    ngpu = _gpus_sysfs()
+    if ngpu and local > ngpu and "GPU_MAX_HW_QUEUES" not in os.environ:
+        per_gpu = -(-local // ngpu)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, 8 // per_gpu))
+
+
 def main():
+    _limit_queues_when_sharing()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)

@@ -937,21 +937,9 @@ void DistributedDomain::realize() {
       if (!ctx.pipesOut.empty()) ctx.pipeSent = Event(ctx.dev);
       if (!ctx.pipesIn.empty()) ctx.pipeUnpacked = Event(ctx.dev);
     }
-    // copy streams for DMA-engine copies (Colocated sends and outgoing pipes of a device: at most 4 streams)
-    {
-      std::map<int, int> coloOut;
-      for (auto &c : I.chans)
-        if (c.method == MethodFlags::Colocated && c.send) ++coloOut[c.localDev];
-      for (auto &ctx : I.devs) {
-        const int n = std::min(4, std::max(coloOut[ctx.dev], int(ctx.pipesOut.size())));
-        if (n < 2) continue;
-        ctx.copyFork = Event(ctx.dev);
-        for (int k = 0; k < n; ++k) {
-          ctx.copyStreams.emplace_back(ctx.dev, Priority::HIGH);
-          ctx.copyJoin.emplace_back(ctx.dev);
-        }
-      }
-    }
+    // copy streams for DMA-engine copies are created on first use (forked_copies): every stream can take a hardware
+    // queue, and ranks that share a GPU slow down by orders of magnitude once their queues oversubscribe the
+    // device (profiles/r3/cliff/)
 
     // channel buffers
     for (int ci = 0; ci < int(I.chans.size()); ++ci) {
@@ -1587,6 +1575,13 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   // run copies[k] (k = 0..n-1) behind the work on `st`, on the device's copy streams when it has them (concurrent
   // DMA engines / links), and make `st` wait for all of them
   auto forked_copies = [&](DevCtx &ctx, hipStream_t st, int n, const std::function<void(int, hipStream_t)> &copy) {
+    if (!over && n > 1 && ctx.copyStreams.empty()) { // first engine copies of this device: its copy streams
+      ctx.copyFork = Event(ctx.dev);
+      for (int k = 0; k < std::min(4, n); ++k) {
+        ctx.copyStreams.emplace_back(ctx.dev, Priority::HIGH);
+        ctx.copyJoin.emplace_back(ctx.dev);
+      }
+    }
     const bool fork = !over && ctx.copyStreams.size() > 1 && n > 1;
     if (!fork) {
       for (int k = 0; k < n; ++k) copy(k, st);
