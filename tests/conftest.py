@@ -53,6 +53,10 @@ def run_ranks(n, script, args=(), env_extra=None, per_rank_env=None, timeout=240
         env.pop("WORLD_SIZE", None)
         if env_extra:
             env.update(env_extra)
+        if env.get("MP_DEVICE") == "1" and "GPU_MAX_HW_QUEUES" not in env:
+            # ranks sharing the one GPU: at most 8 hardware queues in all, or the GPU time-slices the processes'
+            # queues (bench.py _limit_queues_when_sharing, profiles/r3/cliff/)
+            env["GPU_MAX_HW_QUEUES"] = str(max(1, 8 // n))
         if per_rank_env:
             env.update(per_rank_env(r))
         procs.append(subprocess.Popen([sys.executable, script, *map(str, args)], env=env, stdout=subprocess.PIPE,
