@@ -116,6 +116,8 @@ def main():
                     help="memory of the co-located receive slots (TransportOptions.inbox)")
     ap.add_argument("--completion", choices=["kernel", "streamop"], default="kernel",
                     help="co-located arrival/credit signalling: bounded spin kernels or hipStreamWait/WriteValue64")
+    ap.add_argument("--fuse-flags", type=int, default=1,
+                    help="co-located flag waits/signals folded into the pack/unpack kernels (0: separate kernels)")
     ap.add_argument("--self-test", type=int, default=1,
                     help="multi-process: verify the transports on a probe domain first and fall back along "
                          "Colocated -> Rccl -> Staged until every halo arrives correctly")
@@ -171,6 +173,7 @@ def main():
     topt.inbox = {"uncached": topt.Inbox.Uncached, "fine": topt.Inbox.Fine, "coarse": topt.Inbox.Coarse}[args.inbox]
     topt.colo_copy = topt.Copy.Engine if args.colo_copy == "engine" else topt.Copy.Store
     topt.completion = topt.Completion.StreamOp if args.completion == "streamop" else topt.Completion.Kernel
+    topt.fuse_flags = bool(args.fuse_flags)
     if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # rehearses the fallback (scripts): IPC probe reports failure
         topt.fail_ipc_probe = True
 
@@ -301,7 +304,7 @@ def main():
                        "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
                        "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none",
                        "transport": {"inbox": args.inbox, "colo_copy": str(model.domain.transport_options().colo_copy).split(".")[-1].lower(),
-                                     "completion": args.completion},
+                                     "completion": args.completion, "fuse_flags": bool(args.fuse_flags)},
                        "build": st.build_info()["git_sha"]},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),

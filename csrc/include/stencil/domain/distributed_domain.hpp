@@ -92,6 +92,9 @@ struct TransportOptions {
   //             wait itself is unbounded: sync_exchange's host watchdog reports a stall)
   enum class Completion : int { Kernel = 0, StreamOp = 1 };
   Completion completion = Completion::Kernel;
+  // Kernel completion: fold the flag waits / signals into the pack and unpack kernels (one launch per side instead
+  // of three; copy_plan_device_sync). Engine copies keep a separate credit wait and arrival signal around the copies.
+  bool fuseFlags = true;
   // seconds before a device-side spin, a host wait on a peer, or the RCCL watchdog gives up (<= 0: the
   // STENCIL_WAIT_TIMEOUT environment variable, else 60)
   double waitTimeout = 0;

@@ -95,5 +95,19 @@ void wait_flags_device(const std::vector<uint64_t *> &flags, uint64_t target, in
 // System-scope release, then lane i stores *flags[i] = value (flags may be IPC-mapped peer memory).
 void signal_flags_device(const std::vector<uint64_t *> &flags, uint64_t value, hipStream_t stream);
 constexpr int kMaxFlagsPerLaunch = 64;
+// One fused launch: wait until every `wait` flag >= waitTarget (bounded: on timeout `code` goes to *err), run the
+// copy plan on at most maxBlocks 1024-thread blocks (0: up to one per CU), then release-store signalValue into every
+// `signal` flag once all blocks are done (`counter`: a zeroed device word, reset by the kernel; one per stream).
+struct FlagSyncArgs {
+  std::vector<uint64_t *> wait;
+  uint64_t waitTarget = 0;
+  std::vector<uint64_t *> signal;
+  uint64_t signalValue = 0;
+  uint32_t *counter = nullptr;
+  int *err = nullptr;
+  int code = 0;
+  double timeout_s = 60;
+};
+void copy_plan_device_sync(const CopyPlan &p, hipStream_t stream, int maxBlocks, const FlagSyncArgs &a);
 
 } // namespace stencil

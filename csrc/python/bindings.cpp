@@ -467,6 +467,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("colo_copy", &TransportOptions::coloCopy)
       .def_readwrite("peer_copy", &TransportOptions::peerCopy)
       .def_readwrite("completion", &TransportOptions::completion)
+      .def_readwrite("fuse_flags", &TransportOptions::fuseFlags)
       .def_readwrite("wait_timeout", &TransportOptions::waitTimeout)
       .def_readwrite("fake_remote_axes", &TransportOptions::fakeRemoteAxes)
       .def_readwrite("ipc_probe", &TransportOptions::ipcProbe)

@@ -101,6 +101,9 @@ struct SegList {
     }
   }
   void run_device(int v, hipStream_t s, int maxBlocks = 0) const { copy_plan_device(plan[v], s, maxBlocks); }
+  void run_device_sync(int v, hipStream_t s, int maxBlocks, const FlagSyncArgs &a) const {
+    copy_plan_device_sync(plan[v], s, maxBlocks, a);
+  }
   void run_host(int v) const { copy_segs_host(host[v]); }
   void release() {
     for (auto &p : plan) free_copy_plan(p);
@@ -166,6 +169,7 @@ struct DevCtx {
   Event copyFork;
   std::vector<Stream> copyStreams;
   std::vector<Event> copyJoin;
+  uint32_t *syncCounter = nullptr; // [0] colo send, [1] colo receive: block counters of the fused transport kernels
   SegList rcclPack, rcclUnpack;   // variant = parity
   SegList stagedPack, stagedUnpack;
   rccl::Comm nccl = nullptr;
@@ -266,6 +270,7 @@ DistributedDomain::~DistributedDomain() {
       d.pipePack[k].release();
       d.pipeUnpack[k].release();
     }
+    if (d.syncCounter) (void)hipFree(d.syncCounter);
     d.coloUnpack.release();
     d.rcclPack.release();
     d.rcclUnpack.release();
@@ -936,6 +941,9 @@ void DistributedDomain::realize() {
       ctx.pipeUnpack[0].upload(ctx.dev);
       if (!ctx.pipesOut.empty()) ctx.pipeSent = Event(ctx.dev);
       if (!ctx.pipesIn.empty()) ctx.pipeUnpacked = Event(ctx.dev);
+      HIP_CHECK(hipSetDevice(ctx.dev));
+      HIP_CHECK(hipMalloc(&ctx.syncCounter, 2 * sizeof(uint32_t)));
+      HIP_CHECK(hipMemset(ctx.syncCounter, 0, 2 * sizeof(uint32_t)));
     }
     // copy streams for DMA-engine copies are created on first use (forked_copies): every stream can take a hardware
     // queue, and ranks that share a GPU slow down by orders of magnitude once their queues oversubscribe the
@@ -1354,6 +1362,7 @@ void DistributedDomain::set_transport_options_live(const TransportOptions &o) {
   set_colo_copy(o.coloCopy);
   set_completion(o.completion);
   topt_.spinWait = o.spinWait;
+  topt_.fuseFlags = o.fuseFlags; // flag words are monotonic epochs: either form continues where the other left off
   topt_.nullStreamProducers = o.nullStreamProducers;
   topt_.jitterUs = o.jitterUs;
   if (o.waitTimeout > 0) topt_.waitTimeout = o.waitTimeout;
@@ -1547,6 +1556,8 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   // Colocated completion (TransportOptions::completion): bounded spin / release kernels, or command-processor
   // stream operations on the same flag words
   const bool streamOps = topt_.completion == TransportOptions::Completion::StreamOp;
+  // Colocated flag waits / signals folded into the pack and unpack kernels (TransportOptions::fuseFlags)
+  const bool fused = !streamOps && topt_.fuseFlags;
   auto wait_flags = [&](const std::vector<uint64_t *> &flags, uint64_t target, int code, hipStream_t st) {
     if (!streamOps) {
       wait_flags_device(flags, target, I.errDev, code, topt_.waitTimeout, st);
@@ -1661,12 +1672,25 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     HIP_CHECK(hipSetDevice(ctx.dev));
     TraceRange t("colo send");
     const bool engine = topt_.coloCopy == TransportOptions::Copy::Engine;
-    if (engine) ctx.coloPackLocal.run_device(parity, S(ctx), commBlocks_);
-    if (I.epoch > 2) {
-      std::vector<uint64_t *> credits;
+    std::vector<uint64_t *> credits, arrived;
+    if (I.epoch > 2)
       for (int ci : ctx.coloSend) credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownFlag));
-      wait_flags(credits, I.epoch - 2, 1, S(ctx));
+    for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteFlag));
+    if (!engine && fused) { // one launch: credit wait, pack into the peer slots, arrival flags
+      FlagSyncArgs fa;
+      fa.wait = credits;
+      fa.waitTarget = I.epoch - 2;
+      fa.signal = arrived;
+      fa.signalValue = I.epoch;
+      fa.counter = ctx.syncCounter;
+      fa.err = I.errDev;
+      fa.code = 1;
+      fa.timeout_s = topt_.waitTimeout;
+      ctx.coloPack.run_device_sync(cv, S(ctx), commBlocks_, fa);
+      continue;
     }
+    if (engine) ctx.coloPackLocal.run_device(parity, S(ctx), commBlocks_);
+    if (!credits.empty()) wait_flags(credits, I.epoch - 2, 1, S(ctx));
     if (engine) {
       forked_copies(ctx, S(ctx), int(ctx.coloSend.size()), [&](int k, hipStream_t cs) {
         const Channel &c = I.chans[size_t(ctx.coloSend[size_t(k)])];
@@ -1675,8 +1699,6 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     } else {
       ctx.coloPack.run_device(cv, S(ctx), commBlocks_);
     }
-    std::vector<uint64_t *> arrived;
-    for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteFlag));
     signal_flags(arrived, I.epoch, S(ctx));
   }
 
@@ -1747,6 +1769,19 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     for (int ci : ctx.coloRecv) {
       arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownFlag));
       credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteFlag));
+    }
+    if (fused) { // one launch: arrival wait, unpack from our slots, credit flags
+      FlagSyncArgs fa;
+      fa.wait = arrived;
+      fa.waitTarget = I.epoch;
+      fa.signal = credits;
+      fa.signalValue = I.epoch;
+      fa.counter = ctx.syncCounter + 1;
+      fa.err = I.errDev;
+      fa.code = 2;
+      fa.timeout_s = topt_.waitTimeout;
+      ctx.coloUnpack.run_device_sync(cv, S(ctx), commBlocks_, fa);
+      continue;
     }
     wait_flags(arrived, I.epoch, 2, S(ctx));
     ctx.coloUnpack.run_device(cv, S(ctx), commBlocks_);

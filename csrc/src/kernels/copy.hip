@@ -299,12 +299,14 @@ struct FlagList {
   int n;
 };
 
-__global__ void wait_flags_kernel(FlagList f, uint64_t target, int *err, int code, uint64_t timeoutTicks) {
-  const int i = threadIdx.x;
-  if (i < f.n) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime(); // 100 MHz constant clock
+// lanes i < f.n of the calling wave poll *f.p[i] until >= target (relaxed, system scope, s_sleep back-off); bounded:
+// past timeoutTicks of the 100-MHz constant clock the lane stores `code` into *err and gives up
+__device__ __forceinline__ void poll_flags(const FlagList &f, uint64_t target, int *err, int code,
+                                           uint64_t timeoutTicks, int lane) {
+  if (lane < f.n) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (true) {
-      const uint64_t v = __hip_atomic_load(f.p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t v = __hip_atomic_load(f.p[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (v >= target) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > timeoutTicks) {
         __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -313,6 +315,54 @@ __global__ void wait_flags_kernel(FlagList f, uint64_t target, int *err, int cod
       __builtin_amdgcn_s_sleep(4);
     }
   }
+}
+
+struct FlagSync {
+  FlagList wait;        // polled before any copy (n = 0: none)
+  uint64_t waitTarget;
+  FlagList signal;      // stored after every block's copies are done
+  uint64_t signalValue;
+  uint32_t *counter;    // blocks done; 0 at launch, reset by the last block
+  int *err;
+  int code;
+  uint64_t timeoutTicks;
+};
+
+// Fused transport step (Colocated sends / receives): wait for the peer's flags, run the copy plan, raise the
+// peer's flags -- one launch instead of three (each one-wave flag kernel costs ~4.5 us of serial stream time on
+// MI355X, profiles/r3/cliff/gaps_mp2x_exchange_loop.txt). Every block waits for itself (the flags are few and
+// uncached). The signal follows the classic last-block pattern: each block's thread 0 publishes the block's copies
+// with a system-scope release fence and counts itself done; the block that completes the count acquires every
+// other block's publication and release-stores the flags.
+__global__ __launch_bounds__(1024) void copy_plan_kernel_sync(const CopySeg *__restrict__ segs,
+                                                              const CopyWork *__restrict__ work, uint32_t nwork,
+                                                              FlagSync fs) {
+  if (fs.wait.n > 0) {
+    if (threadIdx.x < 64) poll_flags(fs.wait, fs.waitTarget, fs.err, fs.code, fs.timeoutTicks, int(threadIdx.x));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the peer's slot writes / reads before our copies
+    __syncthreads();
+  }
+  const uint32_t g = threadIdx.x >> 8; // wave-uniform (a group is 4 whole waves)
+  for (uint32_t wi = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + g); wi < nwork; wi += gridDim.x * 4) {
+    const CopyWork w = work[wi];
+    copy_work(segs[w.seg], w, threadIdx.x & 255);
+  }
+  if (fs.signal.n == 0) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const uint32_t done = __hip_atomic_fetch_add(fs.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      for (int i = 0; i < fs.signal.n; ++i)
+        __hip_atomic_store(fs.signal.p[i], fs.signalValue, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(fs.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void wait_flags_kernel(FlagList f, uint64_t target, int *err, int code, uint64_t timeoutTicks) {
+  poll_flags(f, target, err, code, timeoutTicks, int(threadIdx.x));
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
 }
@@ -336,6 +386,26 @@ void wait_flags_device(const std::vector<uint64_t *> &flags, uint64_t target, in
   if (flags.empty()) return;
   const uint64_t ticks = uint64_t(timeout_s * 1e8);
   hipLaunchKernelGGL(wait_flags_kernel, dim3(1), dim3(64), 0, stream, to_list(flags), target, err, code, ticks);
+  HIP_CHECK(hipGetLastError());
+}
+
+void copy_plan_device_sync(const CopyPlan &p, hipStream_t stream, int maxBlocks, const FlagSyncArgs &a) {
+  FlagSync fs{};
+  fs.wait = to_list(a.wait);
+  fs.waitTarget = a.waitTarget;
+  fs.signal = to_list(a.signal);
+  fs.signalValue = a.signalValue;
+  fs.counter = a.counter;
+  fs.err = a.err;
+  fs.code = a.code;
+  fs.timeoutTicks = uint64_t(a.timeout_s * 1e8);
+  STENCIL_REQUIRE(fs.signal.n == 0 || a.counter, "copy_plan_device_sync: signal flags need a block counter");
+  // one CU per block (1024 threads): at most maxBlocks, or the whole GPU when unconfined; at least one block, so
+  // the flags are waited for and raised even when this device has nothing to copy
+  const int cap = maxBlocks > 0 ? maxBlocks : 256;
+  const int blocks = std::max(1, std::min(cap, (p.nwork + 3) / 4));
+  hipLaunchKernelGGL(copy_plan_kernel_sync, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dwork, uint32_t(p.nwork),
+                     fs);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -19,6 +19,7 @@ def transport_from_env():
     t.peer_copy = getattr(st.TransportOptions.Copy, e.get("MP_PEER_COPY", "Store"))
     t.completion = getattr(st.TransportOptions.Completion, e.get("MP_COMPLETION", "Kernel"))
     t.jitter_us = int(e.get("MP_JITTER_US", "0"))
+    t.fuse_flags = e.get("MP_FUSE_FLAGS", "1") == "1"
     t.fail_ipc_probe = e.get("MP_IPC_PROBE_FAIL") == "1"
     t.fail_rccl_init = e.get("MP_RCCL_INIT_FAIL") == "1"
     return t

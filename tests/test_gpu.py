@@ -574,15 +574,21 @@ def test_colocated_ipc_two_ranks_one_gpu(radius):
         assert rc == 0, out[-3000:]
 
 
-@pytest.mark.parametrize("inbox,copy,completion", [("Uncached", "Engine", "Kernel"), ("Coarse", "Store", "Kernel"),
-                                                   ("Coarse", "Engine", "Kernel"), ("Fine", "Store", "Kernel"),
-                                                   ("Uncached", "Store", "StreamOp"), ("Coarse", "Engine", "StreamOp")])
-def test_colocated_transport_variants_two_ranks(inbox, copy, completion):
+@pytest.mark.parametrize("inbox,copy,completion,fuse", [("Uncached", "Engine", "Kernel", "1"),
+                                                        ("Coarse", "Store", "Kernel", "1"),
+                                                        ("Coarse", "Engine", "Kernel", "1"),
+                                                        ("Fine", "Store", "Kernel", "1"),
+                                                        ("Uncached", "Store", "Kernel", "0"),
+                                                        ("Uncached", "Engine", "Kernel", "0"),
+                                                        ("Uncached", "Store", "StreamOp", "1"),
+                                                        ("Coarse", "Engine", "StreamOp", "1")])
+def test_colocated_transport_variants_two_ranks(inbox, copy, completion, fuse):
     """Every TransportOptions variant of the HIP IPC transport (receive-slot memory, kernel stores vs DMA-engine
-    copies, spin kernels vs stream wait/write operations): coordinate oracle over faces, edges and corners, then
-    fused Jacobi pairs vs the torch oracle, two ranks sharing one GPU."""
+    copies, flag waits/signals fused into the pack/unpack kernels or separate spin kernels, or stream wait/write
+    operations): coordinate oracle over faces, edges and corners, then fused Jacobi pairs vs the torch oracle, two
+    ranks sharing one GPU."""
     env = {"MP_DEVICE": "1", "MP_METHODS": "Colocated|Kernel", "STENCIL_WAIT_TIMEOUT": "20", "MP_INBOX": inbox,
-           "MP_COLO_COPY": copy, "MP_COMPLETION": completion}
+           "MP_COLO_COPY": copy, "MP_COMPLETION": completion, "MP_FUSE_FLAGS": fuse}
     for rc, out in run_ranks(2, WORKER, ["exchange", "fec", "20,12,10"], env_extra=env):
         assert rc == 0, out[-3000:]
     env.update({"MP_METHODS": "All", "MP_TEMPORAL": "2", "MP_EXPECT_OVERLAP": "1"})
@@ -690,15 +696,16 @@ def test_ipc_probe_failure_falls_back_on_shared_gpu():
         assert "bytes_Rccl=0 " in out and "bytes_Colocated=0 " in out and "bytes_Staged=0 " not in out, out[-2000:]
 
 
-@pytest.mark.parametrize("methods,copy", [("Colocated|Kernel", "Store"), ("Colocated|Kernel", "Engine"),
-                                          ("Staged|Kernel", "Store")])
-def test_race_canary_two_ranks_one_gpu(methods, copy):
+@pytest.mark.parametrize("methods,copy,fuse", [("Colocated|Kernel", "Store", "1"), ("Colocated|Kernel", "Store", "0"),
+                                               ("Colocated|Kernel", "Engine", "1"), ("Staged|Kernel", "Store", "1")])
+def test_race_canary_two_ranks_one_gpu(methods, copy, fuse):
     """Race canary over HIP IPC (double-buffered inboxes + credits; pack-kernel stores or DMA-engine copies) and the
     staged path, with jitter. Every host wait on a peer is bounded by STENCIL_WAIT_TIMEOUT and a stalled rank dumps
     its stacks (MP_STALL_DUMP_S), so a stall fails with every rank's phase instead of hanging."""
     outs = run_ranks(2, WORKER, ["canary", "fec", "20,12,10"],  # ~2.5 s normally; 90 s: rank outputs on a hang
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20",
-                                "MP_JITTER_US": "200", "MP_COLO_COPY": copy, "MP_STALL_DUMP_S": "30"}, timeout=90)
+                                "MP_JITTER_US": "200", "MP_COLO_COPY": copy, "MP_STALL_DUMP_S": "30",
+                                "MP_FUSE_FLAGS": fuse}, timeout=90)
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 
