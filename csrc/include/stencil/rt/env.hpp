@@ -10,7 +10,7 @@
 //   STENCIL_TRACE         1: roctx ranges around realize / exchange / transport phases (rocprofv3 --marker-trace)
 //   STENCIL_PLAN_FILE     0: do not write plan_<rank>.txt during realize (reference src/stencil.cu:259-353)
 //   STENCIL_HOSTNAME      host name this rank reports (fakes multi-node layouts in tests)
-//   STENCIL_NO_AMDSMI     1: GPU topology from HIP link queries only (skip amd-smi)
+//   STENCIL_AMDSMI        1: also query amd-smi (link weights/bandwidths; off by default: exit-time abort on ROCm 7.2)
 //   rendezvous            STENCIL_RANK / STENCIL_WORLD_SIZE / STENCIL_MASTER_ADDR / STENCIL_MASTER_PORT, or torchrun's
 //                         RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (+1: torch's store holds MASTER_PORT)
 #include <cstdlib>

@@ -22,7 +22,13 @@ namespace stencil {
 namespace gpu_topo {
 
 // ---- amd-smi, resolved with dlopen so the runtime still loads where the library is absent ----
+// Opt-in (STENCIL_AMDSMI=1): on the MI355X pool's ROCm 7.2 image a process that has initialised amd-smi next to the
+// HIP runtime aborts with glibc "double free or corruption" when it exits (build/bin/jacobi3d 128^3: rc 134 with
+// amd-smi, rc 0 without; gpurun_out/d1, r3). Every query the runtime needs has an amd-smi-free source: link type
+// and hops from hipExtGetLinkTypeAndHopCount, the NUMA node from sysfs. amd-smi adds the link weights and
+// bandwidths of links(); when it is enabled, amdsmi_shut_down runs at exit.
 namespace {
+amdsmi_status_t (*g_smi_shutdown)() = nullptr;
 struct Smi {
   bool ok = false;
   std::vector<amdsmi_processor_handle> byDev; // HIP ordinal -> processor handle (null if unmatched)
@@ -43,7 +49,7 @@ template <typename F> static bool sym(void *lib, const char *name, F *out) {
 const Smi &smi() {
   static Smi s = [] {
     Smi r;
-    if (env::get_int("STENCIL_NO_AMDSMI", 0) != 0) return r;
+    if (env::get_int("STENCIL_AMDSMI", 0) == 0) return r;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
       (void)hipGetLastError();
@@ -63,6 +69,8 @@ const Smi &smi() {
         !sym(lib, "amdsmi_topo_get_numa_node_number", &r.numa))
       return r;
     if (init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return r;
+    if (sym(lib, "amdsmi_shut_down", &g_smi_shutdown))
+      std::atexit([] { (void)g_smi_shutdown(); });
     uint32_t ns = 0;
     if (sockets(&ns, nullptr) != AMDSMI_STATUS_SUCCESS || ns == 0) return r;
     std::vector<amdsmi_socket_handle> sh(ns);
@@ -107,11 +115,7 @@ const Smi &smi() {
 bool smi_available() { return smi().ok; }
 
 int numa_node(int dev) {
-  const Smi &s = smi();
-  amdsmi_processor_handle h = s.handle(dev);
-  uint32_t n = 0;
-  if (h && s.numa(h, &n) == AMDSMI_STATUS_SUCCESS) return int(n);
-  // sysfs: the PCI function's NUMA node
+  // sysfs: the PCI function's NUMA node (amd-smi only when enabled and sysfs has no answer)
   char bus[64] = {0};
   if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) {
     (void)hipGetLastError();
@@ -121,7 +125,11 @@ int numa_node(int dev) {
   for (auto &c : b) c = char(std::tolower(c));
   std::ifstream f("/sys/bus/pci/devices/" + b + "/numa_node");
   int node = -1;
-  if (f >> node) return node;
+  if (f >> node && node >= 0) return node;
+  const Smi &s = smi();
+  amdsmi_processor_handle h = s.handle(dev);
+  uint32_t n = 0;
+  if (h && s.numa(h, &n) == AMDSMI_STATUS_SUCCESS) return int(n);
   return -1;
 }
 
