@@ -282,6 +282,11 @@ def main():
     # the same exchanges stream-ordered back to back (exchange_async on one stream, a single synchronize at the end):
     # the transports' own rate without the host round trip of every blocking exchange()
     xs = torch.cuda.Stream()
+    for _ in range(3):  # untimed: the first launches on a new stream create its hardware queue (~ms)
+        dd.exchange_async(xs.cuda_stream, 0)
+        dd.swap()
+    xs.synchronize()
+    dd.sync_exchange()
     barrier()
     t2 = time.perf_counter()
     for _ in range(args.exchange_iters):
