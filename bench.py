@@ -4,8 +4,10 @@
 Metric (BASELINE.json): "halo-exchange GB/s + Jacobi3D Gcells/s, 512^3/GPU weak scaling at 1/2/4/8 MI355X".
 `value` is the whole-job Jacobi3D throughput in Gcells/s (global cells x steps / time). One step is the
 reference's full iteration (bin/jacobi3d.cu:265-346): interior stencil overlapped with the halo exchange of all
-faces (periodic), exterior stencil, swap. The global grid follows the reference weak-scaling rule
-(512 * N^0.33333 per axis: 512/645/813/1024 for N=1/2/4/8), decomposed by the NodeAware placement.
+faces (periodic), exterior stencil, swap. Every GPU holds exactly 512^3 cells (--grid exact); the decomposition is
+the NodeAware partitioner's MaxLink choice for the xGMI mesh (1x1xN slabs: two faces per GPU, each on its own
+link); --grid cbrt runs the reference's cube rule (512 * N^0.33333 per axis: 645/813/1024 for N=2/4/8) and
+--partition interface the reference's cut rule.
 Secondary numbers in the JSON line: the halo-exchange GB/s of an exchange-only loop on the same decomposition
 (bin/bench_exchange.cu definition: aggregate halo bytes / time).
 
@@ -20,12 +22,14 @@ import sys
 import time
 
 
-def weak_grid(st, per_gpu: int, n: int, rule: str, axis_cost) -> tuple:
+def weak_grid(st, per_gpu: int, n: int, rule: str, axis_cost, objective) -> tuple:
     """Global grid of the weak-scaling run on n GPUs.
 
     cbrt: the reference's cube of side per_gpu * n^(1/3) (bin/jacobi3d.cu:167-169).
-    exact: the same NodeAware decomposition of that cube (e.g. 1x1x2 / 1x2x2 / 1x2x4 for n = 2 / 4 / 8 with the
-    default cut costs), but every sub-domain exactly per_gpu^3, so per-GPU work is the N=1 work to the cell.
+    exact: every sub-domain exactly per_gpu^3, so per-GPU work is the N=1 work to the cell; the decomposition d is
+    the partitioner's choice for n cubes (MaxLink on the node's xGMI mesh: 1x1xN slabs, two faces per GPU on two
+    links; Interface: the reference's greedy cut of the cbrt-scaled cube, 1x1x2 / 1x2x2 / 1x2x4), the grid is
+    per_gpu x d.
     """
     L = st.models.weak_scaled_size(per_gpu, n)
     if rule == "cbrt" or n == 1:
@@ -33,9 +37,24 @@ def weak_grid(st, per_gpu: int, n: int, rule: str, axis_cost) -> tuple:
     r = st.Radius.constant(0)
     r.set_face(1)
     cost = st.Dim3(*axis_cost)
-    d = st.NodePartition(st.Dim3(L, L, L), r, 1, n, cost).dim()
+    if objective == st.PartitionObjective.MaxLink:
+        # every factorization d of n, scored on the grid of n per_gpu^3 cubes it forms (busiest link, total)
+        best = None
+        for dx in range(1, n + 1):
+            for dy in range(1, n // dx + 1):
+                if n % (dx * dy):
+                    continue
+                dz = n // (dx * dy)
+                g = st.Dim3(per_gpu * dx, per_gpu * dy, per_gpu * dz)
+                c = st.NodePartition.link_cost(g, st.Dim3(dx, dy, dz), r, cost)
+                key = (c, dx, dy)
+                if best is None or key < best[0]:
+                    best = (key, st.Dim3(dx, dy, dz))
+        d = best[1]
+    else:
+        d = st.NodePartition(st.Dim3(L, L, L), r, 1, n, cost).dim()
     grid = (per_gpu * d.x, per_gpu * d.y, per_gpu * d.z)
-    p = st.NodePartition(st.Dim3(*grid), r, 1, n, cost)
+    p = st.NodePartition(st.Dim3(*grid), r, 1, n, cost, objective)
     if p.dim() != d or any(p.subdomain_size(st.Dim3(i, j, k)) != st.Dim3(per_gpu, per_gpu, per_gpu)
                            for i in range(d.x) for j in range(d.y) for k in range(d.z)):
         return (L, L, L)  # the partitioner would not cut the scaled grid into equal cubes: the reference rule
@@ -102,6 +121,10 @@ def main():
                          "of those halos); 0 = copy every halo")
     ap.add_argument("--axis-cost", default="4,3,2",
                     help="NodeAware partition cost per interface cell of x,y,z cuts (1,1,1 = the reference's rule)")
+    ap.add_argument("--partition", choices=["maxlink", "interface"], default="maxlink",
+                    help="NodeAware cut rule inside the node: maxlink = fewest halo cells on the busiest xGMI link "
+                         "(then fewest in total): 1x1xN slabs of 512^3; interface = the reference's greedy minimum "
+                         "interface (1x2x2 / 1x2x4)")
     ap.add_argument("--grid", choices=["exact", "cbrt"], default="exact",
                     help="weak-scaling grid: exact = every GPU holds exactly per_gpu^3 cells (global grid = per_gpu x the "
                          "decomposition of the cbrt-scaled cube); cbrt = the reference's rule, a per_gpu*N^(1/3) cube "
@@ -150,7 +173,8 @@ def main():
     n = world
     L = st.models.weak_scaled_size(args.per_gpu, n)
     axis_cost = tuple(int(v) for v in args.axis_cost.split(","))
-    grid = weak_grid(st, args.per_gpu, n, args.grid, axis_cost)
+    objective = st.PartitionObjective.MaxLink if args.partition == "maxlink" else st.PartitionObjective.Interface
+    grid = weak_grid(st, args.per_gpu, n, args.grid, axis_cost, objective)
     methods = st.MethodFlags.All
     if args.methods != "all":
         methods = st.MethodFlags.None_
@@ -193,7 +217,7 @@ def main():
     overlap = not args.no_overlap and args.overlap != "off"
     model = st.Jacobi3D(grid, gpus=[device], methods=methods, overlap=overlap,
                         auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
-                        axis_cost=axis_cost, wrap_self=bool(args.wrap), transport=topt,
+                        axis_cost=axis_cost, partition=objective, wrap_self=bool(args.wrap), transport=topt,
                         self_test=bool(args.self_test) and world > 1)
     model.init()
     methods = model.domain.methods()
@@ -315,7 +339,7 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (reference Jacobi3D initial condition: 0.5 + hot/cold spheres)",
             "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": max(grid),
-                       "grid": list(grid), "grid_rule": args.grid, "per_gpu": args.per_gpu, "radius": 1,
+                       "grid": list(grid), "grid_rule": args.grid, "partition": args.partition, "per_gpu": args.per_gpu, "radius": 1,
                        "parallelism": f"domain-decomp{n}",
                        "decomposition": "x".join(str(v) for v in (model.domain.placement_dim().x,
                                                                    model.domain.placement_dim().y,

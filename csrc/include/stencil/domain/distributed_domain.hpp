@@ -171,6 +171,9 @@ public:
   // NodeAware partition: relative cost per interface cell of cuts normal to x/y/z (NodePartition; default 1,1,1)
   void set_axis_cost(const Dim3 &c) { axisCost_ = c; }
   const Dim3 &axis_cost() const { return axisCost_; }
+  // NodeAware cut rule inside a node (PartitionObjective; default Interface = the reference's greedy rule)
+  void set_partition_objective(PartitionObjective o) { objective_ = o; }
+  PartitionObjective partition_objective() const { return objective_; }
   void set_gpus(const std::vector<int> &gpus) { gpus_ = gpus; }
   const std::vector<int> &gpus() const { return gpus_; }
   void set_backend(Backend b) { backend_ = b; backendSet_ = true; }
@@ -300,6 +303,7 @@ private:
   MethodFlags flags_ = MethodFlags::All;
   PlacementStrategy strategy_ = PlacementStrategy::NodeAware;
   Dim3 axisCost_{1, 1, 1};
+  PartitionObjective objective_ = PartitionObjective::Interface;
   int commBlocks_ = 0;
   Backend backend_ = Backend::Device;
   bool backendSet_ = false;

@@ -32,6 +32,7 @@ struct StencilModelConfig {
   // N=2 645x645x323 837 vs 645x323x645 790; N=4 813x407x407 664 (either order); N=8 1024x512x256 1000 vs
   // 1024x256x512 972 Gcells/s
   Dim3 axisCost{4, 3, 2};
+  PartitionObjective partition = PartitionObjective::Interface; // NodeAware cut rule inside a node
   std::vector<int> gpus;       // empty = automatic
   bool overlap = true;
   // when every halo comes from this GPU (periodic self-wrap / co-resident sub-domains) the exchange is a local

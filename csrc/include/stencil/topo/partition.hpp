@@ -5,6 +5,7 @@
 //   NodePartition  two-level (nodes, then GPUs per node) minimum radius-weighted interface       :148-310
 #include <algorithm>
 #include <cmath>
+#include <utility>
 #include <vector>
 
 #include "stencil/core/geometry.hpp"
@@ -91,6 +92,20 @@ public:
   }
 };
 
+// How NodePartition chooses the cuts inside a node.
+//   Interface  the reference's rule (partition.hpp:210-264): each prime-factor cut goes where the radius-weighted
+//              interface (x axis cost) is smallest, greedily.
+//   MaxLink    the GPUs of an MI355X node are a fully connected xGMI mesh (7 point-to-point links per GPU, no
+//              switch): the neighbours of a sub-domain sit on different links, so an exchange takes as long as its
+//              busiest link, not its total surface. Every factorization dx*dy*dz of the node's GPU count is scored by
+//              (max over axes of the halo cells one link carries) x axis cost, then by the total halo cells x axis
+//              cost; an axis cut into 2 puts both of its faces on the same link (double volume), an axis cut into
+//              >= 3 gives each face its own link, an uncut axis wraps on the GPU. For equal cubes per GPU this
+//              prefers slabs (1x1xN: two faces per GPU, one per link, x and y wrapped in the stencil kernel) over
+//              1x2x4 (four faces, two on one link) or 2x2x2 (six faces, two per link, strided x faces).
+//              The node-level cuts (inter-node links) keep the greedy interface rule.
+enum class PartitionObjective { Interface, MaxLink };
+
 class NodePartition : public GridPartition {
   Dim3 sysDim_{1, 1, 1};
   Dim3 nodeDim_{1, 1, 1};
@@ -117,16 +132,62 @@ class NodePartition : public GridPartition {
   }
 
 public:
+  // (max-link cost, total cost) of cutting a box of `size` into d sub-domains (MaxLink objective)
+  static std::pair<int64_t, int64_t> link_cost(const Dim3 &size, const Dim3 &d, const Radius &radius, const Dim3 &cost) {
+    const Dim3 s(div_ceil(size.x, d.x), div_ceil(size.y, d.y), div_ceil(size.z, d.z));
+    const int64_t face[3] = {s.y * s.z, s.x * s.z, s.x * s.y};
+    const int64_t n[3] = {d.x, d.y, d.z};
+    const int64_t c[3] = {cost.x, cost.y, cost.z};
+    int64_t worst = 0, total = 0;
+    for (int a = 0; a < 3; ++a) {
+      if (n[a] == 1) continue;
+      const Dim3 pd(a == 0, a == 1, a == 2);
+      const int64_t rp = radius.dir(pd), rm = radius.dir(Dim3(0, 0, 0) - pd);
+      const int64_t link = face[a] * (n[a] == 2 ? rp + rm : std::max(rp, rm)) * c[a];
+      worst = std::max(worst, link);
+      total += face[a] * (rp + rm) * c[a];
+    }
+    return {worst, total};
+  }
+
+  // the MaxLink choice of dims for `n` parts of a box of `size` (ties: fewer x cuts, then fewer y cuts)
+  static Dim3 max_link_dims(const Dim3 &size, int64_t n, const Radius &radius, const Dim3 &cost) {
+    Dim3 best(1, 1, n);
+    std::pair<int64_t, int64_t> bc{-1, -1};
+    for (int64_t dx = 1; dx <= n; ++dx) {
+      if (n % dx) continue;
+      for (int64_t dy = 1; dy <= n / dx; ++dy) {
+        if ((n / dx) % dy) continue;
+        const Dim3 d(dx, dy, n / dx / dy);
+        if (d.x > size.x || d.y > size.y || d.z > size.z) continue;
+        const auto c = link_cost(size, d, radius, cost);
+        const bool better = bc.first < 0 || c < bc ||
+                            (c == bc && (d.x < best.x || (d.x == best.x && d.y < best.y)));
+        if (better) {
+          bc = c;
+          best = d;
+        }
+      }
+    }
+    return best;
+  }
+
   NodePartition() = default;
   // axisCost: relative cost per interface cell of a cut normal to x / y / z (default 1,1,1: the reference's plain
-  // radius-weighted interface). StencilModel uses (2,1,1): an x face is a strided column (one 128-B line per row
+  // radius-weighted interface). StencilModel uses (4,3,2): an x face is a strided column (one 128-B line per row
   // for a 2-cell halo, packed and unpacked by gathers) while y/z faces are contiguous rows, and a domain without x
   // cuts can overlap its exchange with row-contiguous exterior slabs only.
-  NodePartition(const Dim3 &size, const Radius &radius, int64_t nodes, int64_t gpus, const Dim3 &axisCost = Dim3(1, 1, 1)) {
+  NodePartition(const Dim3 &size, const Radius &radius, int64_t nodes, int64_t gpus, const Dim3 &axisCost = Dim3(1, 1, 1),
+                PartitionObjective objective = PartitionObjective::Interface) {
     size_ = size;
     cost_ = axisCost;
     for (int64_t amt : prime_factors_desc(nodes)) split(sysDim_, amt, radius);
-    for (int64_t amt : prime_factors_desc(gpus)) split(nodeDim_, amt, radius);
+    if (objective == PartitionObjective::MaxLink && gpus > 1) {
+      nodeDim_ = max_link_dims(size_, gpus, radius, cost_);
+      size_ = Dim3(div_ceil(size_.x, nodeDim_.x), div_ceil(size_.y, nodeDim_.y), div_ceil(size_.z, nodeDim_.z));
+    } else {
+      for (int64_t amt : prime_factors_desc(gpus)) split(nodeDim_, amt, radius);
+    }
     dim_ = sysDim_ * nodeDim_;
     rem_ = size % dim_;
   }

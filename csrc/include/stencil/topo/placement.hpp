@@ -76,7 +76,8 @@ public:
   // `bw` is evaluated on rank 0 only. All ranks must contribute the same number of devices and every node must host
   // the same number of ranks (as in the reference, partition.hpp:749).
   NodeAwarePlacement(const Dim3 &size, comm::ProcGroup &pg, const Radius &radius, const std::vector<int> &rankDevices,
-                     const BandwidthFn &bw, const Dim3 &axisCost = Dim3(1, 1, 1));
+                     const BandwidthFn &bw, const Dim3 &axisCost = Dim3(1, 1, 1),
+                     PartitionObjective objective = PartitionObjective::Interface);
   Dim3 subdomain_size(const Dim3 &idx) const override { return part_.subdomain_size(idx); }
   Dim3 subdomain_origin(const Dim3 &idx) const override { return part_.subdomain_origin(idx); }
   Dim3 dim() const override { return part_.dim(); }

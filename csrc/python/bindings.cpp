@@ -302,9 +302,17 @@ PYBIND11_MODULE(_C, m) {
       .def("subdomain_origin", &RankPartition::subdomain_origin)
       .def("linearize", &RankPartition::linearize)
       .def("dimensionize", &RankPartition::dimensionize);
+  py::enum_<PartitionObjective>(m, "PartitionObjective")
+      .value("Interface", PartitionObjective::Interface)
+      .value("MaxLink", PartitionObjective::MaxLink);
   py::class_<NodePartition>(m, "NodePartition")
-      .def(py::init<const Dim3 &, const Radius &, int64_t, int64_t, const Dim3 &>(), py::arg("size"), py::arg("radius"),
-           py::arg("nodes"), py::arg("gpus"), py::arg("axis_cost") = Dim3(1, 1, 1))
+      .def(py::init<const Dim3 &, const Radius &, int64_t, int64_t, const Dim3 &, PartitionObjective>(), py::arg("size"),
+           py::arg("radius"), py::arg("nodes"), py::arg("gpus"), py::arg("axis_cost") = Dim3(1, 1, 1),
+           py::arg("objective") = PartitionObjective::Interface)
+      .def_static("max_link_dims", &NodePartition::max_link_dims, py::arg("size"), py::arg("n"), py::arg("radius"),
+                  py::arg("axis_cost") = Dim3(1, 1, 1))
+      .def_static("link_cost", &NodePartition::link_cost, py::arg("size"), py::arg("dims"), py::arg("radius"),
+                  py::arg("axis_cost") = Dim3(1, 1, 1))
       .def("dim", &NodePartition::dim)
       .def("sys_dim", &NodePartition::sys_dim)
       .def("node_dim", &NodePartition::node_dim)
@@ -542,6 +550,8 @@ PYBIND11_MODULE(_C, m) {
       .def("methods", &DistributedDomain::methods)
       .def("set_placement", &DistributedDomain::set_placement)
       .def("set_axis_cost", &DistributedDomain::set_axis_cost)
+      .def("set_partition_objective", &DistributedDomain::set_partition_objective)
+      .def("partition_objective", &DistributedDomain::partition_objective)
       .def("set_comm_max_blocks", &DistributedDomain::set_comm_max_blocks)
       .def("set_gpus", &DistributedDomain::set_gpus)
       .def("gpus", &DistributedDomain::gpus)
@@ -669,6 +679,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("methods", &StencilModelConfig::methods)
       .def_readwrite("placement", &StencilModelConfig::placement)
       .def_readwrite("axis_cost", &StencilModelConfig::axisCost)
+      .def_readwrite("partition", &StencilModelConfig::partition)
       .def_readwrite("gpus", &StencilModelConfig::gpus)
       .def_readwrite("overlap", &StencilModelConfig::overlap)
       .def_readwrite("auto_overlap", &StencilModelConfig::autoOverlap)

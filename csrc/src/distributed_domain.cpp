@@ -334,6 +334,7 @@ int64_t DistributedDomain::probe_transports(MethodFlags m) {
   p.set_methods(m);
   p.set_placement(strategy_);
   p.set_axis_cost(axisCost_);
+  p.set_partition_objective(objective_);
   if (!gpus_.empty()) p.set_gpus(gpus_);
   if (backendSet_) p.set_backend(backend_);
   p.set_transport_options(topt_);
@@ -588,7 +589,7 @@ void DistributedDomain::realize() {
     if (strategy_ == PlacementStrategy::NodeAware) {
       BandwidthFn bw = dev ? BandwidthFn([](int a, int b) { return gpu_topo::bandwidth(a, b); })
                            : BandwidthFn([](int a, int b) { return a == b ? 10.0 : 1.0; });
-      placement_.reset(new NodeAwarePlacement(size_, pg, radius_, gpus_, bw, axisCost_));
+      placement_.reset(new NodeAwarePlacement(size_, pg, radius_, gpus_, bw, axisCost_, objective_));
     } else {
       placement_.reset(new TrivialPlacement(size_, pg, gpus_));
     }

@@ -45,7 +45,8 @@ TrivialPlacement::TrivialPlacement(const Dim3 &size, comm::ProcGroup &pg, const 
 }
 
 NodeAwarePlacement::NodeAwarePlacement(const Dim3 &size, comm::ProcGroup &pg, const Radius &radius,
-                                       const std::vector<int> &rankDevices, const BandwidthFn &bw, const Dim3 &axisCost) {
+                                       const std::vector<int> &rankDevices, const BandwidthFn &bw, const Dim3 &axisCost,
+                                       PartitionObjective objective) {
   const int gpusPerRank = int(rankDevices.size());
   STENCIL_REQUIRE(pg.allreduce_min_i64(gpusPerRank) == -pg.allreduce_min_i64(-int64_t(gpusPerRank)),
                   "NodeAware placement requires the same number of GPUs on every rank");
@@ -67,7 +68,7 @@ NodeAwarePlacement::NodeAwarePlacement(const Dim3 &size, comm::ProcGroup &pg, co
   for (auto &nr : nodeRanks)
     STENCIL_REQUIRE(int(nr.size()) == ranksPerNode, "NodeAware placement requires the same number of ranks per node");
   const int gpusPerNode = gpusPerRank * ranksPerNode;
-  part_ = NodePartition(size, radius, numNodes, gpusPerNode, axisCost);
+  part_ = NodePartition(size, radius, numNodes, gpusPerNode, axisCost, objective);
   const Dim3 dim = part_.dim();
   const int64_t numSub = dim.flatten();
 

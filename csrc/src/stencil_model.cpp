@@ -29,6 +29,7 @@ StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::
   dd_->set_methods(cfg.methods);
   dd_->set_placement(cfg.placement);
   dd_->set_axis_cost(cfg.axisCost);
+  dd_->set_partition_objective(cfg.partition);
   if (!cfg.gpus.empty()) dd_->set_gpus(cfg.gpus);
   if (cfg.setBackend) dd_->set_backend(cfg.backend);
   dd_->set_transport_options(cfg.transport);

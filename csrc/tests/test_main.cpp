@@ -72,6 +72,18 @@ TEST(partition_reference_values, false) {
   CHECK(q.subdomain_origin(Dim3(2, 2, 0)) == Dim3(7, 10, 0));
 }
 
+TEST(partition_max_link, false) {
+  Radius r = Radius::constant(0);
+  r.set_face(1);
+  const Dim3 c(4, 3, 2);
+  // stacked 512^3 cubes on one xGMI node: slabs (one face per link) beat 1x2x4 (two faces on the y link)
+  CHECK(NodePartition(Dim3(512, 512, 4096), r, 1, 8, c, PartitionObjective::MaxLink).dim() == Dim3(1, 1, 8));
+  CHECK(NodePartition(Dim3(512, 512, 2048), r, 1, 4, c, PartitionObjective::MaxLink).dim() == Dim3(1, 1, 4));
+  CHECK(NodePartition::link_cost(Dim3(512, 512, 1024), Dim3(1, 1, 2), r, c).first == 512 * 512 * 2 * 2);
+  // the reference rule is unchanged by default
+  CHECK(NodePartition(Dim3(1024, 1024, 1024), r, 1, 8, c).dim() == Dim3(1, 2, 4));
+}
+
 TEST(qap_reference_values, false) {
   const double inf = INFINITY;
   Mat2D<double> bw = {{inf, 1, 10}, {1, inf, 1}, {10, 1, inf}};

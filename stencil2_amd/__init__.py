@@ -33,6 +33,7 @@ from ._C import (  # noqa: E402,F401
     MethodFlags,
     NodeAwarePlacement,
     NodePartition,
+    PartitionObjective,
     PlacementStrategy,
     Radius,
     RankPartition,

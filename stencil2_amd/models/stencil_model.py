@@ -24,7 +24,7 @@ class StencilModel:
                  use_graph: bool = True, forward: bool = False, temporal: int = 1, backend=None,
                  tune: _C.StencilTune | None = None, group=None, axis_cost=None, wrap_self: bool = True,
                  transport: _C.TransportOptions | None = None, wrap_axes_mask: int = 7, local_interior: bool = True,
-                 overlap_mode: int = 1, self_test: bool = False):
+                 overlap_mode: int = 1, self_test: bool = False, partition=None):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
         cfg.kind = kind
@@ -55,6 +55,8 @@ class StencilModel:
         if axis_cost is not None:  # NodeAware cut costs per axis (default (4, 3, 2): x faces are strided and
             # whole periodic rows feed the whole-row kernels; z cuts before y cuts)
             cfg.axis_cost = _C.Dim3(*axis_cost)
+        if partition is not None:  # NodeAware cut rule inside a node: PartitionObjective.Interface (reference) or
+            cfg.partition = partition  # MaxLink (busiest xGMI link, then total halo)
         self.config = cfg
         self._m = _C.StencilModel(cfg, group if group is not None else get_group())
         self._dd = None

@@ -158,3 +158,34 @@ def test_trivial_and_nodeaware_single_process(st):
         nb = st.Dim3((idx.x + 1) % dim.x, idx.y, 0)
         if dim.x > 1:
             assert na.get_device(idx) // 2 == na.get_device(nb) // 2
+
+
+def test_node_partition_max_link(st):
+    """PartitionObjective.MaxLink: the node's GPUs are a fully connected xGMI mesh, so the cut minimises the halo
+    cells of the busiest link (an axis cut in two puts both faces on one link), then the total."""
+    D = st.Dim3
+    r = st.Radius.constant(0)
+    r.set_face(2)
+    ML = st.PartitionObjective.MaxLink
+    c = D(4, 3, 2)
+    # cost of 1x1x8 slabs of 512^3: one 512x512 face (both radii 2: max 2) per link, z cost 2
+    assert st.NodePartition.link_cost(D(512, 512, 4096), D(1, 1, 8), r, c) == (512 * 512 * 2 * 2, 512 * 512 * 4 * 2)
+    # an axis cut in two: both faces on the one link
+    assert st.NodePartition.link_cost(D(512, 512, 1024), D(1, 1, 2), r, c) == (512 * 512 * 4 * 2, 512 * 512 * 4 * 2)
+    # stacked cubes -> slabs; a cube of 8 GPUs keeps the reference-like 1x2x4 (busiest link ties 2x2x2, fewer x cuts)
+    assert st.NodePartition(D(512, 512, 4096), r, 1, 8, c, ML).dim() == D(1, 1, 8)
+    assert st.NodePartition(D(1024, 1024, 1024), r, 1, 8, D(1, 1, 1), ML).dim() == D(1, 2, 4)
+    assert st.NodePartition.max_link_dims(D(813, 813, 813), 4, r, c) == D(1, 1, 4)
+    # node-level cuts keep the greedy rule; the sub-domains still tile the grid exactly
+    p = st.NodePartition(D(600, 600, 900), r, 2, 4, c, ML)
+    d = p.dim()
+    assert d.x * d.y * d.z == 8
+    tot = 0
+    for i in range(d.x):
+        for j in range(d.y):
+            for k in range(d.z):
+                s = p.subdomain_size(D(i, j, k))
+                tot += s.x * s.y * s.z
+    assert tot == 600 * 600 * 900
+    # the default objective is the reference's rule
+    assert st.NodePartition(D(512, 512, 4096), r, 1, 8, c).dim() == st.NodePartition(D(512, 512, 4096), r, 1, 8, c, st.PartitionObjective.Interface).dim()
