@@ -95,6 +95,11 @@ void wait_flags_device(const std::vector<uint64_t *> &flags, uint64_t target, in
 // System-scope release, then lane i stores *flags[i] = value (flags may be IPC-mapped peer memory).
 void signal_flags_device(const std::vector<uint64_t *> &flags, uint64_t value, hipStream_t stream);
 constexpr int kMaxFlagsPerLaunch = 64;
+// Grid cap of the fused wait + copy + signal kernels: every block spins until the peer's flags arrive, and a
+// spinning block holds its CU. Uncapped (one 1024-thread block per CU) two ranks sharing a GPU could fill every CU
+// slot with waiting blocks while the peers they wait for cannot start their pack kernels: four ranks on one MI355X
+// (1x2x2) deadlocked until the wait timeout (gpurun_out/r3e, r3). 32 CUs still move a 2-MiB face in a few us.
+constexpr int kFusedMaxBlocks = 32;
 // One fused launch: wait until every `wait` flag >= waitTarget (bounded: on timeout `code` goes to *err), run the
 // copy plan on at most maxBlocks 1024-thread blocks (0: up to one per CU), then release-store signalValue into every
 // `signal` flag once all blocks are done (`counter`: a zeroed device word, reset by the kernel; one per stream).

@@ -400,9 +400,9 @@ void copy_plan_device_sync(const CopyPlan &p, hipStream_t stream, int maxBlocks,
   fs.code = a.code;
   fs.timeoutTicks = uint64_t(a.timeout_s * 1e8);
   STENCIL_REQUIRE(fs.signal.n == 0 || a.counter, "copy_plan_device_sync: signal flags need a block counter");
-  // one CU per block (1024 threads): at most maxBlocks, or the whole GPU when unconfined; at least one block, so
-  // the flags are waited for and raised even when this device has nothing to copy
-  const int cap = maxBlocks > 0 ? maxBlocks : 256;
+  // one CU per block (1024 threads): at most maxBlocks and kFusedMaxBlocks (waiting blocks hold their CUs); at
+  // least one block, so the flags are waited for and raised even when this device has nothing to copy
+  const int cap = maxBlocks > 0 ? std::min(maxBlocks, kFusedMaxBlocks) : kFusedMaxBlocks;
   const int blocks = std::max(1, std::min(cap, (p.nwork + 3) / 4));
   hipLaunchKernelGGL(copy_plan_kernel_sync, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dwork, uint32_t(p.nwork),
                      fs);
