@@ -1351,6 +1351,17 @@ void DistributedDomain::set_colo_copy(TransportOptions::Copy c) {
   if (c == topt_.coloCopy) return;
   if (realized_) sync_exchange(); // the staging buffers and inbox slots of the exchanges in flight
   topt_.coloCopy = c;
+  // back to pack-kernel stores with no DMA-engine pipes left: drop the copy streams the engine copies created.
+  // Every stream may take a hardware queue of its own, and a process whose streams outnumber its queues
+  // multiplexes them (4 ranks sharing one MI355X after a warm-up that tried engine copies: 2.94 ms per step
+  // instead of 0.52, profiles/r3/check3)
+  if (realized_ && backend_ == Backend::Device && c == TransportOptions::Copy::Store && impl_->pipes.empty())
+    for (auto &ctx : impl_->devs) {
+      for (auto &s : ctx.copyStreams) s.sync();
+      ctx.copyStreams.clear();
+      ctx.copyJoin.clear();
+      ctx.copyFork = Event();
+    }
 }
 
 void DistributedDomain::set_transport_options_live(const TransportOptions &o) {
