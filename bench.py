@@ -244,19 +244,23 @@ def main():
         k = max(2, args.tune_steps // 2 * 2)
         r0 = args.x2reserve
         # (mode, CUs left to the transports, co-located copy): mode 1 = slabs beside the sweep, 2 = slabs after
-        # it, 0 = whole-region pairs; copy "s" = pack kernel stores into the peer inbox, "e" = DMA engine copy (the
+        # it, 0 = whole-region pairs, 3 = pipelined whole-region pairs; copy "s" = pack kernel stores into the peer inbox, "e" = DMA engine copy (the
         # transports then need fewer CUs: also tried with a quarter of the reserve)
         copies = ["s", "e"] if colo and args.colo_copy == "auto" else ["e" if args.colo_copy == "engine" else "s"]
         cands = []
         for cp in copies:
+            # mode 3 (pipelined pairs: the next exchange gated on the sweep's published boundary planes) needs the
+            # pack-kernel stores
+            if cp == "s" and model.can_pipeline():
+                cands += [(3, r0, cp), (3, max(1, r0 // 2), cp), (3, 2 * r0, cp)]
             cands += [(1, r0, cp), (1, max(1, r0 // 2), cp), (1, 2 * r0, cp), (2, r0, cp), (0, r0, cp)]
             if cp == "e":
                 cands.append((1, max(1, r0 // 4), cp))
 
         def apply(c):
+            model.domain.set_colo_copy(topt.Copy.Engine if c[2] == "e" else topt.Copy.Store)
             model.set_overlap_mode(c[0])
             model.set_comm_reserve(c[1])
-            model.domain.set_colo_copy(topt.Copy.Engine if c[2] == "e" else topt.Copy.Store)
 
         skip = set()
         for c in cands + cands:
@@ -358,7 +362,7 @@ def main():
                        "decomposition": "x".join(str(v) for v in (model.domain.placement_dim().x,
                                                                    model.domain.placement_dim().y,
                                                                    model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
-                       "overlap": model.overlapping(), "overlap_tuned": overlap_tuned, "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
+                       "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned, "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
                        "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
                        "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none",
                        "transport": {"inbox": args.inbox, "colo_copy": str(model.domain.transport_options().colo_copy).split(".")[-1].lower(),

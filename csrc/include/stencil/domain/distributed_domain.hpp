@@ -272,6 +272,15 @@ public:
   // sweep costs the pair ~80 us unconfined (its blocks land on CUs the sweep's blocks then wait for) and ~25 us
   // confined to 8 CUs beside a sweep that leaves 8 free.
   void set_comm_max_blocks(int n) { commBlocks_ = n; }
+  // Producer gate for the next exchange_async on the comm stream (pipelined pairs): instead of waiting for the
+  // producer's whole kernel (record_ready), the fused co-located pack kernel polls *counter >= target, a word the
+  // still-running stencil sweep raises once the boundary planes the exchange reads are written
+  // (StencilTune::publish). Valid only where gated_send_supported(skipAxes); consumed by that one exchange.
+  void set_send_gate(uint64_t *counter, uint64_t target);
+  // every halo of this process's one device leaves through fused pack-kernel stores of the Colocated transport
+  // (no same-GPU translate for these skip axes, no DMA-engine pipes, no RCCL / staged channels): the only kind of
+  // exchange a producer gate can start early
+  bool gated_send_supported(int skipAxes) const;
   void swap();
 
   // ---- output ----

@@ -106,6 +106,10 @@ constexpr int kFusedMaxBlocks = 32;
 struct FlagSyncArgs {
   std::vector<uint64_t *> wait;
   uint64_t waitTarget = 0;
+  // producer gate (pipelined pairs): local words, e.g. the boundary-plane counter a stencil sweep that is still
+  // running publishes (StencilTune::publish), polled before the copies as well, with their own target
+  std::vector<uint64_t *> gate;
+  uint64_t gateTarget = 0;
   std::vector<uint64_t *> signal;
   uint64_t signalValue = 0;
   uint32_t *counter = nullptr;

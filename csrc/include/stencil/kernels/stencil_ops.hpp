@@ -85,7 +85,15 @@ struct StencilTune {
   // 16-B chunk (fused pairs: >= 2 chunks). Fused pairs: stencil7x2_wrappable_axes; single steps (stencil7_apply):
   // stencil7_wrappable_axes. 0 = read halos.
   int wrap = 0;
+  // pipelined pairs (StencilModel overlap mode 3; run-time state, not configuration): the whole-row kernel adds the
+  // number of cells it has written in the first / last `publishDepth` z planes of the region to *publish (device
+  // word, system-scope release after each such plane), so a gated exchange (DistributedDomain::set_send_gate) packs
+  // the boundary planes while the rest of the sweep is still running. Other fused-pair kernels refuse it.
+  uint64_t *publish = nullptr;
+  int publishDepth = 0;
 };
+// the whole-row fused-pair kernel (the one that can publish its boundary planes) takes this region
+bool stencil7x2_row_kernel_used(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune);
 // axes (mask as StencilTune::wrap) the fused-pair kernels can wrap in-kernel for this quantity's layout; x2row as
 // StencilTune::x2row (0: no whole-row kernel, so ragged x extents are not wrappable)
 int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi, int x2row = 1);

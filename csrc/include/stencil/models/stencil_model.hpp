@@ -101,8 +101,13 @@ public:
   // overlapped pairs, where the slabs at the remote faces run: 1 = on the comm stream right behind the exchange,
   // beside the interior sweep (default); 2 = on the compute stream after the interior sweep (the sweep then shares the
   // GPU with the transport kernels only). 0 = whole-region pairs (set_overlap(false)).
+  // 3 = pipelined pairs (can_pipeline()): whole-region sweeps, each publishing its boundary z planes while it runs;
+  // the exchange the NEXT pair needs is gated on that publication (DistributedDomain::set_send_gate), so its pack,
+  // xGMI stores and unpack run beside the rest of this sweep on the CUs it leaves free, and no sweep is split into
+  // interior and slabs. Needs remote halos along z only, the whole-row kernel and fused co-located transports.
   void set_overlap_mode(int mode);
-  int overlap_mode() const { return overlap_ ? (slabsAfter_ ? 2 : 1) : 0; }
+  int overlap_mode() const { return pipelined_ ? 3 : (overlap_ ? (slabsAfter_ ? 2 : 1) : 0); }
+  bool can_pipeline() const { return pipeOk_; }
   // CUs the overlapped sweeps leave to the transport kernels (StencilTune::x2reserve); synchronizes first
   void set_comm_reserve(int cus);
   int comm_reserve() const { return cfg_.tune.x2reserve; }
@@ -127,6 +132,12 @@ private:
   bool pairs_ = false; // temporal blocking active
   bool overlapToggle_ = false;
   bool slabsAfter_ = false; // overlap mode 2 (see set_overlap_mode)
+  bool pipeOk_ = false;      // overlap mode 3 possible (see init)
+  bool pipelined_ = false;   // overlap mode 3
+  bool lastPublished_ = false; // the last enqueued sweep published its boundary planes into pubCounter_
+  uint64_t *pubCounter_ = nullptr; // device word (uncached), cumulative boundary cells published
+  uint64_t pubTotal_ = 0;          // its value once every published sweep so far is done
+  uint64_t pubCells_ = 0;          // boundary cells one sweep publishes (all quantities)
   StencilTune pairTune_; // cfg_.tune + the in-kernel wrap axes of the fused pairs
   StencilTune stepTune_; // cfg_.tune + the in-kernel wrap axes of single steps
   bool localSteps_ = false;                      // overlapped single steps on the local interior (see init)

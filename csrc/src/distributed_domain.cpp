@@ -200,6 +200,8 @@ struct DistributedDomain::Impl {
   bool callerPending = false; // callerDone marks a caller-stream exchange not yet joined by sync_exchange
   bool commPending = false;   // the comm stream holds an exchange (devs[0].done) a caller stream has not waited for
   bool engineRefused = false; // hipMemcpyDeviceToDeviceNoCU not accepted by the runtime (warned once)
+  uint64_t *gateCounter = nullptr; // set_send_gate: consumed by the next exchange_async
+  uint64_t gateTarget = 0;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -1490,6 +1492,26 @@ void DistributedDomain::prepare_skip_wrapped(int axes) {
   I.skipAxes = axes;
 }
 
+void DistributedDomain::set_send_gate(uint64_t *counter, uint64_t target) {
+  STENCIL_REQUIRE(realized_, "set_send_gate before realize");
+  impl_->gateCounter = counter;
+  impl_->gateTarget = target;
+}
+
+bool DistributedDomain::gated_send_supported(int skipAxes) const {
+  if (!realized_ || backend_ != Backend::Device) return false;
+  const Impl &I = *impl_;
+  if (I.devs.size() != 1 || !I.pipes.empty() || I.rccl) return false;
+  const DevCtx &ctx = I.devs[0];
+  if (skipAxes != 0 && skipAxes != I.skipAxes) return false;
+  const SegList &tl = skipAxes != 0 ? ctx.translateSkip : ctx.translate;
+  if (!tl.host[0].empty() || !tl.host[1].empty()) return false;
+  if (!ctx.stagedSend.empty() || !ctx.stagedRecv.empty() || !ctx.rcclSend.empty() || !ctx.rcclRecv.empty())
+    return false;
+  return !ctx.coloSend.empty() && topt_.coloCopy == TransportOptions::Copy::Store && topt_.fuseFlags &&
+         topt_.completion == TransportOptions::Completion::Kernel;
+}
+
 void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   STENCIL_REQUIRE(realized_, "exchange before realize");
   STENCIL_REQUIRE(poisoned_.empty(), "halo exchange unusable after an earlier failure: " << poisoned_);
@@ -1538,8 +1560,15 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     I.callerDone.wait_on(I.devs[0].comm);
   }
 
+  // a producer gate replaces the wait for the producers' kernels (set_send_gate)
+  const bool gated = I.gateCounter != nullptr;
+  uint64_t *gateCounter = I.gateCounter;
+  const uint64_t gateTarget = I.gateTarget;
+  I.gateCounter = nullptr;
+  if (gated)
+    STENCIL_REQUIRE(!over && gated_send_supported(skipAxes), "gated exchange without a fused co-located-only plan");
   // (0) dependencies: the comm streams start after every local domain's producer work
-  if (!over) {
+  if (!over && !gated) {
     bool anyMissing = false;
     for (size_t di = 0; di < domains_.size(); ++di) anyMissing |= !I.readyPending[di];
     if (anyMissing && topt_.nullStreamProducers && I.devs.size() == 1) {
@@ -1692,6 +1721,10 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       FlagSyncArgs fa;
       fa.wait = credits;
       fa.waitTarget = I.epoch - 2;
+      if (gated) {
+        fa.gate = {gateCounter};
+        fa.gateTarget = gateTarget;
+      }
       fa.signal = arrived;
       fa.signalValue = I.epoch;
       fa.counter = ctx.syncCounter;

@@ -320,6 +320,8 @@ __device__ __forceinline__ void poll_flags(const FlagList &f, uint64_t target, i
 struct FlagSync {
   FlagList wait;        // polled before any copy (n = 0: none)
   uint64_t waitTarget;
+  FlagList gate;        // also polled before any copy (producer gate, own target)
+  uint64_t gateTarget;
   FlagList signal;      // stored after every block's copies are done
   uint64_t signalValue;
   uint32_t *counter;    // blocks done; 0 at launch, reset by the last block
@@ -337,8 +339,11 @@ struct FlagSync {
 __global__ __launch_bounds__(1024) void copy_plan_kernel_sync(const CopySeg *__restrict__ segs,
                                                               const CopyWork *__restrict__ work, uint32_t nwork,
                                                               FlagSync fs) {
-  if (fs.wait.n > 0) {
-    if (threadIdx.x < 64) poll_flags(fs.wait, fs.waitTarget, fs.err, fs.code, fs.timeoutTicks, int(threadIdx.x));
+  if (fs.wait.n > 0 || fs.gate.n > 0) {
+    if (threadIdx.x < 64) {
+      poll_flags(fs.wait, fs.waitTarget, fs.err, fs.code, fs.timeoutTicks, int(threadIdx.x));
+      poll_flags(fs.gate, fs.gateTarget, fs.err, fs.code, fs.timeoutTicks, int(threadIdx.x));
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the peer's slot writes / reads before our copies
     __syncthreads();
   }
@@ -393,6 +398,8 @@ void copy_plan_device_sync(const CopyPlan &p, hipStream_t stream, int maxBlocks,
   FlagSync fs{};
   fs.wait = to_list(a.wait);
   fs.waitTarget = a.waitTarget;
+  fs.gate = to_list(a.gate);
+  fs.gateTarget = a.gateTarget;
   fs.signal = to_list(a.signal);
   fs.signalValue = a.signalValue;
   fs.counter = a.counter;

@@ -533,7 +533,17 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
         cs[nbuf][w][h][lane] = C[s2][h];
         if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
       }
+      // boundary-plane publication (block-uniform): every wave's stores of plane z complete before the barrier,
+      // then one thread writes the XCD's L2 back (system-scope release) and counts the block's cells of the plane
+      const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
+      if (pubStep) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (pubStep && lane == 0 && w == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        const unsigned long long cells =
+            (unsigned long long)(min(YO, a.hiy - yblk)) * (unsigned long long)(a.hix - a.lox);
+        __hip_atomic_fetch_add(a.pub, cells, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       buf = nbuf;
 #pragma unroll
       for (int h = 0; h < H; ++h) {
@@ -1101,6 +1111,11 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   a.nchunks = 128;
   a.remap = tune.xcdRemap ? 1 : 0;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  if (tune.publish) {
+    a.pub = reinterpret_cast<unsigned long long *>(tune.publish);
+    a.pubLo = a.loz + tune.publishDepth;
+    a.pubHi = a.hiz - tune.publishDepth;
+  }
   a.gx = 1;
   a.gy = (ny + YO - 1) / YO;
   const void *kern = (const void *)stencil7x2_row_kernel<NW, PF, KIND, H, RAG>;
@@ -1189,6 +1204,14 @@ static void apply_x2col2_wrap(const LocalDomain &dom, int64_t qi, const Rect3 &r
     apply_x2col2_t<KIND, PF, 0>(dom, qi, region, sph, stream, tune);
 }
 
+bool stencil7x2_row_kernel_used(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune) {
+  if (region.empty() || !stencil7x2_supported(dom, qi) || dom.elem_size(qi) != 4 || !tune.x2row || !(tune.wrap & 1))
+    return false;
+  const Rect3 rr(region.lo - dom.accessor_origin(), region.hi - dom.accessor_origin());
+  const int64_t nx = rr.hi.x - rr.lo.x;
+  return (nx == 512 || (nx > 256 && nx <= 768)) && (rr.lo.x - dom.radius().x(-1)) % 4 == 0;
+}
+
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune) {
   if (region.empty()) return;
@@ -1228,6 +1251,7 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
                    : apply_x2row_t<1, 1, 3, true>(dom, qi, region, sph, stream, tune);
       if (done) return;
     }
+    STENCIL_REQUIRE(!tune.publish, "boundary-plane publication needs the whole-row kernel");
     // x a whole number of 512-cell columns from a 16-B aligned first cell: the 512-cell column kernel
     if (nx % 512 == 0 && (rr.lo.x - dom.radius().x(-1)) % 4 == 0) {
       // one plane of lookahead (two would spill the Jacobi instance; the row kernel shows no difference)
@@ -1236,6 +1260,7 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
       return;
     }
   }
+  STENCIL_REQUIRE(!tune.publish, "boundary-plane publication needs the whole-row kernel");
   // the column kernels wrap x only for whole chunks (ragged periodic rows are the whole-row kernel's)
   STENCIL_REQUIRE(!(tune.wrap & 1) || (stencil7x2_wrappable_axes(dom, qi, 0) & 1),
                   "in-kernel x wrap of a ragged row needs the whole-row kernel (fp32, x2row, 256 < nx < 1024)");

@@ -66,6 +66,9 @@ template <typename T> struct StencilArgs {
   // the exchange would have to copy first (raw coordinates)
   int wrapm;
   int wlo[3], wn[3];
+  // boundary-plane publication (StencilTune::publish): output planes z < pubLo or z >= pubHi (raw) count into *pub
+  unsigned long long *pub;
+  int pubLo, pubHi;
 };
 
 // periodic image of raw coordinate c along axis ax (identity unless the axis wraps)

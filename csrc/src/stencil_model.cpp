@@ -52,6 +52,7 @@ StencilModel::~StencilModel() {
     if (g) (void)hipGraphExecDestroy(g);
   for (auto &g : graphBlock_)
     if (g) (void)hipGraphExecDestroy(g);
+  if (pubCounter_) (void)hipFree(pubCounter_);
 }
 
 int64_t StencilModel::local_cells() const {
@@ -151,6 +152,26 @@ void StencilModel::init() {
       ok = ok && !pairInteriors_[di].empty();
     }
     overlapToggle_ = remote && ok && doms0[0].backend() == Backend::Device;
+  }
+  // pipelined pairs (overlap mode 3): one device, halos remote along z only (every boundary plane an exchange reads
+  // is one of the first / last two z planes of the sweep), the whole-row kernel for every quantity, and a plan the
+  // producer gate can start (fused co-located stores only; re-checked per pair since the co-located copy can change)
+  if (overlapToggle_ && doms0.size() == 1 && doms0[0].backend() == Backend::Device) {
+    const auto li = dd_->get_local_interior(2);
+    const Rect3 c = doms0[0].get_compute_region();
+    bool ok = li[0].lo.x == c.lo.x && li[0].hi.x == c.hi.x && li[0].lo.y == c.lo.y && li[0].hi.y == c.hi.y &&
+              dd_->gated_send_supported(pairTune_.wrap) && c.extent().z >= 8;
+    for (int64_t q = 0; q < doms0[0].num_data() && ok; ++q) ok = stencil7x2_row_kernel_used(doms0[0], q, c, pairTune_);
+    if (ok) {
+      pipeOk_ = true;
+      const Dim3 e = c.extent();
+      pubCells_ = uint64_t(e.x) * uint64_t(e.y) * uint64_t(std::min<int64_t>(e.z, 4)) * uint64_t(doms0[0].num_data());
+      doms0[0].set_device();
+      HIP_CHECK(hipExtMallocWithFlags((void **)&pubCounter_, 256, hipDeviceMallocUncached));
+      HIP_CHECK(hipMemset(pubCounter_, 0, 256));
+      HIP_CHECK(hipDeviceSynchronize());
+      if (cfg_.overlapMode == 3 && overlap_) pipelined_ = true;
+    }
   }
   // single steps: the self-periodic axes are read in-kernel at their periodic image and their same-GPU copies leave
   // the exchange (a fully periodic sub-domain exchanges nothing; one MI355X at 512^3: the ~25 us copy-plan kernel of
@@ -331,6 +352,31 @@ void StencilModel::prepare() {
 void StencilModel::enqueue_step(int k) {
   auto &doms = dd_->domains();
   const bool device = !compute_.empty();
+  const bool gateOk = lastPublished_; // the previous sweep published: the next exchange may start on its planes
+  lastPublished_ = false;
+  if (k == 2 && pipelined_) {
+    // pipelined pairs: this pair's exchange was gated on the previous sweep's boundary planes (it ran beside the
+    // rest of that sweep); the sweep waits for it, then publishes its own boundary planes for the next exchange
+    const bool gate = gateOk && dd_->gated_send_supported(pairTune_.wrap);
+    if (gate) dd_->set_send_gate(pubCounter_, pubTotal_);
+    dd_->exchange_async(nullptr, pairTune_.wrap);
+    dd_->wait_exchange(0, compute_[0]);
+    StencilTune ti = pairTune_;
+    ti.reserveCUs = cfg_.tune.x2reserve;
+    const Rect3 c = doms[0].get_compute_region();
+    const bool pub = dd_->gated_send_supported(pairTune_.wrap);
+    if (pub) {
+      ti.publish = pubCounter_;
+      ti.publishDepth = 2;
+    }
+    for (int64_t q = 0; q < doms[0].num_data(); ++q)
+      stencil7x2_apply(doms[0], q, c, cfg_.kind, sph_, compute_[0].get(), ti);
+    if (pub) {
+      pubTotal_ += pubCells_;
+      lastPublished_ = true;
+    }
+    return;
+  }
   if (k == 2 && overlap_) {
     // temporal blocking, overlapped: interior S o S on the compute stream while the depth-2 exchange runs on the
     // comm stream, then the exterior slabs on the comm stream behind it; the compute stream joins them
@@ -451,10 +497,12 @@ void StencilModel::set_overlap(bool on) {
 }
 
 void StencilModel::set_overlap_mode(int mode) {
-  STENCIL_REQUIRE(mode >= 0 && mode <= 2, "overlap mode " << mode);
+  STENCIL_REQUIRE(mode >= 0 && mode <= 3, "overlap mode " << mode);
+  STENCIL_REQUIRE(mode != 3 || pipeOk_, "overlap mode 3 (pipelined pairs) is not possible for this model");
   if (mode == overlap_mode()) return;
   set_overlap(mode != 0);
   slabsAfter_ = mode == 2;
+  pipelined_ = mode == 3;
 }
 
 void StencilModel::set_comm_reserve(int cus) {

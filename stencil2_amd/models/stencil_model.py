@@ -97,8 +97,13 @@ class StencilModel:
 
     def set_overlap_mode(self, mode: int):
         """0 = whole-region pairs; 1 = overlapped, slabs on the comm stream beside the interior sweep; 2 = overlapped,
-        slabs after the interior sweep on the compute stream."""
+        slabs after the interior sweep on the compute stream; 3 = pipelined (can_pipeline()): whole-region sweeps that
+        publish their boundary z planes, the next pair's exchange gated on them runs beside the rest of the sweep."""
         self._m.set_overlap_mode(int(mode))
+
+    def can_pipeline(self) -> bool:
+        """Overlap mode 3 is possible: one device, remote halos along z only, whole-row kernel, fused IPC stores."""
+        return self._m.can_pipeline()
 
     def overlap_mode(self) -> int:
         return self._m.overlap_mode()
