@@ -132,9 +132,11 @@ def main():
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU, and then "
                          "overlapped or whole-region pairs, whichever runs faster in the warm-up)")
-    ap.add_argument("--colo-copy", choices=["auto", "store", "engine"], default="auto",
-                    help="co-located (HIP IPC) halos: the pack kernel stores into the peer's inbox (store), or a DMA "
-                         "engine copies the packed message (engine); auto: both tried in the warm-up")
+    ap.add_argument("--colo-copy", choices=["auto", "store", "engine"], default="store",
+                    help="co-located (HIP IPC) halos: the pack kernel stores into the peer's inbox (store, default), or "
+                         "a DMA engine copies the packed message (engine); auto: both tried in the warm-up. Engine "
+                         "copies never won on one MI355X and, with 4 ranks sharing it, ran at 0.6-1.7 s per step and "
+                         "left the store path 3.5x slower afterwards (profiles/r3/check4), so they are opt-in")
     ap.add_argument("--inbox", choices=["uncached", "fine", "coarse"], default="uncached",
                     help="memory of the co-located receive slots (TransportOptions.inbox)")
     ap.add_argument("--completion", choices=["kernel", "streamop"], default="kernel",
