@@ -312,7 +312,13 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
 // (x = nx-1, lane Lr, element kr of chunk H-1) with v_readlane and selects them in: left of x = 0 on lane 0, right of
 // x = nx-1 on lane Lr. Chunks wholly past the row end load the row start (finite values, never selected) and store
 // nothing; the partial chunk stores its cells one by one.
-template <int NW, int PF, int KIND, int H = 2, bool RAG = false>
+//
+// Tail rows (TL: 256 H < nx <= 256 H + 64, e.g. the 4-GPU ladder's 813): H = 3 whole chunks per lane and one more
+// cell per lane after them (x = 768 + lane, lanes < nx - 768), so a row of up to 832 cells still fits one wave at
+// 98 % lane use for 813 (four chunks per lane need 196 KiB of LDS and spill). The tail's x-neighbours are lane
+// rotates of the tail (lane 0's left is chunk H-1 of lane 63, the right of chunk H-1 on lane 63 is lane 0's tail);
+// the row ends wrap through the broadcast first cell and last tail cell. +12 KiB of LDS for the tail rows.
+template <int NW, int PF, int KIND, int H = 2, bool RAG = false, bool TL = false>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x2_row_kernel(StencilArgs<float> a) {
   using T = float;
@@ -322,9 +328,12 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   constexpr int YO = NW - 4;
   constexpr int NC = 3 + PF;
   static_assert(NW == 12 && H <= 3, "3 waves per SIMD: the 168-VGPR budget; 144 KiB of LDS at H = 3");
-  static_assert(RAG || H == 2, "unragged rows: 512 cells");
+  static_assert(RAG || TL || H == 2, "unragged rows: 512 cells");
+  static_assert(!(RAG && TL), "ragged last chunk or a tail, not both");
   __shared__ NV cs[2][NW][H][64]; // src rows (plane z+2dz at publish)
   __shared__ NV us[2][NW][H][64]; // u1 rows (plane z+dz at publish)
+  __shared__ T cst[TL ? 2 : 1][TL ? NW : 1][TL ? 64 : 1]; // tail cells of the src / u1 rows (TL)
+  __shared__ T ust[TL ? 2 : 1][TL ? NW : 1][TL ? 64 : 1];
 
   const uint32_t nb = gridDim.x;
   const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
@@ -390,6 +399,11 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   auto choff = [&](int h) -> int { // byte offset of chunk h from the lane's first chunk
     return (h < H - 1 || lastIn) ? h * HS * int(sizeof(T)) : 0;
   };
+  // tail rows: cell x = 256 H + lane on lanes < ntl (the others read the row start: finite, never stored)
+  const int ntl = TL ? a.hix - a.lox - HS * H : 0;
+  const int Lt = ntl - 1;
+  const bool tailIn = lane < ntl;
+  const int toff = (tailIn ? HS * H - (V - 1) * lane : -V * lane) * int(sizeof(T)); // from the lane's chunk 0
 
   const int yw = (a.wrapm & 2) ? (y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y)) : y;
   const int yc = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
@@ -421,24 +435,32 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
     return hot ? T(1) : (cold ? T(0) : v);
   };
   // S of the wave's row (both chunks), x-neighbours by lane rotates
+  // the tail arguments (cmt .. zmt, ot) are the same terms for the tail cell of each row (TL only)
   auto apply_row = [&](const NV (&cm)[H], const NV (&up)[H], const NV (&dn)[H], const NV (&zp)[H], const NV (&zm)[H],
-                       const RowSph &rs, NV (&o)[H]) {
+                       const RowSph &rs, NV (&o)[H], T cmt, T upt, T dnt, T zpt, T zmt, T &ot) {
     T r3[H], l0[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       r3[h] = rot_prev(cm[h][V - 1]);
       l0[h] = rot_next(cm[h][0]);
     }
-    T first = 0, last = 0; // ragged rows: the cells x = 0 and x = nx-1, broadcast
+    T first = 0, last = 0; // ragged / tail rows: the cells x = 0 and x = nx-1, broadcast
     if constexpr (RAG) {
       first = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cm[0][0]), 0));
       const T e = kr == 0 ? cm[H - 1][0] : (kr == 1 ? cm[H - 1][1] : (kr == 2 ? cm[H - 1][2] : cm[H - 1][3]));
       last = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), Lr));
     }
+    T tp = 0, tn = 0; // tail of lane-1 / lane+1
+    if constexpr (TL) {
+      first = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cm[0][0]), 0));
+      last = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cmt), Lt));
+      tp = rot_prev(cmt);
+      tn = rot_next(cmt);
+    }
 #pragma unroll
     for (int h = 0; h < H; ++h) {
-      const T left = lane0 ? (RAG && h == 0 ? last : r3[(h + H - 1) % H]) : r3[h];
-      const T right = lane63 ? l0[(h + 1) % H] : l0[h];
+      const T left = lane0 ? ((RAG || TL) && h == 0 ? last : r3[(h + H - 1) % H]) : r3[h];
+      const T right = lane63 ? (TL && h == H - 1 ? tn : l0[(h + 1) % H]) : l0[h];
       NV vpx, vmx;
 #pragma unroll
       for (int k = 0; k < V; ++k) {
@@ -451,11 +473,22 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
       }
       o[h] = div6v<T, NV, V>(sum6v<T, KIND>(vpx, vmx, dn[h], up[h], zp[h], zm[h]));
     }
+    if constexpr (TL) {
+      const T lt = lane0 ? r3[H - 1] : tp;  // lane 0: chunk H-1's last cell on lane 63
+      const T rt = lane == Lt ? first : tn; // the last cell of the row wraps to x = 0
+      const T s = sum6v<T, KIND>(rt, lt, dnt, upt, zpt, zmt);
+      const T c = T(1) / T(6); // exact /6 as div6v, element-wise
+      const T q0 = s * c;
+      T q = __builtin_fmaf(__builtin_fmaf(-q0, T(6), s), c, q0);
+      if (__builtin_expect(__builtin_fabsf(s) < 0x1p-100f, 0) && s != T(0)) q = s / T(6);
+      ot = q;
+    }
     if (KIND == 0 && rs.hit) {
 #pragma unroll
       for (int h = 0; h < H; ++h)
 #pragma unroll
         for (int k = 0; k < V; ++k) o[h][k] = fix(rs, xb + h * HS + k, o[h][k]);
+      if constexpr (TL) ot = fix(rs, a.lox + HS * H + lane, ot);
     }
   };
 
@@ -465,10 +498,12 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
     const int z0 = DOWN ? ze - 1 : zs;
     NV C[NC][H];
     NV Ub[H], Uc[H], Ua[H];
+    T Ct[NC] = {}, Ubt = 0, Uct = 0, Uat = 0; // tail cells (TL)
     auto load_row = [&](int zz, int k) {
       const char *b = planep(zz) + rowoff;
 #pragma unroll
       for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + choff(h));
+      if constexpr (TL) Ct[k] = *reinterpret_cast<const T *>(b + toff);
     };
     {
       const int zw = z0 - 2 * dz;
@@ -476,6 +511,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
       for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, k);
 #pragma unroll
       for (int h = 0; h < H; ++h) cs[0][w][h][lane] = C[1][h];
+      if constexpr (TL) cst[0][w][lane] = Ct[1];
       __syncthreads();
     }
     int buf = 0;
@@ -494,19 +530,28 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
           cA[h] = cs[buf][wA][h][lane];
           cB[h] = cs[buf][wB][h][lane];
         }
-        apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], row_sph(P), Ua);
+        const T cAt = TL ? cst[buf][wA][TL ? lane : 0] : T(0), cBt = TL ? cst[buf][wB][TL ? lane : 0] : T(0);
+        apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], row_sph(P), Ua, Ct[s1], cAt, cBt,
+                  DOWN ? Ct[s0] : Ct[s2], DOWN ? Ct[s2] : Ct[s0], Uat);
       } else {
 #pragma unroll
         for (int h = 0; h < H; ++h) Ua[h] = C[s1][h]; // never read: the edge waves' u1 feeds no output row
+        Uat = Ct[s1];
       }
       if (t >= 0 && needU2) {
         NV uA[H], uB[H], o[H];
+        T ot = 0;
 #pragma unroll
         for (int h = 0; h < H; ++h) {
           uA[h] = us[buf][wA][h][lane];
           uB[h] = us[buf][wB][h][lane];
         }
-        apply_row(Uc, uA, uB, DOWN ? Ub : Ua, DOWN ? Ua : Ub, row_sph(z), o);
+        const T uAt = TL ? ust[buf][wA][TL ? lane : 0] : T(0), uBt = TL ? ust[buf][wB][TL ? lane : 0] : T(0);
+        apply_row(Uc, uA, uB, DOWN ? Ub : Ua, DOWN ? Ua : Ub, row_sph(z), o, Uct, uAt, uBt, DOWN ? Ubt : Uat,
+                  DOWN ? Uat : Ubt, ot);
+        if constexpr (TL)
+          if (outRow && tailIn)
+            *reinterpret_cast<T *>(reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff + toff) = ot;
         if (outRow) {
           char *dp = reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff;
 #pragma unroll
@@ -533,6 +578,10 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
         cs[nbuf][w][h][lane] = C[s2][h];
         if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
       }
+      if constexpr (TL) {
+        cst[nbuf][w][lane] = Ct[s2];
+        if (needU1) ust[nbuf][w][lane] = Uat;
+      }
       // boundary-plane publication (block-uniform): every wave's stores of plane z complete before the barrier,
       // then one thread writes the XCD's L2 back (system-scope release) and counts the block's cells of the plane
       const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
@@ -550,6 +599,8 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
         Ub[h] = Uc[h];
         Uc[h] = Ua[h];
       }
+      Ubt = Uct;
+      Uct = Uat;
       ++t;
       return true;
     };
@@ -1017,9 +1068,9 @@ int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi, int x2row) {
   if (!stencil7x2_supported(dom, qi)) return 0;
   const int64_t es = dom.elem_size(qi), V = 16 / es;
   const int64_t lox = dom.radius().x(-1), nx = dom.size().x, px = dom.pitch(qi).x, pad = dom.pad_x(qi);
-  // ragged fp32 rows of 257-768 cells: the whole-row kernel wraps x by broadcasting the row-end cells (its last
-  // chunk reads at most 3 cells past the row end, inside the padded row)
-  const bool rowX = x2row != 0 && es == 4 && nx > 256 && nx <= 768 && lox + (nx + V - 1) / V * V < px - pad;
+  // ragged fp32 rows of 257-832 cells: the whole-row kernel wraps x by broadcasting the row-end cells (a ragged last
+  // chunk reads at most 3 cells past the row end, inside the padded row; rows of 769-832 end in per-lane tail cells)
+  const bool rowX = x2row != 0 && es == 4 && nx > 256 && nx <= 832 && lox + (nx + V - 1) / V * V < px - pad;
   if (rowX && nx % V != 0) return 1 | (dom.size().y >= 2 ? 2 : 0) | (dom.size().z >= 2 ? 4 : 0);
   // x: whole chunks only (the chunk grid starts at the 16-B aligned lox), at least two, and the last chunk not on
   // lane 0 of its column (a wrap lane shifts both of its edge pairs: its other edge must be the unused one, never a
@@ -1095,14 +1146,14 @@ static void apply_x2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
 
 // whole-row kernel: fp32, x wrapped in-kernel, rows starting on a 16-B chunk; H chunks per lane (RAG: rows shorter
 // than 256 H cells)
-template <int KIND, int PF, int H = 2, bool RAG = false, int NW = 12>
+template <int KIND, int PF, int H = 2, bool RAG = false, int NW = 12, bool TL = false>
 static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
                           const StencilTune &tune) {
   constexpr int YO = NW - 4;
   StencilArgs<float> a = make_args<float>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   const int rxm = int(dom.radius().x(-1));
   const int nx = a.hix - a.lox;
-  const bool fitsH = RAG ? (nx > 256 * (H - 1) && nx <= 256 * H) : nx == 512;
+  const bool fitsH = TL ? (nx > 256 * H && nx <= 256 * H + 64) : (RAG ? (nx > 256 * (H - 1) && nx <= 256 * H) : nx == 512);
   if (!(tune.wrap & 1) || !fitsH || (a.lox - rxm) % 4 != 0) return false;
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
@@ -1118,7 +1169,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   }
   a.gx = 1;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = (const void *)stencil7x2_row_kernel<NW, PF, KIND, H, RAG>;
+  const void *kern = (const void *)stencil7x2_row_kernel<NW, PF, KIND, H, RAG, TL>;
   const int64_t cols = a.gy;
   const int64_t resident = x2_resident_blocks(kern, 64 * NW);
   uint32_t blocks;
@@ -1147,7 +1198,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     blocks = uint32_t(cols * a.gz);
   }
   dom.set_device();
-  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG, TL>), dim3(blocks), dim3(64, NW), 0, stream, a);
   HIP_CHECK(hipGetLastError());
   return true;
 }
@@ -1209,7 +1260,7 @@ bool stencil7x2_row_kernel_used(const LocalDomain &dom, int64_t qi, const Rect3 
     return false;
   const Rect3 rr(region.lo - dom.accessor_origin(), region.hi - dom.accessor_origin());
   const int64_t nx = rr.hi.x - rr.lo.x;
-  return (nx == 512 || (nx > 256 && nx <= 768)) && (rr.lo.x - dom.radius().x(-1)) % 4 == 0;
+  return (nx == 512 || (nx > 256 && nx <= 832)) && (rr.lo.x - dom.radius().x(-1)) % 4 == 0;
 }
 
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
@@ -1249,6 +1300,12 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
       else
         done = jac ? apply_x2row_t<0, 1, 3, true>(dom, qi, region, sph, stream, tune)
                    : apply_x2row_t<1, 1, 3, true>(dom, qi, region, sph, stream, tune);
+      if (done) return;
+    }
+    // rows of 769-832 cells (the 4-GPU ladder's 813): three chunks per lane plus one tail cell per lane
+    if ((tune.wrap & 1) && nx > 768 && nx <= 832) {
+      done = jac ? apply_x2row_t<0, 1, 3, false, 12, true>(dom, qi, region, sph, stream, tune)
+                 : apply_x2row_t<1, 1, 3, false, 12, true>(dom, qi, region, sph, stream, tune);
       if (done) return;
     }
     STENCIL_REQUIRE(!tune.publish, "boundary-plane publication needs the whole-row kernel");

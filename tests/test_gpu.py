@@ -226,10 +226,14 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
     # ragged periodic rows: 2 / 3 / 4 chunks per lane, the row-end cells broadcast for the wrap
     ("astaroth", (645, 20, 24), [0], 1, 1), ("astaroth", (301, 24, 20), [0], 1, 1), ("astaroth", (300, 20, 16), [0], 1, 1),
     ("astaroth", (768, 12, 16), [0], 1, 1), ("astaroth", (646, 520, 12), [0, 0], 1, 1), ("jacobi", (645, 136, 136), [0], 1, 1),
+    # tail rows: 3 chunks + one cell per lane (769-832 cells; the 4-GPU ladder's 813)
+    ("astaroth", (813, 20, 24), [0], 1, 1), ("astaroth", (769, 12, 16), [0], 1, 1), ("astaroth", (832, 12, 16), [0], 1, 1),
+    ("astaroth", (800, 264, 12), [0, 0], 1, 1), ("jacobi", (813, 168, 176), [0], 1, 1), ("jacobi", (813, 176, 264), [0, 0], 1, 1),
 ])
 def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf, row):
-    """Fused pairs on periodic rows of 257-768 cells take the whole-row kernel (one wave per row, x-neighbours by
-    lane rotates, StencilTune.x2row; ragged rows broadcast their end cells): bitwise equal to single steps, with the
+    """Fused pairs on periodic rows of 257-832 cells take the whole-row kernel (one wave per row, x-neighbours by
+    lane rotates, StencilTune.x2row; ragged rows broadcast their end cells, rows of 769-832 add one tail cell per
+    lane): bitwise equal to single steps, with the
     hot/cold spheres (Jacobi) inside the grid, and to the column kernel (x2row = 0, which copies ragged x halos)."""
     from stencil2_amd.ops import astaroth_step_reference
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
