@@ -338,7 +338,9 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   const uint32_t nb = gridDim.x;
   const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
   const int lane = threadIdx.x;
-  const int w = int(threadIdx.y);
+  // three-chunk rows (H = 3, ragged or with tail cells) are at the 168-VGPR budget: the wave index (and with it the
+  // row and its sphere bounds below) is made explicitly wave-uniform, so those live in SGPRs
+  const int w = H == 3 ? __builtin_amdgcn_readfirstlane(int(threadIdx.y)) : int(threadIdx.y);
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
   uint32_t s, e, s2 = 0, e2 = 0;
   int qodd = -1; // lockstep quarter-major: z direction by quarter parity
@@ -419,19 +421,43 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   struct RowSph {
     int dh, dc;
     bool hit;
+    int hlo, hhi, clo, chi; // H = 3: the row's hot / cold cells are hlo <= x <= hhi / clo <= x <= chi (wave-uniform)
+  };
+  // largest s >= 0 with s * s < d (d > 0), exact: float estimate, then integer correction
+  auto isqrt_below = [](int d) -> int {
+    int s = int(__builtin_sqrtf(float(d - 1)));
+    while (s > 0 && s * s > d - 1) --s;
+    while ((s + 1) * (s + 1) <= d - 1) ++s;
+    return s;
   };
   auto row_sph = [&](int P) -> RowSph {
-    RowSph r{0, 0, false};
+    RowSph r{0, 0, false, 0, 0, 0, 0};
     if (KIND == 0 && a.r1sq > 0) {
       r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
       r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
       r.hit = r.dh < a.r1sq || r.dc < a.r1sq;
+      if constexpr (H == 3) {
+        // (x - hx)^2 + dh < r1sq  <=>  |x - hx| <= s with s * s < r1sq - dh: bounds instead of per-cell squares
+        constexpr int kNone = -(1 << 24); // empty interval: never matches a cell coordinate
+        const int sh = r.dh < a.r1sq ? isqrt_below(a.r1sq - r.dh) : -1;
+        const int sc = r.dc < a.r1sq ? isqrt_below(a.r1sq - r.dc) : -1;
+        r.hlo = __builtin_amdgcn_readfirstlane(sh >= 0 ? a.hx - sh : kNone);
+        r.hhi = __builtin_amdgcn_readfirstlane(sh >= 0 ? a.hx + sh : kNone);
+        r.clo = __builtin_amdgcn_readfirstlane(sc >= 0 ? a.cx - sc : kNone);
+        r.chi = __builtin_amdgcn_readfirstlane(sc >= 0 ? a.cx + sc : kNone);
+      }
     }
     return r;
   };
   auto fix = [&](const RowSph &rs, int x, T v) -> T {
-    const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
-    const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+    bool hot, cold;
+    if constexpr (H == 3) {
+      hot = unsigned(x - rs.hlo) <= unsigned(rs.hhi - rs.hlo);
+      cold = unsigned(x - rs.clo) <= unsigned(rs.chi - rs.clo);
+    } else {
+      hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
+      cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+    }
     return hot ? T(1) : (cold ? T(0) : v);
   };
   // S of the wave's row (both chunks), x-neighbours by lane rotates
