@@ -228,7 +228,7 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
     ("astaroth", (768, 12, 16), [0], 1, 1), ("astaroth", (646, 520, 12), [0, 0], 1, 1), ("jacobi", (645, 136, 136), [0], 1, 1),
     # tail rows: 3 chunks + one cell per lane (769-832 cells; the 4-GPU ladder's 813)
     ("astaroth", (813, 20, 24), [0], 1, 1), ("astaroth", (769, 12, 16), [0], 1, 1), ("astaroth", (832, 12, 16), [0], 1, 1),
-    ("astaroth", (800, 520, 12), [0, 0], 1, 1), ("jacobi", (813, 168, 176), [0], 1, 1), ("jacobi", (813, 432, 24), [0, 0], 1, 1),
+    ("astaroth", (800, 520, 12), [0, 0], 1, 1), ("jacobi", (813, 168, 176), [0], 1, 1), ("jacobi", (813, 432, 176), [0, 0], 1, 1),
 ])
 def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf, row):
     """Fused pairs on periodic rows of 257-832 cells take the whole-row kernel (one wave per row, x-neighbours by
