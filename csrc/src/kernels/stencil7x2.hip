@@ -338,9 +338,11 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   const uint32_t nb = gridDim.x;
   const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
   const int lane = threadIdx.x;
-  // three-chunk rows (H = 3, ragged or with tail cells) are at the 168-VGPR budget: the wave index (and with it the
-  // row and its sphere bounds below) is made explicitly wave-uniform, so those live in SGPRs
-  const int w = H == 3 ? __builtin_amdgcn_readfirstlane(int(threadIdx.y)) : int(threadIdx.y);
+  // tail rows (three chunks plus a tail cell per lane) are over the 168-VGPR budget with per-cell sphere tests (192,
+  // 24 spilled): their wave index, row and per-row sphere x bounds are made wave-uniform (SGPRs; 165, no scratch).
+  // Ragged three-chunk rows keep the per-cell test: with the bounds they ran 10 % slower (645x645x323 867-891 vs
+  // 972 Gcells/s, same box; the 512-cell kernel with bounds 1047-1052 vs 1142-1157; profiles/r3/s3/ab_sphere.txt)
+  const int w = TL ? __builtin_amdgcn_readfirstlane(int(threadIdx.y)) : int(threadIdx.y);
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
   uint32_t s, e, s2 = 0, e2 = 0;
   int qodd = -1; // lockstep quarter-major: z direction by quarter parity
@@ -421,7 +423,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   struct RowSph {
     int dh, dc;
     bool hit;
-    int hlo, hhi, clo, chi; // H = 3: the row's hot / cold cells are hlo <= x <= hhi / clo <= x <= chi (wave-uniform)
+    int hlo, hhi, clo, chi; // TL: the row's hot / cold cells are hlo <= x <= hhi / clo <= x <= chi (wave-uniform)
   };
   // largest s >= 0 with s * s < d (d > 0), exact: float estimate, then integer correction
   auto isqrt_below = [](int d) -> int {
@@ -436,7 +438,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
       r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
       r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
       r.hit = r.dh < a.r1sq || r.dc < a.r1sq;
-      if constexpr (H == 3) {
+      if constexpr (TL) {
         // (x - hx)^2 + dh < r1sq  <=>  |x - hx| <= s with s * s < r1sq - dh: bounds instead of per-cell squares
         constexpr int kNone = -(1 << 24); // empty interval: never matches a cell coordinate
         const int sh = r.dh < a.r1sq ? isqrt_below(a.r1sq - r.dh) : -1;
@@ -451,7 +453,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   };
   auto fix = [&](const RowSph &rs, int x, T v) -> T {
     bool hot, cold;
-    if constexpr (H == 3) {
+    if constexpr (TL) {
       hot = unsigned(x - rs.hlo) <= unsigned(rs.hhi - rs.hlo);
       cold = unsigned(x - rs.clo) <= unsigned(rs.chi - rs.clo);
     } else {
