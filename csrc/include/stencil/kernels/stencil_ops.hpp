@@ -160,6 +160,27 @@ void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vec
 // the sweep kernel (6 waves per block for 2-row slabs), thin x slabs by a lanes-on-rows kernel
 void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &interior, StencilKind kind,
                                const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());
+// Lockstep block schedule of the whole-row fused pair: `slots` resident blocks, `cols` row groups (8 output rows
+// each), `nz` planes. P blocks per row group march P z parts side by side (y-adjacent blocks on one XCD, so their
+// shared y-halo rows meet in L2): quarters (P = 4) over the first slots / 4 row groups with the rest as short
+// second segments, or P = slots / cols over every row group when that fills 15 / 16 of the slots (or the grid has
+// fewer than slots / 4 row groups). parts == 0: no lockstep (parts under 16 planes, or nz < 64): balanced split.
+struct X2Schedule {
+  int parts = 0;
+  int64_t blocks = 0;
+};
+inline X2Schedule x2_lockstep_schedule(int64_t slots, int64_t cols, int64_t nz) {
+  X2Schedule r;
+  if (slots < 4 || cols < 1) return r;
+  int64_t P = slots / 4 <= cols ? 4 : slots / cols;
+  if (P == 4 && cols > slots / 4 && slots / cols >= 1 && 16 * (slots / cols) * cols >= 15 * slots) P = slots / cols;
+  const int64_t cm = cols < slots / P ? cols : slots / P;
+  if (cm < 1 || nz < 64 || nz / P < 16) return r;
+  r.parts = int(P);
+  r.blocks = P * cm;
+  return r;
+}
+
 // axes (mask as StencilTune::wrap) stencil7_apply can wrap in-kernel for this quantity's layout: with tune.wrap set
 // the single step reads the periodic image along those axes instead of the halo (the region must span them)
 int stencil7_wrappable_axes(const LocalDomain &dom, int64_t qi);

@@ -644,6 +644,14 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("dd"), py::arg("domain"), py::arg("qi"), py::arg("region"), py::arg("kind"), py::arg("spheres"),
         py::arg("stream") = 0);
+  m.def(
+      "x2_lockstep_schedule",
+      [](int64_t slots, int64_t cols, int64_t nz) {
+        const X2Schedule r = x2_lockstep_schedule(slots, cols, nz);
+        return py::make_tuple(r.parts, r.blocks);
+      },
+      py::arg("slots"), py::arg("cols"), py::arg("nz"),
+      "lockstep schedule of the whole-row fused pair: (z parts per row group, blocks); (0, 0) = balanced split");
   m.def("jacobi_spheres", [](const Rect3 &cReg) {
     Spheres s = Spheres::jacobi(cReg);
     return py::make_tuple(s.hot, s.cold, s.radius);

@@ -347,15 +347,17 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   uint32_t s, e, s2 = 0, e2 = 0;
   int qodd = -1; // lockstep quarter-major: z direction by quarter parity
   if (a.seg == 2) {
-    // lockstep: four blocks per column (quarters of the z range) for the first nb/4 columns, so y-adjacent blocks
-    // (4 apart, one XCD after the remap) march the same planes together and their shared y-halo rows meet in L2;
-    // the columns left over (grids of fewer than 4 x columns blocks) spread over all blocks as short second segments
-    const uint32_t cm = nb / 4;
-    // quarter-major: consecutive blocks (one XCD after the remap) take y-adjacent columns of one quarter, so an
-    // XCD's blocks share every interior y-halo row through its L2 (column-major: 1146 vs 1164 Gcells/s, r2s3)
+    // lockstep: P = a.zparts blocks per column (parts of the z range; quarters unless the grid has fewer than
+    // nb/4 columns) for the first nb/P columns, so y-adjacent blocks march the same planes together and their shared
+    // y-halo rows meet in L2; the columns left over (grids of fewer than P x columns blocks) spread over all blocks
+    // as short second segments
+    const uint32_t P = uint32_t(a.zparts);
+    const uint32_t cm = nb / P;
+    // part-major: consecutive blocks (one XCD after the remap) take y-adjacent columns of one part, so an XCD's
+    // blocks share every interior y-halo row through its L2 (column-major: 1146 vs 1164 Gcells/s, r2s3)
     const uint32_t qq = lb / cm, col = lb % cm;
-    s = col * nzt + qq * nzt / 4;
-    e = col * nzt + (qq + 1) * nzt / 4;
+    s = col * nzt + qq * nzt / P;
+    e = col * nzt + (qq + 1) * nzt / P;
     qodd = int(qq & 1);
     const uint64_t LW = uint64_t(uint32_t(a.gy) - cm) * nzt;
     s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
@@ -1210,13 +1212,14 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
     const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
     blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 16)));
-    // lockstep quarters (a.seg = 2) when the resident blocks cover at most four per column and the quarters stay
-    // long: with 8 CUs left to the transports (248 blocks) the balanced split puts y-adjacent blocks 16 planes apart
-    // and their halo rows miss L2 (512^3 local interior: 276 vs 237 us at 256 blocks)
-    const int64_t q4 = slots / 4 * 4;
-    if (tune.x2lockstep && q4 >= 4 && q4 / 4 <= cols && nz >= 64) {
+    // lockstep parts (a.seg = 2, x2_lockstep_schedule): with 8 CUs left to the transports (248 blocks) the balanced
+    // split puts y-adjacent blocks 16 planes apart and their halo rows miss L2 (512^3 local interior: 276 vs 237 us
+    // at 256 blocks); 813x407x407 (51 row groups) runs 5 parts on 255 blocks, 645x645x323 (81) 3 parts on 243
+    const X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
+    if (tune.x2lockstep && ls.parts > 0) {
       a.seg = 2;
-      blocks = uint32_t(q4);
+      a.zparts = ls.parts;
+      blocks = uint32_t(ls.blocks);
     }
   } else {
     int zc = tune.zchunk;

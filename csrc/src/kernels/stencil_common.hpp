@@ -48,6 +48,7 @@ template <typename T> struct StencilArgs {
   int zc;                           // planes per block
   int gx, gy, gz;                   // logical grid
   int seg;                          // stencil7x2: 1 = balanced (column, plane) segments over gridDim.x blocks, 2 = lockstep quarters
+  int zparts;                       // stencil7x2 lockstep (seg = 2): z parts per column (4 = quarters)
   int xfast;                        // stencil7x2: 1 = column index x-major (x-adjacent columns on one XCD)
   int remap;                        // stencil7x2: 1 = XCD-aware block remap
   // spheres, raw coordinates

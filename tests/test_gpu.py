@@ -513,6 +513,24 @@ def test_temporal2_row_kernel_lockstep_quarters(st, fake, reserve, lockstep, alt
     assert torch.equal(_gather(m), u)
 
 
+@pytest.mark.parametrize("size", [(512, 320, 112), (645, 200, 160), (813, 136, 256)])
+def test_temporal2_row_kernel_lockstep_parts(st, size):
+    """Grids of fewer row groups than resident blocks / 4 run lockstep with P = blocks / columns z parts per column
+    (40 columns: P = 6 over 240 blocks; 25 ragged 645-cell columns: P = 10; 17 tail-row columns: P = 15 over 255):
+    bitwise equal to single steps."""
+    from stencil2_amd.ops import astaroth_step_reference
+    m = st.AstarothSim(size, quantities=1, gpus=[0], temporal=2, axis_cost=(64, 3, 2))
+    m.init()
+    assert m.temporal_blocking()
+    u = _gather(m)
+    for n in (2, 6):
+        m.run(n)
+        for _ in range(n):
+            u = astaroth_step_reference(u)
+        m.synchronize()
+        assert torch.equal(_gather(m), u), f"after run({n})"
+
+
 @pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy", "PeerCopyEngine"])
 def test_jacobi_temporal2_transports(st, methods):
     """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs (PeerCopyEngine: the
