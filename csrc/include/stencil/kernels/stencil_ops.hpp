@@ -163,8 +163,11 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
 // Lockstep block schedule of the whole-row fused pair: `slots` resident blocks, `cols` row groups (8 output rows
 // each), `nz` planes. P blocks per row group march P z parts side by side (y-adjacent blocks on one XCD, so their
 // shared y-halo rows meet in L2): quarters (P = 4) over the first slots / 4 row groups with the rest as short
-// second segments, or P = slots / cols over every row group when that fills 15 / 16 of the slots (or the grid has
-// fewer than slots / 4 row groups). parts == 0: no lockstep (parts under 16 planes, or nz < 64): balanced split.
+// second segments, or P = slots / cols over every row group when the grid has fewer than slots / 4 row groups
+// (813x407x407: 51 groups, 5 parts, 847 -> 910-917 Gcells/s; 645x323x645: 41 groups, 6 parts, 847 -> 1067-1072).
+// Whole columns over fewer slots instead of quarters plus leftovers lose (645x645x323, 81 groups: 3 parts on 243
+// blocks 930-946 vs 994-1001; profiles/r3/s3/ab_lockstep_parts.txt). parts == 0: no lockstep (parts under 16
+// planes, or nz < 64): balanced split.
 struct X2Schedule {
   int parts = 0;
   int64_t blocks = 0;
@@ -172,8 +175,7 @@ struct X2Schedule {
 inline X2Schedule x2_lockstep_schedule(int64_t slots, int64_t cols, int64_t nz) {
   X2Schedule r;
   if (slots < 4 || cols < 1) return r;
-  int64_t P = slots / 4 <= cols ? 4 : slots / cols;
-  if (P == 4 && cols > slots / 4 && slots / cols >= 1 && 16 * (slots / cols) * cols >= 15 * slots) P = slots / cols;
+  const int64_t P = slots / 4 <= cols ? 4 : slots / cols;
   const int64_t cm = cols < slots / P ? cols : slots / P;
   if (cm < 1 || nz < 64 || nz / P < 16) return r;
   r.parts = int(P);

@@ -1214,7 +1214,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 16)));
     // lockstep parts (a.seg = 2, x2_lockstep_schedule): with 8 CUs left to the transports (248 blocks) the balanced
     // split puts y-adjacent blocks 16 planes apart and their halo rows miss L2 (512^3 local interior: 276 vs 237 us
-    // at 256 blocks); 813x407x407 (51 row groups) runs 5 parts on 255 blocks, 645x645x323 (81) 3 parts on 243
+    // at 256 blocks); 813x407x407 (51 row groups) runs 5 parts on 255 blocks
     const X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
     if (tune.x2lockstep && ls.parts > 0) {
       a.seg = 2;

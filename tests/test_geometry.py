@@ -96,13 +96,13 @@ def test_padded_pitch_alignment(st):
 
 def test_x2_lockstep_schedule(st):
     """whole-row fused-pair block schedule: quarters over 64 row groups of 512^3, quarters plus second segments when
-    fewer slots (the overlap's 248), P = slots / groups parts over every row group for the cbrt ladder's shapes"""
+    more row groups than slots / 4 (the overlap's 248 slots, 645x645x323), P = slots / groups parts over every row
+    group when fewer (813x407x407, 645x323x645)"""
     f = st._C.x2_lockstep_schedule
     assert f(256, 64, 512) == (4, 256)     # 512^3: 64 row groups of 8, quarters
     assert f(248, 64, 508) == (4, 248)     # overlap interior: 62 groups in lockstep, 2 as second segments
     assert f(256, 51, 407) == (5, 255)     # 813x407x407: 51 groups x 5 parts of 81-82 planes
-    assert f(256, 81, 323) == (3, 243)     # 645x645x323: 81 groups x 3 parts (243 >= 15/16 of 256)
-    assert f(256, 70, 512) == (4, 256)     # 70 groups: 3 parts would leave 46 slots idle -> quarters + leftovers
+    assert f(256, 81, 323) == (4, 256)     # 645x645x323: quarters over 64 groups + 17 as second segments
     assert f(256, 41, 645) == (6, 246)     # 645x323x645
     assert f(256, 64, 40) == (0, 0)        # thin grids: balanced split
     assert f(256, 17, 200) == (0, 0)       # 15 parts of 13 planes: too short
