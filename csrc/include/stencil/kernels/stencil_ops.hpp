@@ -160,10 +160,11 @@ void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vec
 // the sweep kernel (6 waves per block for 2-row slabs), thin x slabs by a lanes-on-rows kernel
 void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &interior, StencilKind kind,
                                const Spheres &sph, hipStream_t stream, const StencilTune &tune = StencilTune());
-// Lockstep block schedule of the whole-row fused pair: `slots` resident blocks, `cols` row groups (8 output rows
-// each), `nz` planes. P blocks per row group march P z parts side by side (y-adjacent blocks on one XCD, so their
+// Lockstep block schedule of the whole-row / 512-cell-column fused pairs: `slots` resident blocks, `cols` row
+// groups (8 output rows of one column strip each), `nz` planes. P blocks per row group march P z parts side by side (y-adjacent blocks on one XCD, so their
 // shared y-halo rows meet in L2): quarters (P = 4) over the first slots / 4 row groups with the rest as short
-// second segments, or P = slots / cols over every row group when the grid has fewer than slots / 4 row groups
+// second segments, or P = slots / cols over every row group when the grid has fewer than slots / 4 row groups or
+// the row groups divide the slots evenly
 // (813x407x407: 51 groups, 5 parts, 847 -> 910-917 Gcells/s; 645x323x645: 41 groups, 6 parts, 847 -> 1067-1072).
 // Whole columns over fewer slots instead of quarters plus leftovers lose (645x645x323, 81 groups: 3 parts on 243
 // blocks 930-946 vs 994-1001; profiles/r3/s3/ab_lockstep_parts.txt). parts == 0: no lockstep (parts under 16
@@ -175,7 +176,8 @@ struct X2Schedule {
 inline X2Schedule x2_lockstep_schedule(int64_t slots, int64_t cols, int64_t nz) {
   X2Schedule r;
   if (slots < 4 || cols < 1) return r;
-  const int64_t P = slots / 4 <= cols ? 4 : slots / cols;
+  // whole columns when they divide the slots evenly (1024x512x256 on the 512-cell column kernel: 128 columns, P = 2)
+  const int64_t P = (slots / 4 > cols || slots % cols == 0) ? slots / cols : 4;
   const int64_t cm = cols < slots / P ? cols : slots / P;
   if (cm < 1 || nz < 64 || nz / P < 16) return r;
   r.parts = int(P);

@@ -318,6 +318,44 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
 // 98 % lane use for 813 (four chunks per lane need 196 KiB of LDS and spill). The tail's x-neighbours are lane
 // rotates of the tail (lane 0's left is chunk H-1 of lane 63, the right of chunk H-1 on lane 63 is lane 0's tail);
 // the row ends wrap through the broadcast first cell and last tail cell. +12 KiB of LDS for the tail rows.
+// (column, plane) segments of one fused-pair block over ncols columns of nzt planes (column c covers [c nzt,
+// (c+1) nzt)). seg 2 = lockstep: a.zparts = P blocks per column for the first nb / P columns, each marching one of
+// the P z parts, consecutive blocks on y-adjacent columns of one part (one XCD after the remap), so their shared
+// y-halo rows meet in L2; the columns left over spread over all blocks as short second segments [s2, e2); parts
+// alternate their z direction. seg 1 = balanced split of all (column, plane) pairs; seg 0 = fixed z chunks.
+struct X2Segs {
+  uint32_t s, e, s2, e2;
+  bool odd; // first segment marches down (before the flip)
+};
+template <typename T>
+__device__ __forceinline__ X2Segs x2_segments(const StencilArgs<T> &a, uint32_t lb, uint32_t nb, uint32_t ncols,
+                                              uint32_t nzt) {
+  X2Segs r{0, 0, 0, 0, false};
+  if (a.seg == 2) {
+    const uint32_t P = uint32_t(a.zparts);
+    const uint32_t cm = nb / P;
+    // part-major: consecutive blocks take y-adjacent columns of one part (column-major: 1146 vs 1164 Gcells/s, r2s3)
+    const uint32_t qq = lb / cm, col = lb % cm;
+    r.s = col * nzt + qq * nzt / P;
+    r.e = col * nzt + (qq + 1) * nzt / P;
+    r.odd = (qq & 1) != 0;
+    const uint64_t LW = uint64_t(ncols - cm) * nzt;
+    r.s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
+    r.e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
+  } else if (a.seg) {
+    const uint64_t W = uint64_t(ncols) * nzt;
+    r.s = uint32_t(uint64_t(lb) * W / nb);
+    r.e = uint32_t(uint64_t(lb + 1) * W / nb);
+    r.odd = (lb & 1) != 0;
+  } else {
+    const uint32_t col = lb / uint32_t(a.gz);
+    r.s = col * nzt + (lb % uint32_t(a.gz)) * uint32_t(a.zc);
+    r.e = min(r.s + uint32_t(a.zc), (col + 1) * nzt);
+    r.odd = ((r.s % nzt) / uint32_t(a.zc) & 1) != 0;
+  }
+  return r;
+}
+
 template <int NW, int PF, int KIND, int H = 2, bool RAG = false, bool TL = false>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x2_row_kernel(StencilArgs<float> a) {
@@ -344,40 +382,15 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   // 972 Gcells/s, same box; the 512-cell kernel with bounds 1047-1052 vs 1142-1157; profiles/r3/s3/ab_sphere.txt)
   const int w = TL ? __builtin_amdgcn_readfirstlane(int(threadIdx.y)) : int(threadIdx.y);
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
-  uint32_t s, e, s2 = 0, e2 = 0;
-  int qodd = -1; // lockstep quarter-major: z direction by quarter parity
-  if (a.seg == 2) {
-    // lockstep: P = a.zparts blocks per column (parts of the z range; quarters unless the grid has fewer than
-    // nb/4 columns) for the first nb/P columns, so y-adjacent blocks march the same planes together and their shared
-    // y-halo rows meet in L2; the columns left over (grids of fewer than P x columns blocks) spread over all blocks
-    // as short second segments
-    const uint32_t P = uint32_t(a.zparts);
-    const uint32_t cm = nb / P;
-    // part-major: consecutive blocks (one XCD after the remap) take y-adjacent columns of one part, so an XCD's
-    // blocks share every interior y-halo row through its L2 (column-major: 1146 vs 1164 Gcells/s, r2s3)
-    const uint32_t qq = lb / cm, col = lb % cm;
-    s = col * nzt + qq * nzt / P;
-    e = col * nzt + (qq + 1) * nzt / P;
-    qodd = int(qq & 1);
-    const uint64_t LW = uint64_t(uint32_t(a.gy) - cm) * nzt;
-    s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
-    e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
-  } else if (a.seg) {
-    const uint64_t W = uint64_t(uint32_t(a.gy)) * nzt;
-    s = uint32_t(uint64_t(lb) * W / nb);
-    e = uint32_t(uint64_t(lb + 1) * W / nb);
-  } else {
-    const uint32_t col = lb / uint32_t(a.gz);
-    s = col * nzt + (lb % uint32_t(a.gz)) * uint32_t(a.zc);
-    e = min(s + uint32_t(a.zc), (col + 1) * nzt);
-  }
   // z-march direction alternates between neighbouring segments (their shared boundary planes meet in cache); in the
-  // quarter-major lockstep order it alternates by quarter, so y-adjacent blocks march together
-  bool odd = qodd >= 0 ? qodd != 0 : (a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0);
+  // part-major lockstep order it alternates by part, so y-adjacent blocks march together
+  const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gy), nzt);
+  uint32_t s = sg.s, e = sg.e;
+  bool odd = sg.odd;
   for (int pass = 0; pass < 2; ++pass) {
   if (pass == 1) {
-    s = s2;
-    e = e2;
+    s = sg.s2;
+    e = sg.e2;
   }
   while (s < e) { // block-uniform
   const uint32_t by = s / nzt; // one column per row range
@@ -675,17 +688,16 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   const int lane = threadIdx.x;
   const int w = int(threadIdx.y);
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
-  uint32_t s, e;
-  if (a.seg) {
-    const uint64_t W = uint64_t(uint32_t(a.gx) * uint32_t(a.gy)) * nzt;
-    s = uint32_t(uint64_t(lb) * W / nb);
-    e = uint32_t(uint64_t(lb + 1) * W / nb);
-  } else {
-    const uint32_t col = lb / uint32_t(a.gz);
-    s = col * nzt + (lb % uint32_t(a.gz)) * uint32_t(a.zc);
-    e = min(s + uint32_t(a.zc), (col + 1) * nzt);
+  // lockstep parts as the whole-row kernel (y-adjacent columns of one 512-cell column strip are consecutive unless
+  // xfast): 1024x512x256, 128 columns, marches 2 parts on 256 blocks
+  const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gx) * uint32_t(a.gy), nzt);
+  uint32_t s = sg.s, e = sg.e;
+  bool odd = sg.odd;
+  for (int pass = 0; pass < 2; ++pass) {
+  if (pass == 1) {
+    s = sg.s2;
+    e = sg.e2;
   }
-  bool odd = a.seg ? (lb & 1) != 0 : ((s % nzt) / uint32_t(a.zc) & 1) != 0;
   while (s < e) { // block-uniform
   const uint32_t col = s / nzt;
   const int zo = int(s - col * nzt);
@@ -892,6 +904,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   else
     march(std::false_type{});
   } // segments
+  } // passes
 }
 
 // S o S on a few small boxes (the exterior slabs of an overlapped step: interior sweep during the exchange, these
@@ -1263,6 +1276,13 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
     const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
     const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
     blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 16)));
+    // lockstep parts (x2_lockstep_schedule) when y-adjacent columns are consecutive (column index y-major)
+    const X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
+    if (tune.x2lockstep && !tune.x2xfast && ls.parts > 0) {
+      a.seg = 2;
+      a.zparts = ls.parts;
+      blocks = uint32_t(ls.blocks);
+    }
   } else {
     int zc = tune.zchunk;
     if (zc <= 0) zc = pick_zchunk(cols, nz, resident, 4, 16);

@@ -104,5 +104,8 @@ def test_x2_lockstep_schedule(st):
     assert f(256, 51, 407) == (5, 255)     # 813x407x407: 51 groups x 5 parts of 81-82 planes
     assert f(256, 81, 323) == (4, 256)     # 645x645x323: quarters over 64 groups + 17 as second segments
     assert f(256, 41, 645) == (6, 246)     # 645x323x645
+    assert f(256, 128, 256) == (2, 256)    # 1024x512x256 (512-cell columns: 2 x 64): two parts over whole columns
+    assert f(256, 256, 256) == (1, 256)    # one block per column
+    assert f(256, 300, 512) == (4, 256)    # more columns than slots: quarters + second segments
     assert f(256, 64, 40) == (0, 0)        # thin grids: balanced split
     assert f(256, 17, 200) == (0, 0)       # 15 parts of 13 planes: too short

@@ -513,11 +513,11 @@ def test_temporal2_row_kernel_lockstep_quarters(st, fake, reserve, lockstep, alt
     assert torch.equal(_gather(m), u)
 
 
-@pytest.mark.parametrize("size", [(512, 320, 112), (645, 200, 160), (813, 136, 256)])
+@pytest.mark.parametrize("size", [(512, 320, 112), (645, 200, 160), (813, 136, 256), (1024, 128, 128)])
 def test_temporal2_row_kernel_lockstep_parts(st, size):
     """Grids of fewer row groups than resident blocks / 4 run lockstep with P = blocks / columns z parts per column
-    (40 columns: P = 6 over 240 blocks; 25 ragged 645-cell columns: P = 10; 17 tail-row columns: P = 15 over 255):
-    bitwise equal to single steps."""
+    (40 columns: P = 6 over 240 blocks; 25 ragged 645-cell columns: P = 10; 17 tail-row columns: P = 15 over 255;
+    the 512-cell column kernel over 2 x 16 columns: P = 8): bitwise equal to single steps."""
     from stencil2_amd.ops import astaroth_step_reference
     m = st.AstarothSim(size, quantities=1, gpus=[0], temporal=2, axis_cost=(64, 3, 2))
     m.init()
