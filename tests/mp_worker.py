@@ -106,6 +106,8 @@ def scenario_jacobi(backend, methods, size):
     kind = os.environ.get("MP_KIND", "jacobi")
     cost = os.environ.get("MP_AXIS_COST")  # NodeAware cut costs, e.g. "4,2,3" (default: the model's)
     kw = {"axis_cost": tuple(int(v) for v in cost.split(","))} if cost else {}
+    if os.environ.get("MP_PARTITION") == "maxlink":  # bench.py's decomposition of the xGMI mesh (1x1xN slabs)
+        kw["partition"] = st.PartitionObjective.MaxLink
     if kind == "astaroth":
         from stencil2_amd.ops import astaroth_step_reference as ref
         m = st.AstarothSim(size, quantities=1, gpus=gpus, backend=backend, methods=methods, group=g,

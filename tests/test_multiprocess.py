@@ -31,6 +31,15 @@ def test_jacobi_ranks_match_oracle():
     _ok(run_ranks(3, WORKER, ["jacobi", "15,11,9"]))
 
 
+def test_jacobi_eight_ranks_maxlink_slabs():
+    """bench.py's 8-GPU layout on the CPU backend: eight ranks over the TCP mesh, MaxLink 1x1x8 slabs (every rank
+    exchanges its two z faces with two different ranks, x and y self-periodic), fused pairs vs the torch oracle"""
+    outs = run_ranks(8, WORKER, ["jacobi", "12,10,64"],
+                     env_extra={"MP_PARTITION": "maxlink", "MP_RANDOM": "1", "MP_TEMPORAL": "2", "MP_AXIS_COST": "4,3,2"})
+    _ok(outs)
+    assert all("bad 0 " in out and "dim Dim3(1, 1, 8)" in out for _, out in outs)
+
+
 @pytest.mark.parametrize("n,radius", [(2, "r1"), (3, "fec")])
 def test_race_canary_staged(n, radius):
     """NaN-poisoned halos, iteration-tagged interiors, back-to-back exchanges with random transport jitter."""
