@@ -5,7 +5,9 @@
 //                          (H 16-B chunks per lane), PF rows of loads in flight, z-marching columns of NW rows
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <chrono>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                                                          \
@@ -84,6 +86,41 @@ __global__ __launch_bounds__(64 * NW, 1) void k_rows(const f4 *__restrict__ s, f
   }
 }
 
+__global__ void k_null(float *o) {
+  if (threadIdx.x == 1023) o[1] = 0;
+}
+
+// host round trip of a blocking launch (launch + hipStreamSynchronize), the floor under a blocking exchange()
+static void roundtrip(float *o, f4 *b, long n4) {
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  auto run = [&](const char *name, auto launch) {
+    for (int i = 0; i < 20; ++i) {
+      launch();
+      CK(hipStreamSynchronize(s));
+    }
+    const int reps = 200;
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; ++i) {
+      launch();
+      CK(hipStreamSynchronize(s));
+    }
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+    auto t1 = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipStreamSynchronize(s));
+    const double us2 = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count() / reps;
+    std::printf("roundtrip,%s,blocking_us,%.2f,stream_ordered_us,%.2f\n", name, us, us2);
+    std::fflush(stdout);
+  };
+  run("null_kernel", [&] { k_null<<<1, 1024, 0, s>>>(o); });
+  // 12.68 MB written (the 512^3 depth-2 self-exchange's payload) as one grid-stride store stream
+  const long w4 = 12681216 / 16;
+  run("write_12.7MB", [&] { k_write<false><<<1024, 256, 0, s>>>(b, w4, 1.f); });
+  run("copy_12.7MB", [&] { k_copy<false><<<1024, 256, 0, s>>>(b + n4 / 2, b, w4); });
+  CK(hipStreamDestroy(s));
+}
+
 int main(int argc, char **argv) {
   const int X = 512, Y = 512, Z = 512;
   const long n4 = long(X) * Y * Z / 4;
@@ -117,6 +154,8 @@ int main(int argc, char **argv) {
                 mult * bytes / (sum / reps * 1e-3) / 1e12);
     std::fflush(stdout);
   };
+  roundtrip(o, b, n4);
+  if (argc > 1 && std::string(argv[1]) == "--roundtrip") return 0;
   std::printf("name,blocks,waves_per_block,best_us,best_TBps,mean_TBps\n");
   for (int blocks : {1024, 2048, 4096, 8192}) {
     time("copy", blocks, 4, 2, [&] { k_copy<false><<<blocks, 256>>>(a, b, n4); });
