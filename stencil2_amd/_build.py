@@ -6,6 +6,7 @@ plus the C++ apps in ``build/bin``. Everything stays in-tree so it travels with 
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -28,10 +29,27 @@ def _artifacts():
     return glob.glob(os.path.join(PKG, "_C*.so")) + glob.glob(os.path.join(PKG, "libstencil2.so"))
 
 
+STAMP = os.path.join(PKG, ".build_stamp")
+
+
+def _source_hash() -> str:
+    """sha256 over the native sources' paths and contents: copies, checkouts and snapshots change mtimes without
+    changing what the artifacts were built from"""
+    h = hashlib.sha256()
+    for f in sorted(_sources()):
+        h.update(os.path.relpath(f, REPO).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def is_stale() -> bool:
     arts = _artifacts()
     if len(arts) < 2 or not os.path.exists(os.path.join(BUILD, "bin", "jacobi3d")):
         return True
+    if os.path.exists(STAMP):
+        with open(STAMP) as f:
+            return f.read().strip() != _source_hash()
     newest_src = max(os.path.getmtime(s) for s in _sources())
     oldest_art = min(os.path.getmtime(a) for a in arts)
     return newest_src > oldest_art
@@ -55,11 +73,21 @@ def build(verbose: bool = False, jobs: int | None = None) -> None:
         tmp = dst + ".tmp"
         shutil.copy2(so, tmp)
         os.replace(tmp, dst)
+    with open(STAMP + ".tmp", "w") as f:
+        f.write(_source_hash() + "\n")
+    os.replace(STAMP + ".tmp", STAMP)
 
 
 def ensure_built() -> None:
-    if is_stale():
-        build()
+    if not is_stale():
+        return
+    if _artifacts() and not os.path.exists(os.path.join(BUILD, "CMakeFiles", "rules.ninja")):
+        # a snapshot without the configured build tree (a GPU box): the shipped artifacts are what there is to load;
+        # rebuilding here would fail half-way, so load them and say so
+        print("stencil2_amd: native sources differ from the build stamp and no build tree is configured here; "
+              "loading the shipped artifacts", file=sys.stderr)
+        return
+    build()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,22 @@
+"""The in-tree build's staleness check is by content (a sha256 stamp over the native sources written by build()):
+snapshots and copies that only change mtimes must not trigger a rebuild on a GPU box that has no build tree."""
+import os
+
+from stencil2_amd import _build
+
+
+def test_stamp_matches_sources():
+    assert os.path.exists(_build.STAMP)
+    with open(_build.STAMP) as f:
+        assert f.read().strip() == _build._source_hash()
+    assert not _build.is_stale()
+
+
+def test_mtime_only_change_is_not_stale():
+    src = sorted(_build._sources())[0]
+    st = os.stat(src)
+    try:
+        os.utime(src, (st.st_atime, st.st_mtime + 3600))
+        assert not _build.is_stale()
+    finally:
+        os.utime(src, (st.st_atime, st.st_mtime))
