@@ -658,22 +658,21 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   } // passes
 }
 
-// 512-cell columns (fp32): the whole-row layout of stencil7x2_row_kernel (two 16-B chunks per lane, 256 cells apart,
-// x-neighbours by lane rotates) for rows longer than one wave: a column of 512 cells per wave, and only the two
-// cells beyond each column end come from outside the wave - a pair left of the column (lane 0 of chunk 0) and a pair
-// right of it (lane 63 of chunk 1). Those pairs have one address per wave (a broadcast load each, shifted by the
-// period at the wrapped row ends), and the neighbour rows' pairs come through LDS, as the edge scalars of
-// stencil7x2_kernel. Taken for x extents that are whole multiples of 512 cells (the 1024-wide sub-domains of the
-// 8-GPU weak-scaling ladder): per row and plane the edge work and the fixed per-step cost of the 256-cell column
-// kernel are paid once per 512 cells. Summation order, exact /6 and spheres as everywhere: bitwise equal to two
-// single steps.
-template <int NW, int PF, int KIND, int WRAP>
+// Two-chunk columns (512 fp32 / 256 fp64 cells): the whole-row layout of stencil7x2_row_kernel (two 16-B chunks per
+// lane, 64 chunks apart, x-neighbours by lane rotates) for rows longer than one wave: a column of CW cells per wave,
+// and only the two cells beyond each column end come from outside the wave - a pair left of the column (lane 0 of
+// chunk 0) and a pair right of it (lane 63 of chunk 1). Those pairs have one address per wave (a broadcast load each,
+// shifted by the period at the wrapped row ends), and the neighbour rows' pairs come through LDS, as the edge scalars
+// of stencil7x2_kernel. Taken for x extents that are whole multiples of CW cells (the 1024-wide sub-domains of the
+// 8-GPU weak-scaling ladder; fp64 1024-cell rows as 4 columns): per row and plane the edge work and the fixed per-step
+// cost of the one-chunk column kernel are paid once per two chunks per lane. Summation order, exact /6 and spheres
+// as everywhere: bitwise equal to two single steps.
+template <typename T, int NW, int PF, int KIND, int WRAP>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void stencil7x2_col2_kernel(
-    StencilArgs<float> a) {
-  using T = float;
-  using NV = nf4;
+    StencilArgs<T> a) {
+  using NV = typename Vec16<T>::native;
   using P2 = typename Pk<T>::t;
-  constexpr int V = 4, H = 2;   // chunks per lane
+  constexpr int V = int(16 / sizeof(T)), H = 2; // chunks per lane
   constexpr int HS = 64 * V;    // cells between a lane's chunks
   constexpr int CW = H * HS;    // cells per column
   constexpr int YO = NW - 4;
@@ -681,7 +680,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   static_assert(NW == 12, "3 waves per SIMD: the 168-VGPR budget");
   __shared__ NV cs[2][NW][H][64]; // src rows (plane z+2dz at publish)
   __shared__ NV us[2][NW][H][64]; // u1 rows (plane z+dz at publish)
-  __shared__ T ce[2][NW][2];      // src at x-1 and x+512 of the published rows
+  __shared__ T ce[2][NW][2];      // src at x-1 and x+CW of the published rows
 
   const uint32_t nb = gridDim.x;
   const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
@@ -730,7 +729,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   const int yc = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
   const uint32_t rowoff = uint32_t((yc * int64_t(a.px) + xb) * int64_t(sizeof(T)));
   const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
-  // the edge pairs (x-2, x-1 left of the column; x+512, x+513 right of it): one address per wave; x wrap moves the
+  // the edge pairs (x-2, x-1 left of the column; x+CW, x+CW+1 right of it): one address per wave; x wrap moves the
   // left pair of the first column and the right pair of the last one by the period
   int xl = xcol - 2, xr = xcol + CW;
   if (WRAP == 2 && (a.wrapm & 1)) {
@@ -800,9 +799,9 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
     constexpr int dz = DOWN ? -1 : 1;
     const int z0 = DOWN ? ze - 1 : zs;
     NV C[NC][H];
-    P2 EL[NC], ER[NC]; // (x-2, x-1) and (x+512, x+513) of the column, per window plane
+    P2 EL[NC], ER[NC]; // (x-2, x-1) and (x+CW, x+CW+1) of the column, per window plane
     NV Ub[H], Uc[H], Ua[H];
-    P2 UcE, UaE; // u1 at (x-1, x+512), planes z and z+dz
+    P2 UcE, UaE; // u1 at (x-1, x+CW), planes z and z+dz
     auto load_row = [&](int zz, int k) {
       const char *b = planep(zz);
 #pragma unroll
@@ -849,7 +848,7 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
         const T cBL = ce[buf][wB][0], cBR = ce[buf][wB][1];
         const RowSph rs = row_sph(P);
         apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], EL[s1][1], ER[s1][0], rs, Ua);
-        // u1 just outside the column: (x-1) on lane 0, (x+512) on lane 63
+        // u1 just outside the column: (x-1) on lane 0, (x+CW) on lane 63
         const P2 epx = {C[s1][0][0], ER[s1][1]}, emx = {EL[s1][0], C[s1][H - 1][V - 1]}, epy = {cBL, cBR},
                  emy = {cAL, cAR};
         const P2 ezp = DOWN ? P2{EL[s0][1], ER[s0][0]} : P2{EL[s2][1], ER[s2][0]};
@@ -1247,23 +1246,24 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   return true;
 }
 
-// 512-cell column kernel: fp32, the region's x extent a whole number of 512-cell columns starting on a 16-B chunk
-template <int KIND, int PF, int WRAP>
+// two-chunk column kernel: the region's x extent a whole number of CW-cell columns (512 fp32, 256 fp64) starting on
+// a 16-B chunk
+template <typename T, int KIND, int PF, int WRAP>
 static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph,
                            hipStream_t stream, const StencilTune &tune) {
-  constexpr int NW = 12, YO = NW - 4;
-  StencilArgs<float> a = make_args<float>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
+  constexpr int NW = 12, YO = NW - 4, V = int(16 / sizeof(T)), CW = 128 * V;
+  StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
   a.wrapm = tune.wrap;
   a.xfast = tune.x2xfast;
   a.remap = tune.xcdRemap ? 1 : 0;
   a.x0 = a.lox; // 16-B aligned (checked by the caller)
-  a.nchunks = (a.hix - a.x0) / 4;
+  a.nchunks = (a.hix - a.x0) / V;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
-  a.gx = (a.hix - a.x0) / 512;
+  a.gx = (a.hix - a.x0) / CW;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = (const void *)stencil7x2_col2_kernel<NW, PF, KIND, WRAP>;
+  const void *kern = (const void *)stencil7x2_col2_kernel<T, NW, PF, KIND, WRAP>;
   const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x2_resident_blocks(kern, 64 * NW);
   uint32_t blocks;
@@ -1291,19 +1291,19 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
     blocks = uint32_t(cols * a.gz);
   }
   dom.set_device();
-  hipLaunchKernelGGL((stencil7x2_col2_kernel<NW, PF, KIND, WRAP>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  hipLaunchKernelGGL((stencil7x2_col2_kernel<T, NW, PF, KIND, WRAP>), dim3(blocks), dim3(64, NW), 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }
 
-template <int KIND, int PF>
+template <typename T, int KIND, int PF>
 static void apply_x2col2_wrap(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph,
                               hipStream_t stream, const StencilTune &tune) {
   if (tune.wrap & 1)
-    apply_x2col2_t<KIND, PF, 2>(dom, qi, region, sph, stream, tune);
+    apply_x2col2_t<T, KIND, PF, 2>(dom, qi, region, sph, stream, tune);
   else if (tune.wrap)
-    apply_x2col2_t<KIND, PF, 1>(dom, qi, region, sph, stream, tune);
+    apply_x2col2_t<T, KIND, PF, 1>(dom, qi, region, sph, stream, tune);
   else
-    apply_x2col2_t<KIND, PF, 0>(dom, qi, region, sph, stream, tune);
+    apply_x2col2_t<T, KIND, PF, 0>(dom, qi, region, sph, stream, tune);
 }
 
 bool stencil7x2_row_kernel_used(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune) {
@@ -1363,8 +1363,18 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
     // x a whole number of 512-cell columns from a 16-B aligned first cell: the 512-cell column kernel
     if (nx % 512 == 0 && (rr.lo.x - dom.radius().x(-1)) % 4 == 0) {
       // one plane of lookahead (two would spill the Jacobi instance; the row kernel shows no difference)
-      jac ? apply_x2col2_wrap<0, 1>(dom, qi, region, sph, stream, tune)
-          : apply_x2col2_wrap<1, 1>(dom, qi, region, sph, stream, tune);
+      jac ? apply_x2col2_wrap<float, 0, 1>(dom, qi, region, sph, stream, tune)
+          : apply_x2col2_wrap<float, 1, 1>(dom, qi, region, sph, stream, tune);
+      return;
+    }
+  }
+  if (!f32 && tune.x2row && !tune.publish) {
+    // fp64: x a whole number of 256-cell columns (two 2-double chunks per lane) from a 16-B aligned first cell
+    const Rect3 rr(region.lo - dom.accessor_origin(), region.hi - dom.accessor_origin());
+    const int64_t nx = rr.hi.x - rr.lo.x;
+    if (nx % 256 == 0 && (rr.lo.x - dom.radius().x(-1)) % 2 == 0) {
+      jac ? apply_x2col2_wrap<double, 0, 1>(dom, qi, region, sph, stream, tune)
+          : apply_x2col2_wrap<double, 1, 1>(dom, qi, region, sph, stream, tune);
       return;
     }
   }

@@ -92,4 +92,17 @@ __device__ __forceinline__ float rot_next(float v) { // lane i <- lane i+1, lane
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xf, 0xf, false));
 }
 
+__device__ __forceinline__ double rot_prev(double v) { // fp64: both 32-bit halves rotated
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), 0x13C, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), 0x13C, 0xf, 0xf, false);
+  return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
+}
+__device__ __forceinline__ double rot_next(double v) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), 0x134, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), 0x134, 0xf, 0xf, false);
+  return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
+}
+
 } // namespace stencil

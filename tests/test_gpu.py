@@ -294,18 +294,25 @@ def test_single_step_in_kernel_wrap(st, kind, size, gpus, fp64):
             assert torch.equal(_gather(m), u), f"wrap_self={ms.index(m) == 0} after run({n}) + step()"
 
 
-@pytest.mark.parametrize("kind,size,gpus,wrap,cost", [
-    ("astaroth", (1024, 24, 20), [0], True, (4, 2, 3)),     # periodic x: two 512-cell columns
-    ("astaroth", (1024, 20, 16), [0], False, (4, 2, 3)),    # x halos in memory
-    ("astaroth", (512, 20, 24), [0], False, (4, 2, 3)),     # one column between halos
-    ("astaroth", (1024, 16, 20), [0, 0], True, (1, 1, 1)),  # x cut: 512-wide halves, halos from the other half
-    ("jacobi", (1024, 216, 212), [0], True, (4, 2, 3)),     # spheres
-    ("jacobi", (512, 120, 116), [0], False, (4, 2, 3)),
+@pytest.mark.parametrize("kind,size,gpus,wrap,cost,fp64", [
+    ("astaroth", (1024, 24, 20), [0], True, (4, 2, 3), False),     # periodic x: two 512-cell columns
+    ("astaroth", (1024, 20, 16), [0], False, (4, 2, 3), False),    # x halos in memory
+    ("astaroth", (512, 20, 24), [0], False, (4, 2, 3), False),     # one column between halos
+    ("astaroth", (1024, 16, 20), [0, 0], True, (1, 1, 1), False),  # x cut: 512-wide halves, halos from the other half
+    ("jacobi", (1024, 216, 212), [0], True, (4, 2, 3), False),     # spheres
+    ("jacobi", (512, 120, 116), [0], False, (4, 2, 3), False),
+    # fp64: 256-cell columns (two 2-double chunks per lane)
+    ("astaroth", (1024, 24, 20), [0], True, (4, 2, 3), True),      # four periodic columns
+    ("astaroth", (256, 20, 24), [0], True, (4, 2, 3), True),       # one column, wrapped onto itself
+    ("astaroth", (512, 20, 16), [0], False, (4, 2, 3), True),      # x halos in memory
+    ("astaroth", (512, 16, 20), [0, 0], True, (1, 1, 1), True),    # x cut: 256-wide halves
+    ("jacobi", (1024, 216, 212), [0], True, (4, 2, 3), True),      # spheres
+    ("jacobi", (256, 120, 116), [0], False, (4, 2, 3), True),
 ])
-def test_temporal2_col512_kernel(st, kind, size, gpus, wrap, cost):
-    """Fused pairs on x extents of whole 512-cell columns take the 512-cell column kernel (two chunks per lane, the
-    column-end pairs by broadcast loads, stencil7x2_col2_kernel): bitwise equal to single steps and to the 256-cell
-    column kernel (x2row = 0)."""
+def test_temporal2_col512_kernel(st, kind, size, gpus, wrap, cost, fp64):
+    """Fused pairs on x extents of whole two-chunk columns (512 fp32 / 256 fp64 cells) take the two-chunk column
+    kernel (two chunks per lane, the column-end pairs by broadcast loads, stencil7x2_col2_kernel): bitwise equal to
+    single steps and to the one-chunk column kernel (x2row = 0)."""
     from stencil2_amd.ops import astaroth_step_reference
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
@@ -313,7 +320,7 @@ def test_temporal2_col512_kernel(st, kind, size, gpus, wrap, cost):
     for row in (1, 0):
         t = st.StencilTune()
         t.x2row = row
-        ms.append(cls(size, gpus=gpus, temporal=2, tune=t, wrap_self=wrap, axis_cost=cost, **kw))
+        ms.append(cls(size, gpus=gpus, temporal=2, tune=t, wrap_self=wrap, axis_cost=cost, fp64=fp64, **kw))
     for m in ms:
         m.init()
         assert m.temporal_blocking()
