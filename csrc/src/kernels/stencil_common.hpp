@@ -98,6 +98,15 @@ template <> __device__ __forceinline__ float div6<float>(float x) {
   if (__builtin_expect(__builtin_fabsf(x) < 0x1p-100f, 0)) q = x / 6.0f;
   return q;
 }
+// fp64: the same corrected quotient (see div6v in stencil_wave.hpp), true division below 2^-960
+template <> __device__ __forceinline__ double div6<double>(double x) {
+  constexpr double c = 1.0 / 6.0;
+  const double q0 = x * c;
+  const double r = __builtin_fma(-q0, 6.0, x);
+  double q = __builtin_fma(r, c, q0);
+  if (__builtin_expect(__builtin_fabs(x) < 0x1p-960, 0)) q = x / 6.0;
+  return q;
+}
 
 
 // kernel arguments for one quantity of one sub-domain over `region` (global coordinates)

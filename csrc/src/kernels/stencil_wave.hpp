@@ -37,7 +37,7 @@ template <> __device__ __forceinline__ double from_next_lane<double>(double v) {
 
 // Six-term sums in the reference's order (sum6 in stencil_common.hpp), element-wise over a vector type. The fp32
 // sums start from the first term instead of 0 + first term: the two differ only in the sign of an all-zero sum,
-// and the exact /6 below maps both zeros to +0 as the 0-started sum does. fp64 keeps the 0 start (true division).
+// and the exact /6 below maps both zeros to +0 as the 0-started sum does. fp64 keeps the 0 start.
 template <typename T, int KIND, typename X>
 __device__ __forceinline__ X sum6v(const X &vpx, const X &vmx, const X &vpy, const X &vmy, const X &vpz, const X &vmz) {
   X s;
@@ -58,8 +58,8 @@ __device__ __forceinline__ X sum6v(const X &vpx, const X &vmx, const X &vpy, con
   }
   return s;
 }
-// exact element-wise /6 (div6): fp32 two FMAs around the reciprocal, packed; sums with 0 < |s| < 2^-100 (where the
-// FMA form is not exact) take the true division in a branch no wave normally enters
+// exact element-wise /6 (div6): two FMAs around the reciprocal (fp32 packed); sums with 0 < |s| < 2^-100 (fp64:
+// 2^-960), where the FMA form is not exact, take the true division in a branch no wave normally enters
 template <typename T, typename X, int N> __device__ __forceinline__ X div6v(const X &s) {
   if constexpr (std::is_same<T, float>::value) {
     const X c = X(1.0f / 6.0f), six = X(6.0f);
@@ -76,7 +76,22 @@ template <typename T, typename X, int N> __device__ __forceinline__ X div6v(cons
     }
     return q;
   } else {
-    return s / X(T(6));
+    // fp64: the same two FMAs around RN(1/6) (Markstein's corrected quotient; 1.2e9 random inputs, half of them
+    // near multiples of 3, all equal to the IEEE quotient for |s| >= 2^-960: scripts/mi355x/lab/div6_fp64_check.cpp)
+    // instead of the ~10-instruction division sequence; smaller sums (subnormal-range results) divide
+    const X c = X(1.0 / 6.0), six = X(6.0);
+    const X q0 = s * c;
+    const X r = __builtin_elementwise_fma(-q0, six, s);
+    X q = __builtin_elementwise_fma(r, c, q0);
+    double m = __builtin_fabs(s[0]);
+#pragma unroll
+    for (int e = 1; e < N; ++e) m = __builtin_fmin(m, __builtin_fabs(s[e]));
+    if (__builtin_expect(m < 0x1p-960, 0)) {
+#pragma unroll
+      for (int e = 0; e < N; ++e)
+        if (__builtin_fabs(s[e]) < 0x1p-960 && s[e] != 0.0) q[e] = s[e] / 6.0;
+    }
+    return q;
   }
 }
 
