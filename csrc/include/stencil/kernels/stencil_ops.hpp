@@ -164,7 +164,7 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
 // groups (8 output rows of one column strip each), `nz` planes. P blocks per row group march P z parts side by side (y-adjacent blocks on one XCD, so their
 // shared y-halo rows meet in L2): quarters (P = 4) over the first slots / 4 row groups with the rest as short
 // second segments, or P = slots / cols over every row group when the grid has fewer than slots / 4 row groups or
-// the row groups divide the slots evenly
+// the row groups divide the slots evenly; rounds of whole columns when there are more row groups than slots
 // (813x407x407: 51 groups, 5 parts, 847 -> 910-917 Gcells/s; 645x323x645: 41 groups, 6 parts, 847 -> 1067-1072).
 // Whole columns over fewer slots instead of quarters plus leftovers lose (645x645x323, 81 groups: 3 parts on 243
 // blocks 930-946 vs 994-1001; profiles/r3/s3/ab_lockstep_parts.txt). parts == 0: no lockstep (parts under 16
@@ -172,10 +172,21 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
 struct X2Schedule {
   int parts = 0;
   int64_t blocks = 0;
+  int rounds = 1; // > 1: whole columns, block b marching columns b, b + blocks, ... in step with the others
 };
 inline X2Schedule x2_lockstep_schedule(int64_t slots, int64_t cols, int64_t nz) {
   X2Schedule r;
   if (slots < 4 || cols < 1) return r;
+  if (cols > slots) {
+    // more row groups than blocks (fp64 1024^3 as 256-cell columns: 4 x 128 groups): rounds of whole columns, every
+    // block on one column per round, y-adjacent columns side by side (quarters plus leftovers would run most
+    // columns as balanced second segments)
+    if (nz < 16) return r;
+    r.rounds = int((cols + slots - 1) / slots);
+    r.parts = 1;
+    r.blocks = (cols + r.rounds - 1) / r.rounds;
+    return r;
+  }
   // whole columns when they divide the slots evenly (1024x512x256 on the 512-cell column kernel: 128 columns, P = 2)
   const int64_t P = (slots / 4 > cols || slots % cols == 0) ? slots / cols : 4;
   const int64_t cm = cols < slots / P ? cols : slots / P;

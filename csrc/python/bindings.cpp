@@ -648,10 +648,11 @@ PYBIND11_MODULE(_C, m) {
       "x2_lockstep_schedule",
       [](int64_t slots, int64_t cols, int64_t nz) {
         const X2Schedule r = x2_lockstep_schedule(slots, cols, nz);
-        return py::make_tuple(r.parts, r.blocks);
+        return py::make_tuple(r.parts, r.blocks, r.rounds);
       },
       py::arg("slots"), py::arg("cols"), py::arg("nz"),
-      "lockstep schedule of the whole-row fused pair: (z parts per row group, blocks); (0, 0) = balanced split");
+      "lockstep schedule of the whole-row / two-chunk-column fused pairs: (z parts per row group, blocks, rounds of "
+      "whole columns); (0, 0, 1) = balanced split");
   m.def("jacobi_spheres", [](const Rect3 &cReg) {
     Spheres s = Spheres::jacobi(cReg);
     return py::make_tuple(s.hot, s.cold, s.radius);

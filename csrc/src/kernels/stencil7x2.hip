@@ -331,6 +331,7 @@ template <typename T>
 __device__ __forceinline__ X2Segs x2_segments(const StencilArgs<T> &a, uint32_t lb, uint32_t nb, uint32_t ncols,
                                               uint32_t nzt) {
   X2Segs r{0, 0, 0, 0, false};
+  if (a.seg == 3) return r; // rounds of whole columns (x2_pass)
   if (a.seg == 2) {
     const uint32_t P = uint32_t(a.zparts);
     const uint32_t cm = nb / P;
@@ -354,6 +355,23 @@ __device__ __forceinline__ X2Segs x2_segments(const StencilArgs<T> &a, uint32_t 
     r.odd = ((r.s % nzt) / uint32_t(a.zc) & 1) != 0;
   }
   return r;
+}
+// the block's segment of pass p ([s, e) in (column, plane) space); false when it has no more. seg 3 = rounds of
+// whole columns (a.zparts rounds): pass p is column p nb + lb, all blocks on adjacent columns in step
+template <typename T>
+__device__ __forceinline__ bool x2_pass(const StencilArgs<T> &a, const X2Segs &sg, int p, uint32_t lb, uint32_t nb,
+                                        uint32_t ncols, uint32_t nzt, uint32_t &s, uint32_t &e) {
+  if (a.seg == 3) {
+    const uint32_t col = uint32_t(p) * nb + lb;
+    if (p >= a.zparts || col >= ncols) return false;
+    s = col * nzt;
+    e = s + nzt;
+    return true;
+  }
+  if (p > 1) return false;
+  s = p == 0 ? sg.s : sg.s2;
+  e = p == 0 ? sg.e : sg.e2;
+  return true;
 }
 
 template <int NW, int PF, int KIND, int H = 2, bool RAG = false, bool TL = false>
@@ -385,13 +403,9 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   // z-march direction alternates between neighbouring segments (their shared boundary planes meet in cache); in the
   // part-major lockstep order it alternates by part, so y-adjacent blocks march together
   const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gy), nzt);
-  uint32_t s = sg.s, e = sg.e;
+  uint32_t s = 0, e = 0;
   bool odd = sg.odd;
-  for (int pass = 0; pass < 2; ++pass) {
-  if (pass == 1) {
-    s = sg.s2;
-    e = sg.e2;
-  }
+  for (int pass = 0; x2_pass(a, sg, pass, lb, nb, uint32_t(a.gy), nzt, s, e); ++pass) {
   while (s < e) { // block-uniform
   const uint32_t by = s / nzt; // one column per row range
   const int zo = int(s - by * nzt);
@@ -690,13 +704,9 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   // lockstep parts as the whole-row kernel (y-adjacent columns of one 512-cell column strip are consecutive unless
   // xfast): 1024x512x256, 128 columns, marches 2 parts on 256 blocks
   const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gx) * uint32_t(a.gy), nzt);
-  uint32_t s = sg.s, e = sg.e;
+  uint32_t s = 0, e = 0;
   bool odd = sg.odd;
-  for (int pass = 0; pass < 2; ++pass) {
-  if (pass == 1) {
-    s = sg.s2;
-    e = sg.e2;
-  }
+  for (int pass = 0; x2_pass(a, sg, pass, lb, nb, uint32_t(a.gx) * uint32_t(a.gy), nzt, s, e); ++pass) {
   while (s < e) { // block-uniform
   const uint32_t col = s / nzt;
   const int zo = int(s - col * nzt);
@@ -1229,8 +1239,8 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     // at 256 blocks); 813x407x407 (51 row groups) runs 5 parts on 255 blocks
     const X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
     if (tune.x2lockstep && ls.parts > 0) {
-      a.seg = 2;
-      a.zparts = ls.parts;
+      a.seg = ls.rounds > 1 ? 3 : 2;
+      a.zparts = ls.rounds > 1 ? ls.rounds : ls.parts;
       blocks = uint32_t(ls.blocks);
     }
   } else {
@@ -1279,8 +1289,8 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
     // lockstep parts (x2_lockstep_schedule) when y-adjacent columns are consecutive (column index y-major)
     const X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
     if (tune.x2lockstep && !tune.x2xfast && ls.parts > 0) {
-      a.seg = 2;
-      a.zparts = ls.parts;
+      a.seg = ls.rounds > 1 ? 3 : 2;
+      a.zparts = ls.rounds > 1 ? ls.rounds : ls.parts;
       blocks = uint32_t(ls.blocks);
     }
   } else {

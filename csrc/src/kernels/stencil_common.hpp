@@ -47,8 +47,9 @@ template <typename T> struct StencilArgs {
   int rawZm1;                       // clamp for the deep z prefetch
   int zc;                           // planes per block
   int gx, gy, gz;                   // logical grid
-  int seg;                          // stencil7x2: 1 = balanced (column, plane) segments over gridDim.x blocks, 2 = lockstep quarters
-  int zparts;                       // stencil7x2 lockstep (seg = 2): z parts per column (4 = quarters)
+  int seg;                          // stencil7x2: 1 = balanced (column, plane) segments over gridDim.x blocks, 2 = lockstep
+                                    // z parts, 3 = lockstep rounds of whole columns
+  int zparts;                       // stencil7x2 lockstep: z parts per column (seg 2; 4 = quarters) or rounds (seg 3)
   int xfast;                        // stencil7x2: 1 = column index x-major (x-adjacent columns on one XCD)
   int remap;                        // stencil7x2: 1 = XCD-aware block remap
   // spheres, raw coordinates

@@ -99,13 +99,14 @@ def test_x2_lockstep_schedule(st):
     more row groups than slots / 4 (the overlap's 248 slots, 645x645x323), P = slots / groups parts over every row
     group when fewer (813x407x407, 645x323x645)"""
     f = st._C.x2_lockstep_schedule
-    assert f(256, 64, 512) == (4, 256)     # 512^3: 64 row groups of 8, quarters
-    assert f(248, 64, 508) == (4, 248)     # overlap interior: 62 groups in lockstep, 2 as second segments
-    assert f(256, 51, 407) == (5, 255)     # 813x407x407: 51 groups x 5 parts of 81-82 planes
-    assert f(256, 81, 323) == (4, 256)     # 645x645x323: quarters over 64 groups + 17 as second segments
-    assert f(256, 41, 645) == (6, 246)     # 645x323x645
-    assert f(256, 128, 256) == (2, 256)    # 1024x512x256 (512-cell columns: 2 x 64): two parts over whole columns
-    assert f(256, 256, 256) == (1, 256)    # one block per column
-    assert f(256, 300, 512) == (4, 256)    # more columns than slots: quarters + second segments
-    assert f(256, 64, 40) == (0, 0)        # thin grids: balanced split
-    assert f(256, 17, 200) == (0, 0)       # 15 parts of 13 planes: too short
+    assert f(256, 64, 512) == (4, 256, 1)     # 512^3: 64 row groups of 8, quarters
+    assert f(248, 64, 508) == (4, 248, 1)     # overlap interior: 62 groups in lockstep, 2 as second segments
+    assert f(256, 51, 407) == (5, 255, 1)     # 813x407x407: 51 groups x 5 parts of 81-82 planes
+    assert f(256, 81, 323) == (4, 256, 1)     # 645x645x323: quarters over 64 groups + 17 as second segments
+    assert f(256, 41, 645) == (6, 246, 1)     # 645x323x645
+    assert f(256, 128, 256) == (2, 256, 1)    # 1024x512x256 (512-cell columns: 2 x 64): two parts over whole columns
+    assert f(256, 256, 256) == (1, 256, 1)    # one block per column
+    assert f(256, 300, 512) == (1, 150, 2)    # more columns than slots: 2 rounds of whole columns on 150 blocks
+    assert f(256, 512, 1024) == (1, 256, 2)   # fp64 1024^3: 4 x 128 columns, 2 rounds
+    assert f(256, 64, 40) == (0, 0, 1)        # thin grids: balanced split
+    assert f(256, 17, 200) == (0, 0, 1)       # 15 parts of 13 planes: too short

@@ -520,13 +520,18 @@ def test_temporal2_row_kernel_lockstep_quarters(st, fake, reserve, lockstep, alt
     assert torch.equal(_gather(m), u)
 
 
-@pytest.mark.parametrize("size", [(512, 320, 112), (645, 200, 160), (813, 136, 256), (1024, 128, 128)])
-def test_temporal2_row_kernel_lockstep_parts(st, size):
+@pytest.mark.parametrize("size,fp64", [((512, 320, 112), False), ((645, 200, 160), False), ((813, 136, 256), False),
+                                       ((1024, 128, 128), False),
+                                       # more row groups than blocks: rounds of whole columns (seg 3)
+                                       ((512, 2112, 16), False), ((2048, 1040, 16), False), ((1024, 1040, 16), True)])
+def test_temporal2_row_kernel_lockstep_parts(st, size, fp64):
     """Grids of fewer row groups than resident blocks / 4 run lockstep with P = blocks / columns z parts per column
     (40 columns: P = 6 over 240 blocks; 25 ragged 645-cell columns: P = 10; 17 tail-row columns: P = 15 over 255;
-    the 512-cell column kernel over 2 x 16 columns: P = 8): bitwise equal to single steps."""
+    the 512-cell column kernel over 2 x 16 columns: P = 8); grids of more row groups than blocks march rounds of
+    whole columns (264 row groups: 2 rounds; 4 x 130 fp32 512-cell / fp64 256-cell columns: 3 rounds): bitwise equal
+    to single steps."""
     from stencil2_amd.ops import astaroth_step_reference
-    m = st.AstarothSim(size, quantities=1, gpus=[0], temporal=2, axis_cost=(64, 3, 2))
+    m = st.AstarothSim(size, quantities=1, gpus=[0], temporal=2, axis_cost=(64, 3, 2), fp64=fp64)
     m.init()
     assert m.temporal_blocking()
     u = _gather(m)
