@@ -172,7 +172,8 @@ void stencil7x2_apply_exterior(const LocalDomain &dom, int64_t qi, const Rect3 &
 struct X2Schedule {
   int parts = 0;
   int64_t blocks = 0;
-  int rounds = 1; // > 1: whole columns, block b marching columns b, b + blocks, ... in step with the others
+  int rounds = 1; // > 1: block b marches part b / cm of columns b % cm, b % cm + cm, ... (cm = blocks / parts) in
+                  // step with the others; parts 1 = whole columns
 };
 inline X2Schedule x2_lockstep_schedule(int64_t slots, int64_t cols, int64_t nz) {
   X2Schedule r;
@@ -193,6 +194,19 @@ inline X2Schedule x2_lockstep_schedule(int64_t slots, int64_t cols, int64_t nz) 
   if (cm < 1 || nz < 64 || nz / P < 16) return r;
   r.parts = int(P);
   r.blocks = P * cm;
+  if (P == 4 && cm < cols && cols % 2 == 0) {
+    // quarters over slots / 4 row groups leave the rest to balanced second segments; two rounds of P2 parts over
+    // half the row groups each keep every segment in lockstep when they fill 15 / 16 of the slots in both rounds
+    // (813x813x204: 102 groups = 2 rounds x 51 groups x 5 parts on 255 blocks, 928-931 -> 970-971 Gcells/s; an odd
+    // count idles blocks in the second round: 645x645x323, 81 groups as 2 x 41 x 6, 1034 -> 1009-1018, not taken;
+    // profiles/r3/s3/ab_rounds_parts.txt)
+    const int64_t ch = cols / 2, P2 = slots / ch;
+    if (P2 >= 2 && nz / P2 >= 16 && 16 * P2 * ch >= 15 * slots) {
+      r.parts = int(P2);
+      r.blocks = P2 * ch;
+      r.rounds = 2;
+    }
+  }
   return r;
 }
 

@@ -331,7 +331,10 @@ template <typename T>
 __device__ __forceinline__ X2Segs x2_segments(const StencilArgs<T> &a, uint32_t lb, uint32_t nb, uint32_t ncols,
                                               uint32_t nzt) {
   X2Segs r{0, 0, 0, 0, false};
-  if (a.seg == 3) return r; // rounds of whole columns (x2_pass)
+  if (a.seg == 3) { // rounds (x2_pass): parts alternate their z direction as in seg 2
+    r.odd = ((lb / (nb / uint32_t(a.zparts))) & 1) != 0;
+    return r;
+  }
   if (a.seg == 2) {
     const uint32_t P = uint32_t(a.zparts);
     const uint32_t cm = nb / P;
@@ -361,11 +364,12 @@ __device__ __forceinline__ X2Segs x2_segments(const StencilArgs<T> &a, uint32_t 
 template <typename T>
 __device__ __forceinline__ bool x2_pass(const StencilArgs<T> &a, const X2Segs &sg, int p, uint32_t lb, uint32_t nb,
                                         uint32_t ncols, uint32_t nzt, uint32_t &s, uint32_t &e) {
-  if (a.seg == 3) {
-    const uint32_t col = uint32_t(p) * nb + lb;
-    if (p >= a.zparts || col >= ncols) return false;
-    s = col * nzt;
-    e = s + nzt;
+  if (a.seg == 3) { // a.zrounds rounds of a.zparts z parts over cm = nb / parts columns each
+    const uint32_t P = uint32_t(a.zparts), cm = nb / P, qq = lb / cm;
+    const uint32_t col = uint32_t(p) * cm + lb % cm;
+    if (p >= a.zrounds || col >= ncols) return false;
+    s = col * nzt + qq * nzt / P;
+    e = col * nzt + (qq + 1) * nzt / P;
     return true;
   }
   if (p > 1) return false;
@@ -1240,7 +1244,8 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     const X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
     if (tune.x2lockstep && ls.parts > 0) {
       a.seg = ls.rounds > 1 ? 3 : 2;
-      a.zparts = ls.rounds > 1 ? ls.rounds : ls.parts;
+      a.zparts = ls.parts;
+      a.zrounds = ls.rounds;
       blocks = uint32_t(ls.blocks);
     }
   } else {
@@ -1290,7 +1295,8 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
     const X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
     if (tune.x2lockstep && !tune.x2xfast && ls.parts > 0) {
       a.seg = ls.rounds > 1 ? 3 : 2;
-      a.zparts = ls.rounds > 1 ? ls.rounds : ls.parts;
+      a.zparts = ls.parts;
+      a.zrounds = ls.rounds;
       blocks = uint32_t(ls.blocks);
     }
   } else {

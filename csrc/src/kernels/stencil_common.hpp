@@ -49,7 +49,8 @@ template <typename T> struct StencilArgs {
   int gx, gy, gz;                   // logical grid
   int seg;                          // stencil7x2: 1 = balanced (column, plane) segments over gridDim.x blocks, 2 = lockstep
                                     // z parts, 3 = lockstep rounds of whole columns
-  int zparts;                       // stencil7x2 lockstep: z parts per column (seg 2; 4 = quarters) or rounds (seg 3)
+  int zparts;                       // stencil7x2 lockstep: z parts per column (4 = quarters)
+  int zrounds;                      // stencil7x2 lockstep rounds (seg 3)
   int xfast;                        // stencil7x2: 1 = column index x-major (x-adjacent columns on one XCD)
   int remap;                        // stencil7x2: 1 = XCD-aware block remap
   // spheres, raw coordinates

@@ -102,7 +102,9 @@ def test_x2_lockstep_schedule(st):
     assert f(256, 64, 512) == (4, 256, 1)     # 512^3: 64 row groups of 8, quarters
     assert f(248, 64, 508) == (4, 248, 1)     # overlap interior: 62 groups in lockstep, 2 as second segments
     assert f(256, 51, 407) == (5, 255, 1)     # 813x407x407: 51 groups x 5 parts of 81-82 planes
-    assert f(256, 81, 323) == (4, 256, 1)     # 645x645x323: quarters over 64 groups + 17 as second segments
+    assert f(256, 81, 323) == (4, 256, 1)     # 645x645x323 (odd): quarters over 64 groups + 17 as second segments
+    assert f(256, 102, 204) == (5, 255, 2)    # 813x813x204: 2 rounds x 51 groups x 5 parts
+    assert f(256, 70, 512) == (7, 245, 2)     # 2 rounds x 35 groups x 7 parts (245 >= 15/16 of 256)
     assert f(256, 41, 645) == (6, 246, 1)     # 645x323x645
     assert f(256, 128, 256) == (2, 256, 1)    # 1024x512x256 (512-cell columns: 2 x 64): two parts over whole columns
     assert f(256, 256, 256) == (1, 256, 1)    # one block per column
