@@ -20,3 +20,16 @@ def test_mtime_only_change_is_not_stale():
         assert not _build.is_stale()
     finally:
         os.utime(src, (st.st_atime, st.st_mtime))
+
+
+def test_no_build_tree_loads_shipped_artifacts(monkeypatch, tmp_path):
+    """a snapshot whose sources differ from the stamp but that has no configured build tree (a GPU box) must not try
+    to rebuild half-way: ensure_built() leaves the shipped artifacts to be loaded"""
+    monkeypatch.setattr(_build, "BUILD", str(tmp_path))
+    monkeypatch.setattr(_build, "is_stale", lambda: True)
+
+    def no_build(*a, **k):
+        raise AssertionError("build() called without a build tree")
+
+    monkeypatch.setattr(_build, "build", no_build)
+    _build.ensure_built()
