@@ -20,6 +20,7 @@ Steps:
     mpprof:<name>:<n>:<args>  same around an n-rank bench.py run
     pmc:<name>:<ctrs>:<cmd>   rocprofv3 --pmc <ctrs> (comma separated) around `python3 <cmd>`
     appprof:<name>:<app>:<args>  rocprofv3 --kernel-trace --stats around build/bin/<app> <args>
+    apppmc:<name>:<ctrs>:<app>:<args>  rocprofv3 --pmc <ctrs> around build/bin/<app> <args>
     py:<script>:<args>    python3 <script> <args>
 A step may start with environment assignments: "GPU_MAX_HW_QUEUES=2,STENCIL_LOG_LEVEL=3@mp:8:--per-gpu 128".
 """
@@ -79,6 +80,15 @@ def step_cmd(step: str, out: str, k: int):
         os.makedirs(d, exist_ok=True)
         pre = ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "run_%pid%", "--output-format", "csv", "--"]
         return f"appprof_{name}", pre + [os.path.join(REPO, "build/bin", app), *shlex.split(args)], 300
+    if kind == "apppmc":
+        name, _, rest2 = rest.partition(":")
+        ctrs, _, rest3 = rest2.partition(":")
+        app, _, args = rest3.partition(":")
+        d = os.path.join(out, name)
+        os.makedirs(d, exist_ok=True)
+        pre = ["rocprofv3", "--pmc", *ctrs.split(","), "--kernel-trace", "-d", d, "-o", "run_%pid%",
+               "--output-format", "csv", "--"]
+        return f"apppmc_{name}", pre + [os.path.join(REPO, "build/bin", app), *shlex.split(args)], 120
     if kind in ("prof", "mpprof", "pmc"):
         name, _, rest2 = rest.partition(":")
         d = os.path.join(out, name)
