@@ -524,6 +524,8 @@ def test_temporal2_row_kernel_lockstep_quarters(st, fake, reserve, lockstep, alt
                                        ((1024, 128, 128), False),
                                        # 70 row groups: 2 rounds x 35 groups x 7 parts
                                        ((512, 560, 112), False),
+                                       # 81 row groups: quarters over 64 + 17 leftover groups as second segments
+                                       ((512, 648, 240), False),
                                        # more row groups than blocks: rounds of whole columns (seg 3)
                                        ((512, 2112, 16), False), ((2048, 1040, 16), False), ((1024, 1040, 16), True)])
 def test_temporal2_row_kernel_lockstep_parts(st, size, fp64):
