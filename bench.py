@@ -11,7 +11,12 @@ link); --grid cbrt runs the reference's cube rule (512 * N^0.33333 per axis: 645
 Secondary numbers in the JSON line: the halo-exchange GB/s of an exchange-only loop on the same decomposition
 (bin/bench_exchange.cu definition: aggregate halo bytes / time).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]     (N>1: launched by torch.distributed.run)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  N>1 runs one rank per GPU. Under torch.distributed.run (WORLD_SIZE set) it must equal WORLD_SIZE; without a
+  launcher, bench.py itself spawns N fresh child ranks (stencil2_amd/launch.py, loaded by path) before importing
+  torch or touching the GPU, waits for them with a bounded timeout, stops every sibling when one fails and exits with
+  the failing rank's code. Rank 0 prints the JSON line (reference: one rank per GPU from the job script,
+  scripts/summit/weak_256n.sh:26-30).
 """
 from __future__ import annotations
 
@@ -61,6 +66,145 @@ def weak_grid(st, per_gpu: int, n: int, rule: str, axis_cost, objective) -> tupl
     return grid
 
 
+def transport_sweep(st, torch, dist, args, world, device, red_dev, axis_cost, objective, topt_base):
+    """Exchange-only GB/s of the headline decomposition with each transport set in turn, plus the reference-rule
+    point (the cbrt cube cut by the reference's greedy Interface rule with equal axis costs: 2x2x2 at N = 8, the
+    bench_exchange --x 1024 --y 1024 --z 1024 --fr 2 config), so one multi-GPU run yields the whole ladder
+    (reference: src/stencil.cu:163-194 method ladder; scripts/summit/weak_256n.sh:26-30 per-method sweeps).
+
+    Radius-2 faces, one fp32 quantity (the depth-2 exchange of a fused pair), blocking exchange()+swap() as in
+    bin/bench_exchange.cu:39-63 and the same exchanges stream-ordered. Each entry realizes its own domain on a fresh
+    native process group with a short timeout, so a transport that fails on one rank costs that entry (an "error"
+    string), not the run. The number of timed exchanges is agreed over ranks from a timed probe exchange, and the
+    whole section stops starting entries after --sweep-budget seconds."""
+    M = st.MethodFlags
+    C = st.TransportOptions.Completion
+    sets = [("colo_store", M.Colocated | M.Kernel, "store", C.Kernel),
+            ("colo_engine", M.Colocated | M.Kernel, "engine", C.Kernel),
+            ("colo_ipcevent", M.Colocated | M.Kernel, "store", C.IpcEvent),
+            ("rccl", M.Rccl | M.Kernel, "store", C.Kernel), ("staged", M.Staged | M.Kernel, "store", C.Kernel),
+            ("ref_rule", M.All, "store", C.Kernel)]
+    out = {}
+    t_start = time.perf_counter()
+
+    def agreed_max(v):
+        t = torch.tensor([float(v)], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    for name, m, copy, completion in sets:
+        if agreed_max(time.perf_counter() - t_start) > args.sweep_budget:
+            out[name] = {"skipped": f"sweep budget {args.sweep_budget:.0f} s spent"}
+            continue
+        rec = {}
+        ok = 1.0
+        dd = None
+        try:
+            if name == "ref_rule":
+                L = st.models.weak_scaled_size(args.per_gpu, world)
+                g, obj, cost = (L, L, L), st.PartitionObjective.Interface, (1, 1, 1)
+            else:
+                g, obj, cost = weak_grid(st, args.per_gpu, world, args.grid, axis_cost, objective), objective, axis_cost
+            grp = st.init_process_group(set_default=False, timeout_s=max(30.0, args.sweep_budget))
+            dd = st.DistributedDomain(*g, group=grp)
+            r = st.Radius.constant(0)
+            r.set_face(2)
+            dd.set_radius(r)
+            dd.add_data("q", torch.float32)
+            dd.set_methods(m)
+            dd.set_gpus([device])
+            dd.set_axis_cost(st.Dim3(*cost))
+            dd.set_partition_objective(obj)
+            dd.set_plan_file("")
+            topt = st.TransportOptions()
+            topt.inbox = topt_base.inbox
+            topt.completion = completion
+            topt.fuse_flags = topt_base.fuse_flags
+            topt.colo_copy = topt.Copy.Engine if copy == "engine" else topt.Copy.Store
+            topt.wait_timeout = max(30.0, args.sweep_budget)
+            dd.set_transport_options(topt)
+            dd.realize()
+            pd = dd.placement_dim()
+            rec["grid"] = list(g)
+            rec["decomposition"] = f"{pd.x}x{pd.y}x{pd.z}"
+            rec["asked"] = st.methods_to_string(m)
+            rec["realized"] = st.methods_to_string(dd.methods())
+            rec["bytes_by_method"] = {st.methods_to_string(f): int(dd.exchange_bytes_for_method(f))
+                                      for f in (M.Kernel, M.PeerCopy, M.Colocated, M.Rccl, M.Staged)
+                                      if dd.exchange_bytes_for_method(f) > 0}
+            xbytes = dd.exchange_bytes_for_method(M.All)
+            for _ in range(2):
+                dd.exchange()
+                dd.swap()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            dd.exchange()
+            dd.swap()
+            probe = agreed_max(time.perf_counter() - t)
+            iters = int(max(1, min(args.exchange_iters, 1.0 / max(probe, 1e-6))))
+            colo = dd.exchange_bytes_for_method(M.Colocated) > 0 and completion != C.StreamOp
+            if colo:
+                dd.set_transport_log(iters)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t = time.perf_counter()
+            for _ in range(iters):
+                dd.exchange()
+                dd.swap()
+            el = agreed_max(time.perf_counter() - t)
+            if colo:
+                rec["colo_kernels_us"] = colo_breakdown(dd.transport_log(0))
+                dd.set_transport_log(0)
+            xs = torch.cuda.Stream()
+            dd.exchange_async(xs.cuda_stream, 0)
+            dd.swap()
+            xs.synchronize()
+            dd.sync_exchange()
+            if world > 1:
+                dist.barrier()
+            t = time.perf_counter()
+            for _ in range(iters):
+                dd.exchange_async(xs.cuda_stream, 0)
+                dd.swap()
+            xs.synchronize()
+            dd.sync_exchange()
+            el2 = agreed_max(time.perf_counter() - t)
+            rec.update({"iters": iters, "halo_bytes": int(xbytes), "exchange_ms": round(el / iters * 1e3, 4),
+                        "GBps": round(xbytes * iters / el / 1e9, 3),
+                        "stream_GBps": round(xbytes * iters / el2 / 1e9, 3)})
+        except Exception as e:  # noqa: BLE001 -- one transport failing must not end the run
+            ok = 0.0
+            rec["error"] = f"{type(e).__name__}: {str(e)[:300]}"
+        del dd
+        if agreed_max(1.0 - ok) > 0 and "error" not in rec:
+            rec["error"] = "failed on another rank"
+        out[name] = rec
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(f"[bench] transport {name}: {rec}", file=sys.stderr, flush=True)
+    return out
+
+
+def colo_breakdown(log) -> dict:
+    """Median phases (us) of the fused co-located transport kernels from DistributedDomain.transport_log: per
+    exchange {send start, after the credit wait, after the copies, signal, recv start, after the arrival wait, after
+    the copies, signal} in 100-MHz ticks (0: that kernel did not run / that phase does not exist)."""
+    import statistics
+
+    def med(vals):
+        vals = [v for v in vals if v is not None and v >= 0]
+        return round(statistics.median(vals) / 100.0, 2) if vals else None
+
+    def ph(e, a, b):
+        return e[b] - e[a] if e[a] and e[b] else None
+
+    return {"send_wait": med([ph(e, 0, 1) for e in log]), "send_copy": med([ph(e, 1, 2) for e in log]),
+            "send_signal": med([ph(e, 2, 3) for e in log]), "recv_wait": med([ph(e, 4, 5) for e in log]),
+            "recv_copy": med([ph(e, 5, 6) for e in log]), "recv_signal": med([ph(e, 6, 7) for e in log]),
+            "send_end_to_recv_start": med([ph(e, 3, 4) for e in log]), "exchanges": len(log)}
+
+
 def _gpus_sysfs() -> int:
     """GPUs of this node from the KFD topology (no HIP call: the HIP runtime must not start before the queue limit
     below is set)."""
@@ -86,8 +230,43 @@ def _limit_queues_when_sharing():
         os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, 8 // per_gpu))
 
 
+def _launcher():
+    """stencil2_amd/launch.py without importing the package (its __init__ imports torch and the HIP runtime)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stencil2_amd", "launch.py")
+    spec = importlib.util.spec_from_file_location("_stencil2_launch", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def rank_setup(gpus: int, launch_timeout: float, argv: list[str]):
+    """None: this process is a rank (run the bench). An int: the exit code of this process (a spawning parent, or a
+    --gpus / WORLD_SIZE mismatch). Runs before torch is imported: no HIP call may precede the fork."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if gpus <= 1:
+            return None
+        return _launcher().spawn_ranks([sys.executable, os.path.abspath(__file__), *argv], gpus,
+                                       timeout=launch_timeout if launch_timeout > 0 else None)
+    if int(world) != gpus:
+        print(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: the launcher and the bench disagree on the number "
+              f"of GPUs; refusing to time a different job than the one asked for", file=sys.stderr, flush=True)
+        return 2
+    if os.environ.get("STENCIL_BENCH_DRY"):  # launcher tests (CPU): report the rank layout, touch nothing else
+        rank = int(os.environ.get("RANK", "0"))
+        if os.environ.get("STENCIL_BENCH_DRY_FAIL_RANK") == str(rank):
+            return 3
+        if os.environ.get("STENCIL_BENCH_DRY_SLEEP"):
+            time.sleep(float(os.environ["STENCIL_BENCH_DRY_SLEEP"]))
+        print(json.dumps({"rank": rank, "world": int(world), "local_rank": int(os.environ.get("LOCAL_RANK", "-1")),
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
+                          "torch_loaded": "torch" in sys.modules}), flush=True)
+        return 0
+    return None
+
+
 def main():
-    _limit_queues_when_sharing()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -139,8 +318,9 @@ def main():
                          "left the store path 3.5x slower afterwards (profiles/r3/check4), so they are opt-in")
     ap.add_argument("--inbox", choices=["uncached", "fine", "coarse"], default="uncached",
                     help="memory of the co-located receive slots (TransportOptions.inbox)")
-    ap.add_argument("--completion", choices=["kernel", "streamop"], default="kernel",
-                    help="co-located arrival/credit signalling: bounded spin kernels or hipStreamWait/WriteValue64")
+    ap.add_argument("--completion", choices=["kernel", "streamop", "ipcevent"], default="kernel",
+                    help="co-located arrival/credit signalling: bounded spin kernels, hipStreamWait/WriteValue64, or "
+                         "interprocess events with host notify/ack (the reference's design)")
     ap.add_argument("--fuse-flags", type=int, default=1,
                     help="co-located flag waits/signals folded into the pack/unpack kernels (0: separate kernels)")
     ap.add_argument("--self-test", type=int, default=1,
@@ -148,7 +328,18 @@ def main():
                          "Colocated -> Rccl -> Staged until every halo arrives correctly")
     ap.add_argument("--tune-steps", type=int, default=8,
                     help="steps per timed round of the overlap choice (auto, remote halos only; 0 = no choice)")
+    ap.add_argument("--transport-sweep", choices=["auto", "on", "off"], default="auto",
+                    help="after the headline: exchange-only GB/s of every transport set on the same decomposition "
+                         "and of the reference-rule cube (auto: only with N > 1)")
+    ap.add_argument("--sweep-budget", type=float, default=30.0,
+                    help="seconds after which the transport sweep starts no further entry")
+    ap.add_argument("--launch-timeout", type=float, default=3000,
+                    help="--gpus N>1 without a launcher: seconds before the spawned ranks are stopped (0 = none)")
     args = ap.parse_args()
+    rc = rank_setup(args.gpus, args.launch_timeout, sys.argv[1:])
+    if rc is not None:
+        return rc
+    _limit_queues_when_sharing()
 
     import torch
     import torch.distributed as dist
@@ -198,7 +389,8 @@ def main():
     topt = st.TransportOptions()
     topt.inbox = {"uncached": topt.Inbox.Uncached, "fine": topt.Inbox.Fine, "coarse": topt.Inbox.Coarse}[args.inbox]
     topt.colo_copy = topt.Copy.Engine if args.colo_copy == "engine" else topt.Copy.Store
-    topt.completion = topt.Completion.StreamOp if args.completion == "streamop" else topt.Completion.Kernel
+    topt.completion = {"kernel": topt.Completion.Kernel, "streamop": topt.Completion.StreamOp,
+                       "ipcevent": topt.Completion.IpcEvent}[args.completion]
     topt.fuse_flags = bool(args.fuse_flags)
     if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # rehearses the fallback (scripts): IPC probe reports failure
         topt.fail_ipc_probe = True
@@ -344,6 +536,24 @@ def main():
         dist.all_reduce(tx2, op=dist.ReduceOp.MAX)
     xgbs_stream = xbytes * args.exchange_iters / float(tx2.item()) / 1e9
 
+    pdim = model.domain.placement_dim()
+    model_cfg = {
+        "decomposition": f"{pdim.x}x{pdim.y}x{pdim.z}", "methods": st.methods_to_string(methods), "preflight": preflight,
+        "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
+        "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
+        "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched,
+        "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
+        "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none",
+        "transport": {"inbox": args.inbox,
+                      "colo_copy": str(model.domain.transport_options().colo_copy).split(".")[-1].lower(),
+                      "completion": args.completion, "fuse_flags": bool(args.fuse_flags)},
+    }
+    del dd
+    del model
+    transports = None
+    if args.transport_sweep == "on" or (args.transport_sweep == "auto" and world > 1):
+        transports = transport_sweep(st, torch, dist, args, world, device, red_dev, axis_cost, objective, topt)
+
     if rank == 0:
         out = {
             "metric": "Jacobi3D Gcells/s (512^3/GPU weak scaling; halo-exchange GB/s in extra)",
@@ -361,22 +571,14 @@ def main():
             "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": max(grid),
                        "grid": list(grid), "grid_rule": args.grid, "partition": args.partition, "per_gpu": args.per_gpu, "radius": 1,
                        "parallelism": f"domain-decomp{n}",
-                       "decomposition": "x".join(str(v) for v in (model.domain.placement_dim().x,
-                                                                   model.domain.placement_dim().y,
-                                                                   model.domain.placement_dim().z)), "methods": st.methods_to_string(methods), "preflight": preflight,
-                       "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned, "nontemporal": bool(args.nt), "alternate_z": bool(args.altz),
-                       "ty": args.ty, "nw": args.nw, "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched, "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
-                       "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none",
-                       "transport": {"inbox": args.inbox, "colo_copy": str(model.domain.transport_options().colo_copy).split(".")[-1].lower(),
-                                     "completion": args.completion, "fuse_flags": bool(args.fuse_flags)},
+                       **model_cfg,
                        "build": st.build_info()["git_sha"]},
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_exchange_stream_GBps": round(xgbs_stream, 3),
                       "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
-                      "gcells_per_gpu": round(gcells / n, 3)},
+                      "gcells_per_gpu": round(gcells / n, 3), "transports": transports},
         }
         print(json.dumps(out), flush=True)
-    del model
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,0 +1,25 @@
+#pragma once
+// Interprocess HIP events between co-located ranks: the primitive of TransportOptions::Completion::IpcEvent.
+// Parity: reference test/test_cuda_mpi_cudaipc.cu:8-45 (create an interprocess event on rank 0, send its handle, open
+// it on rank 1) and tx_cuda.cuh:231-240 / :366-372 (record after the copy, cudaStreamWaitEvent before the unpack).
+#include <string>
+
+#include "stencil/comm/proc_group.hpp"
+
+namespace stencil {
+
+struct IpcEventReport {
+  bool ok = false;
+  double spinS = 0;   // how long rank 0's GPU was kept busy before it recorded the event
+  double waitedS = 0; // receivers: host time from the notify until their stream (waiting on the event) drained
+  std::string error;
+};
+
+// Collective over every rank of `pg` (all on one node): rank 0 creates an interprocess event (hipEventDisableTiming |
+// hipEventInterprocess), sends its handle to every other rank, which opens it (hipIpcOpenEventHandle). Rank 0 then
+// keeps its GPU busy for `spinS` seconds, records the event behind that work and notifies the others at once; each
+// receiver orders a marker on its stream after hipStreamWaitEvent on the opened event and measures how long the
+// stream takes to drain. ok: every handle opened and every receiver's wait covered (most of) the spin.
+IpcEventReport ipc_event_roundtrip(comm::ProcGroup &pg, int device, double spinS);
+
+} // namespace stencil

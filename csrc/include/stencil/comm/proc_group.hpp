@@ -44,6 +44,11 @@ public:
   // receive timeout of blocking recv / collectives (seconds)
   virtual void set_timeout(double timeout_s) { (void)timeout_s; }
   virtual double timeout() const { return 0; }
+  // collective: a new group over the same ranks with its own connections, mailboxes and collective sequence, whose
+  // blocking receives give up after timeout_s. Work that may fail on some ranks only (the transport self-test probe)
+  // runs on a fork: when one rank abandons it mid-sequence, the others time out there and this group's own
+  // collective sequence stays in step. A size-1 group returns itself.
+  virtual std::shared_ptr<ProcGroup> fork(double timeout_s) = 0;
   virtual void bcast(void *buf, size_t n, int root) = 0;
   virtual void allgather(const void *in, size_t n, void *out) = 0;                           // out: size()*n bytes
   virtual void gatherv(const void *in, size_t n, std::vector<std::vector<char>> *out, int root) = 0; // root only

@@ -19,6 +19,9 @@ enum class MsgKind : uint32_t {
   IpcCredit = 2, // HIP IPC handle of a sender's credit block
   Probe = 3,     // pre-flight IPC probe
   Ctrl = 4,      // anything else (checkpoint/metadata)
+  IpcEvent = 5,  // HIP IPC handle of a sender's interprocess event (Completion::IpcEvent)
+  Notify = 6,    // "recorded epoch e" from a sender (reference MsgKind::Notify, tx_common.hpp)
+  Ack = 7,       // "waited on epoch e" from a receiver (keeps a sender from re-recording an event too early)
 };
 
 constexpr int kTagPairBits = 28;

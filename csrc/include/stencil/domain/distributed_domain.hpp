@@ -33,6 +33,8 @@
 
 namespace stencil {
 
+constexpr int kTransportLogWords = 8; // set_transport_log: stamps per exchange
+
 enum class MethodFlags : int {
   None = 0,
   Staged = 1,    // reference CudaMpi
@@ -73,7 +75,9 @@ struct TransportOptions {
   //   Uncached  hipDeviceMallocUncached: every access bypasses the caches (coherent by construction; the unpack
   //             reads the slots from HBM without L2 reuse)
   //   Fine      hipDeviceMallocFinegrained: coherent at system scope, cached with the fine-grained MTYPE
-  //   Coarse    hipMalloc: L2-cached; relies on the kernel-boundary cache invalidate of the unpack's dispatch
+  //   Coarse    hipMalloc: L2-cached; relies on the kernel-boundary cache invalidate of the unpack's dispatch, so
+  //             its arrival wait always runs as a separate kernel before the unpack (fuseFlags applies to the
+  //             send side only)
   enum class Inbox : int { Uncached = 0, Fine = 1, Coarse = 2 };
   Inbox inbox = Inbox::Uncached;
   // How a packed message reaches another GPU's memory (Colocated: the peer's IPC-mapped inbox; PeerCopy: the peer
@@ -90,7 +94,15 @@ struct TransportOptions {
   //             kernel releases + stores it
   //   StreamOp  hipStreamWaitValue64 / hipStreamWriteValue64 (the command processor waits; no CU is held, but the
   //             wait itself is unbounded: sync_exchange's host watchdog reports a stall)
-  enum class Completion : int { Kernel = 0, StreamOp = 1 };
+  //   IpcEvent  the reference's design (tx_cuda.cuh:231-240, :351, :366-372): the sender records an interprocess
+  //             event (hipIpcGetEventHandle, opened once by the receiver) after its stores / engine copy and sends a
+  //             host Notify(epoch); the receiver, on the notify, orders its unpack with hipStreamWaitEvent on that
+  //             event and answers Ack(epoch). Arrival therefore costs a host message per channel per exchange; the
+  //             double-buffered inbox keeps its device credit flags (the reference's missing ack),
+  //             and a sender records epoch e only after the receiver acknowledged e-2 (an event may only be
+  //             re-recorded once the wait that needs the older record has been enqueued). Requires realize() with
+  //             this completion (the events are created there); not capturable into a hipGraph.
+  enum class Completion : int { Kernel = 0, StreamOp = 1, IpcEvent = 2 };
   Completion completion = Completion::Kernel;
   // Kernel completion: fold the flag waits / signals into the pack and unpack kernels (one launch per side instead
   // of three; copy_plan_device_sync). Engine copies keep a separate credit wait and arrival signal around the copies.
@@ -107,6 +119,12 @@ struct TransportOptions {
   bool failIpcProbe = false;
   // test hook: RCCL communicator creation reports failure on this rank (rehearses the RCCL -> staged fallback)
   bool failRcclInit = false;
+  // test hook: PeerCopy engine pipes between sub-domains on the SAME device also go through hipMemcpyPeerAsync
+  // (src device == dst device is legal), so the cross-GPU peer-copy call runs on a one-GPU box
+  bool peerApiSameDevice = false;
+  // test hook: the first transport self-test probe of this rank throws after realize (the other ranks then time out
+  // on the probe's forked group; the ladder must go on in step on every rank)
+  int failProbeRank = -1;
   // sleep a random 0..jitterUs microseconds between transport phases of every exchange (race canary; reference's
   // unused rand_sleep(), packer.cuh:17-20)
   int jitterUs = 0;
@@ -283,6 +301,14 @@ public:
   bool gated_send_supported(int skipAxes) const;
   void swap();
 
+  // ---- transport log (wait vs copy of the fused co-located kernels) ----
+  // keep the last `exchanges` exchanges' device timestamps (s_memrealtime, 100-MHz constant clock) of every fused
+  // Colocated pack / unpack kernel: per exchange {send start, send after credit wait, send after copies, send
+  // signal, recv start, recv after arrival wait, recv after copies, recv signal}; 0 where no such kernel ran.
+  // 0 turns the log off. transport_log(dev) returns the logged exchanges of local device slot `dev`, oldest first.
+  void set_transport_log(int exchanges);
+  std::vector<std::array<uint64_t, kTransportLogWords>> transport_log(size_t dev = 0);
+
   // ---- output ----
   void write_paraview(const std::string &prefix, bool zeroNaNs = false);
   // binary checkpoint of every local sub-domain's interior (curr buffers): `prefix_<rank>_<di>.ckpt`, one file per
@@ -321,6 +347,7 @@ private:
   TransportOptions topt_;
   bool selfTest_ = false;
   std::string selfTestReport_;
+  int probeFailures_ = 0; // TransportOptions::failProbeRank bookkeeping
   // set when an exchange failed fatally (device wait timed out, RCCL error/timeout): every later exchange refuses to
   // run instead of handing a torn-down transport to the GPU
   std::string poisoned_;

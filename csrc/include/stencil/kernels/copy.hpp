@@ -95,10 +95,12 @@ void wait_flags_device(const std::vector<uint64_t *> &flags, uint64_t target, in
 // System-scope release, then lane i stores *flags[i] = value (flags may be IPC-mapped peer memory).
 void signal_flags_device(const std::vector<uint64_t *> &flags, uint64_t value, hipStream_t stream);
 constexpr int kMaxFlagsPerLaunch = 64;
-// Grid cap of the fused wait + copy + signal kernels: every block spins until the peer's flags arrive, and a
-// spinning block holds its CU. Uncapped (one 1024-thread block per CU) two ranks sharing a GPU could fill every CU
-// slot with waiting blocks while the peers they wait for cannot start their pack kernels: four ranks on one MI355X
-// (1x2x2) deadlocked until the wait timeout (gpurun_out/r3e, r3). 32 CUs still move a 2-MiB face in a few us.
+// Grid cap of the fused wait + copy + signal kernels on a GPU that other ranks drive too: every block spins until
+// the peer's flags arrive, and a spinning block holds its CU. Uncapped (one 1024-thread block per CU) two ranks
+// sharing a GPU could fill every CU slot with waiting blocks while the peers they wait for cannot start their pack
+// kernels: four ranks on one MI355X (1x2x2) deadlocked until the wait timeout (gpurun_out/r3e, r3). 32 CUs still
+// move a 2-MiB face in a few us. A GPU this rank drives alone has no such peer on its CUs: there the grid is only
+// bounded by the work and the caller's maxBlocks (FlagSyncArgs::sharedGpu = false).
 constexpr int kFusedMaxBlocks = 32;
 // One fused launch: wait until every `wait` flag >= waitTarget (bounded: on timeout `code` goes to *err), run the
 // copy plan on at most maxBlocks 1024-thread blocks (0: up to one per CU), then release-store signalValue into every
@@ -116,7 +118,16 @@ struct FlagSyncArgs {
   int *err = nullptr;
   int code = 0;
   double timeout_s = 60;
+  bool sharedGpu = true; // another rank drives this GPU: cap the grid at kFusedMaxBlocks
+  // STENCIL_EXCHANGE_STATS builds: when non-null, block 0 stores s_memrealtime stamps (100-MHz constant clock) at
+  // kernel start, after the flag wait and after its copies into stamps[0..2], and the last block its signal time
+  // into stamps[3] (wait vs copy breakdown of the fused transport kernels)
+  uint64_t *stamps = nullptr;
 };
 void copy_plan_device_sync(const CopyPlan &p, hipStream_t stream, int maxBlocks, const FlagSyncArgs &a);
+
+// one wave that keeps the stream busy for `seconds` of the 100-MHz constant clock (tests: work an event is recorded
+// behind); 0 = an empty marker kernel
+void spin_device(double seconds, hipStream_t stream);
 
 } // namespace stencil

@@ -8,6 +8,7 @@
 #include <cstring>
 
 #include "stencil/comm/proc_group.hpp"
+#include "stencil/comm/ipc_event.hpp"
 #include "stencil/comm/rccl_comm.hpp"
 #include "stencil/domain/distributed_domain.hpp"
 #include "stencil/kernels/copy.hpp"
@@ -292,6 +293,22 @@ PYBIND11_MODULE(_C, m) {
   m.def("default_group", &comm::default_group, py::call_guard<py::gil_scoped_release>());
   m.def("set_default_group", &comm::set_default_group);
   m.def("find_free_port", &comm::find_free_port);
+  m.def(
+      "ipc_event_roundtrip",
+      [](std::shared_ptr<comm::ProcGroup> g, int device, double spin) {
+        IpcEventReport r;
+        {
+          py::gil_scoped_release nogil;
+          r = ipc_event_roundtrip(*g, device, spin);
+        }
+        py::dict d;
+        d["ok"] = r.ok;
+        d["spin_s"] = r.spinS;
+        d["waited_s"] = r.waitedS;
+        d["error"] = r.error;
+        return d;
+      },
+      py::arg("group"), py::arg("device") = 0, py::arg("spin_s") = 0.2);
 
   // ---------------- topology / placement ----------------
   m.def("prime_factors", &prime_factors_desc);
@@ -469,7 +486,8 @@ PYBIND11_MODULE(_C, m) {
       .value("Engine", TransportOptions::Copy::Engine);
   py::enum_<TransportOptions::Completion>(topt, "Completion")
       .value("Kernel", TransportOptions::Completion::Kernel)
-      .value("StreamOp", TransportOptions::Completion::StreamOp);
+      .value("StreamOp", TransportOptions::Completion::StreamOp)
+      .value("IpcEvent", TransportOptions::Completion::IpcEvent);
   topt.def(py::init<>())
       .def_readwrite("inbox", &TransportOptions::inbox)
       .def_readwrite("colo_copy", &TransportOptions::coloCopy)
@@ -481,6 +499,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ipc_probe", &TransportOptions::ipcProbe)
       .def_readwrite("fail_ipc_probe", &TransportOptions::failIpcProbe)
       .def_readwrite("fail_rccl_init", &TransportOptions::failRcclInit)
+      .def_readwrite("fail_probe_rank", &TransportOptions::failProbeRank)
+      .def_readwrite("peer_api_same_device", &TransportOptions::peerApiSameDevice)
       .def_readwrite("jitter_us", &TransportOptions::jitterUs)
       .def_readwrite("spin_wait", &TransportOptions::spinWait)
       .def_readwrite("numa_affinity", &TransportOptions::numaAffinity)
@@ -575,6 +595,9 @@ PYBIND11_MODULE(_C, m) {
         o.nullStreamProducers = on;
         d.set_transport_options_live(o);
       })
+      .def("set_transport_log", &DistributedDomain::set_transport_log, py::call_guard<py::gil_scoped_release>())
+      .def("transport_log", &DistributedDomain::transport_log, py::arg("dev") = 0,
+           py::call_guard<py::gil_scoped_release>())
       .def("poisoned", &DistributedDomain::poisoned)
       .def("numa_node", &DistributedDomain::numa_node)
       .def("set_self_test", &DistributedDomain::set_self_test)

@@ -136,6 +136,8 @@ struct Channel {
   char *ownFlag = nullptr, *ownData = nullptr;
   char *remoteFlag = nullptr, *remoteData = nullptr;
   int64_t slotStride = 0;
+  // Completion::IpcEvent: the sender's interprocess event (send channel) / the opened peer event (receive channel)
+  hipEvent_t ipcEvent = nullptr;
 };
 
 // PeerCopy over a DMA engine (TransportOptions::peerCopy == Engine): every message from one local sub-domain to
@@ -170,6 +172,8 @@ struct DevCtx {
   std::vector<Stream> copyStreams;
   std::vector<Event> copyJoin;
   uint32_t *syncCounter = nullptr; // [0] colo send, [1] colo receive: block counters of the fused transport kernels
+  bool sharedGpu = false;          // another rank drives this GPU too (fused transport kernels stay capped)
+  uint64_t *xlog = nullptr;        // set_transport_log: kTransportLogWords stamps per exchange, a ring of xlogCap
   SegList rcclPack, rcclUnpack;   // variant = parity
   SegList stagedPack, stagedUnpack;
   rccl::Comm nccl = nullptr;
@@ -202,6 +206,11 @@ struct DistributedDomain::Impl {
   bool engineRefused = false; // hipMemcpyDeviceToDeviceNoCU not accepted by the runtime (warned once)
   uint64_t *gateCounter = nullptr; // set_send_gate: consumed by the next exchange_async
   uint64_t gateTarget = 0;
+  bool ipcEvents = false;            // Completion::IpcEvent events were created by realize()
+  uint64_t ipcEventFirstEpoch = 0;  // first exchange in IpcEvent mode since the last set_completion (acks before it
+                                    // were never sent)
+  int xlogCap = 0;                  // set_transport_log ring size (exchanges)
+  uint64_t xlogFirstEpoch = 0;      // first epoch logged since the last set_transport_log
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -247,6 +256,7 @@ DistributedDomain::~DistributedDomain() {
   for (auto &c : I.chans) {
     if (c.dbuf) (void)hipFree(c.dbuf);
     if (c.hbuf) (void)hipHostFree(c.hbuf);
+    if (c.ipcEvent) (void)hipEventDestroy(c.ipcEvent);
     if (c.remoteFlag) (void)hipIpcCloseMemHandle(c.remoteFlag);
     if (c.remoteData) (void)hipIpcCloseMemHandle(c.remoteData);
   }
@@ -273,6 +283,7 @@ DistributedDomain::~DistributedDomain() {
       d.pipeUnpack[k].release();
     }
     if (d.syncCounter) (void)hipFree(d.syncCounter);
+    if (d.xlog) (void)hipFree(d.xlog);
     d.coloUnpack.release();
     d.rcclPack.release();
     d.rcclUnpack.release();
@@ -330,71 +341,82 @@ int64_t DistributedDomain::probe_transports(MethodFlags m) {
   int64_t rmax = 1;
   for (int i = 0; i < 27; ++i) rmax = std::max<int64_t>(rmax, radius_.dir(dir_from_index(i)));
   auto shrink = [&](int64_t n) { return std::min<int64_t>(n, std::max<int64_t>((n + 15) / 16, 6 * rmax + 2)); };
-  DistributedDomain p(shrink(size_.x), shrink(size_.y), shrink(size_.z), pg_);
-  p.set_radius(radius_);
-  p.set_boundary(boundary_);
-  p.set_methods(m);
-  p.set_placement(strategy_);
-  p.set_axis_cost(axisCost_);
-  p.set_partition_objective(objective_);
-  if (!gpus_.empty()) p.set_gpus(gpus_);
-  if (backendSet_) p.set_backend(backend_);
-  p.set_transport_options(topt_);
-  p.set_plan_file("");
-  p.add_data(4, "probe", DType::I32);
+  // the probe runs on a fork of the group: a rank whose probe fails (an exception anywhere in realize / exchange)
+  // abandons the fork mid-sequence and goes straight to the verdict below; the other ranks' next receive on the
+  // fork then times out after waitTimeout, they fail too and join the verdict, and this group's own collective
+  // sequence never goes out of step
+  const double forkTimeout = std::max(1.0, topt_.waitTimeout);
+  std::shared_ptr<comm::ProcGroup> grp = pg_->size() > 1 ? pg_->fork(forkTimeout) : pg_;
   int64_t bad = 0;
-  try {
-    p.realize();
-    const Dim3 L = p.size();
-    for (int it = 0; it < 2; ++it) {
-      const int32_t off = 7 * it;
-      for (auto &d : p.domains_) {
-        const Dim3 raw = d.raw_size(), org = d.accessor_origin();
-        std::vector<int32_t> v(size_t(raw.flatten()), kProbePoison);
-        const Rect3 cr = d.get_compute_region();
-        for (int64_t z = 0; z < raw.z; ++z)
-          for (int64_t y = 0; y < raw.y; ++y)
-            for (int64_t x = 0; x < raw.x; ++x)
-              if (cr.contains(Dim3(org.x + x, org.y + y, org.z + z)))
-                v[size_t(x + raw.x * (y + raw.y * z))] = probe_key(org.x + x, org.y + y, org.z + z, L, off);
-        d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), true);
-        d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), false);
-      }
-      p.exchange();
-      for (auto &d : p.domains_) {
-        const Dim3 raw = d.raw_size(), org = d.accessor_origin();
-        const Rect3 cr = d.get_compute_region();
-        const auto bytes = d.region_to_host(Dim3(0, 0, 0), raw, 0, true);
-        const int32_t *got = reinterpret_cast<const int32_t *>(bytes.data());
-        for (int64_t z = 0; z < raw.z; ++z)
-          for (int64_t y = 0; y < raw.y; ++y)
-            for (int64_t x = 0; x < raw.x; ++x) {
-              const int64_t g[3] = {org.x + x, org.y + y, org.z + z};
-              const int64_t lo[3] = {cr.lo.x, cr.lo.y, cr.lo.z}, hi[3] = {cr.hi.x, cr.hi.y, cr.hi.z};
-              const int64_t n[3] = {L.x, L.y, L.z};
-              int dd[3];
-              bool crossesClosed = false;
-              for (int a = 0; a < 3; ++a) {
-                dd[a] = g[a] >= hi[a] ? 1 : (g[a] < lo[a] ? -1 : 0);
-                if ((g[a] < 0 || g[a] >= n[a]) &&
-                    !boundary_.face_periodic(a == 0 ? dd[a] : 0, a == 1 ? dd[a] : 0, a == 2 ? dd[a] : 0))
-                  crossesClosed = true;
+  {
+    DistributedDomain p(shrink(size_.x), shrink(size_.y), shrink(size_.z), grp);
+    p.set_radius(radius_);
+    p.set_boundary(boundary_);
+    p.set_methods(m);
+    p.set_placement(strategy_);
+    p.set_axis_cost(axisCost_);
+    p.set_partition_objective(objective_);
+    if (!gpus_.empty()) p.set_gpus(gpus_);
+    if (backendSet_) p.set_backend(backend_);
+    p.set_transport_options(topt_);
+    p.set_plan_file("");
+    p.add_data(4, "probe", DType::I32);
+    try {
+      p.realize();
+      if (topt_.failProbeRank == rank() && probeFailures_++ == 0) // test hook: this rank's first probe fails alone
+        LOG_FATAL("TransportOptions::failProbeRank: probe failure forced on rank " << rank());
+      const Dim3 L = p.size();
+      for (int it = 0; it < 2; ++it) {
+        const int32_t off = 7 * it;
+        for (auto &d : p.domains_) {
+          const Dim3 raw = d.raw_size(), org = d.accessor_origin();
+          std::vector<int32_t> v(size_t(raw.flatten()), kProbePoison);
+          const Rect3 cr = d.get_compute_region();
+          for (int64_t z = 0; z < raw.z; ++z)
+            for (int64_t y = 0; y < raw.y; ++y)
+              for (int64_t x = 0; x < raw.x; ++x)
+                if (cr.contains(Dim3(org.x + x, org.y + y, org.z + z)))
+                  v[size_t(x + raw.x * (y + raw.y * z))] = probe_key(org.x + x, org.y + y, org.z + z, L, off);
+          d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), true);
+          d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), false);
+        }
+        p.exchange();
+        for (auto &d : p.domains_) {
+          const Dim3 raw = d.raw_size(), org = d.accessor_origin();
+          const Rect3 cr = d.get_compute_region();
+          const auto bytes = d.region_to_host(Dim3(0, 0, 0), raw, 0, true);
+          const int32_t *got = reinterpret_cast<const int32_t *>(bytes.data());
+          for (int64_t z = 0; z < raw.z; ++z)
+            for (int64_t y = 0; y < raw.y; ++y)
+              for (int64_t x = 0; x < raw.x; ++x) {
+                const int64_t g[3] = {org.x + x, org.y + y, org.z + z};
+                const int64_t lo[3] = {cr.lo.x, cr.lo.y, cr.lo.z}, hi[3] = {cr.hi.x, cr.hi.y, cr.hi.z};
+                const int64_t n[3] = {L.x, L.y, L.z};
+                int dd[3];
+                bool crossesClosed = false;
+                for (int a = 0; a < 3; ++a) {
+                  dd[a] = g[a] >= hi[a] ? 1 : (g[a] < lo[a] ? -1 : 0);
+                  if ((g[a] < 0 || g[a] >= n[a]) &&
+                      !boundary_.face_periodic(a == 0 ? dd[a] : 0, a == 1 ? dd[a] : 0, a == 2 ? dd[a] : 0))
+                    crossesClosed = true;
+                }
+                const bool filled = (dd[0] == 0 && dd[1] == 0 && dd[2] == 0) ||
+                                    (radius_.dir(Dim3(dd[0], dd[1], dd[2])) != 0 && !crossesClosed);
+                const int32_t want =
+                    filled ? probe_key(((g[0] % n[0]) + n[0]) % n[0], ((g[1] % n[1]) + n[1]) % n[1],
+                                       ((g[2] % n[2]) + n[2]) % n[2], L, off)
+                           : kProbePoison;
+                bad += got[size_t(x + raw.x * (y + raw.y * z))] != want;
               }
-              const bool filled = (dd[0] == 0 && dd[1] == 0 && dd[2] == 0) ||
-                                  (radius_.dir(Dim3(dd[0], dd[1], dd[2])) != 0 && !crossesClosed);
-              const int32_t want =
-                  filled ? probe_key(((g[0] % n[0]) + n[0]) % n[0], ((g[1] % n[1]) + n[1]) % n[1],
-                                     ((g[2] % n[2]) + n[2]) % n[2], L, off)
-                         : kProbePoison;
-              bad += got[size_t(x + raw.x * (y + raw.y * z))] != want;
-            }
+        }
+        p.swap();
       }
-      p.swap();
+    } catch (const std::exception &e) {
+      LOG_WARN("rank " << rank() << ": transport probe with " << to_string(m) << " failed: " << e.what());
+      bad += int64_t(1) << 40;
+      p.poison("transport probe failed"); // its destructor must not wait on work stuck behind an absent peer
     }
-  } catch (const std::exception &e) {
-    LOG_WARN("rank " << rank() << ": transport probe with " << to_string(m) << " failed: " << e.what());
-    bad += int64_t(1) << 40;
-  }
+  } // the probe domain (and its bounded destructor barrier on the fork) is gone before the verdict
   return int64_t(pg_->allreduce_sum_u64(uint64_t(bad)));
 }
 
@@ -445,6 +467,21 @@ void DistributedDomain::init_rccl(const std::function<bool(int, int)> &sharedDev
   int ok = boot.ok && !topt_.failRcclInit;
   if (!boot.ok && why.empty()) why = "the root rank could not create an RCCL id";
   if (topt_.failRcclInit) why = "TransportOptions::failRcclInit";
+  // local preconditions (the id, the forced-failure hook, every member device selectable) are agreed on BEFORE any
+  // rank enters ncclCommInitRank: a rank that would skip or abort creation must not leave the others blocked inside
+  // RCCL waiting for it. What remains is a failure inside RCCL itself, reported by the watch thread.
+  for (int k = 0; k < nLocal && ok; ++k) {
+    if (ncclRankOf[size_t(myRank) * size_t(maxN) + size_t(k)] < 0) continue;
+    if (hipSetDevice(I.devs[size_t(k)].dev) != hipSuccess) {
+      (void)hipGetLastError();
+      ok = 0;
+      why = "hipSetDevice(" + std::to_string(I.devs[size_t(k)].dev) + ") before RCCL init";
+    }
+  }
+  if (pg.allreduce_min_i64(ok) != 1) {
+    if (ok) why = "another rank cannot create its RCCL communicator";
+    ok = 0;
+  }
   if (ok) {
     // a communicator that never forms (a rank died between the bcast and here) blocks in RCCL itself: say so
     // with the plan after the wait timeout instead of hanging silently
@@ -940,6 +977,7 @@ void DistributedDomain::realize() {
       I.pipes.push_back(std::move(pp));
     }
     for (auto &ctx : I.devs) {
+      ctx.sharedGpu = shared_dev(myRank, ctx.dev);
       ctx.pipePack[0].upload(ctx.dev);
       ctx.pipeUnpack[0].upload(ctx.dev);
       if (!ctx.pipesOut.empty()) ctx.pipeSent = Event(ctx.dev);
@@ -1016,6 +1054,26 @@ void DistributedDomain::realize() {
         HIP_CHECK(hipSetDevice(c.localDev));
         HIP_CHECK(hipIpcOpenMemHandle((void **)&c.remoteFlag, h[0], hipIpcMemLazyEnablePeerAccess));
         if (c.send) HIP_CHECK(hipIpcOpenMemHandle((void **)&c.remoteData, h[1], hipIpcMemLazyEnablePeerAccess));
+      }
+      // Completion::IpcEvent: sender -> receiver, the handle of the sender's interprocess event per channel
+      if (topt_.completion == TransportOptions::Completion::IpcEvent) {
+        for (auto &c : I.chans) {
+          if (c.method != MethodFlags::Colocated || !c.send) continue;
+          HIP_CHECK(hipSetDevice(c.localDev));
+          HIP_CHECK(hipEventCreateWithFlags(&c.ipcEvent, hipEventDisableTiming | hipEventInterprocess));
+          hipIpcEventHandle_t h{};
+          HIP_CHECK(hipIpcGetEventHandle(&h, c.ipcEvent));
+          pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::IpcEvent), &h, sizeof(h));
+        }
+        for (auto &c : I.chans) {
+          if (c.method != MethodFlags::Colocated || c.send) continue;
+          hipIpcEventHandle_t h{};
+          pg.recv(c.remoteRank, retag(c.tag, comm::MsgKind::IpcEvent), &h, sizeof(h));
+          HIP_CHECK(hipSetDevice(c.localDev));
+          HIP_CHECK(hipIpcOpenEventHandle(&c.ipcEvent, h));
+        }
+        I.ipcEvents = true;
+        I.ipcEventFirstEpoch = 1;
       }
       pg.barrier();
     }
@@ -1290,7 +1348,7 @@ void DistributedDomain::sync_streams(const std::vector<hipStream_t> &extra) {
   // not: then poll the streams, check every communicator's asynchronous error, and give up after the wait timeout
   // with the plan on stderr (a peer that died or never posted its matching send/recv would otherwise block here
   // forever) -- including the caller's compute streams, which join the exchange.
-  const bool unbounded = I.rccl || topt_.completion == TransportOptions::Completion::StreamOp;
+  const bool unbounded = I.rccl || topt_.completion != TransportOptions::Completion::Kernel;
   if (unbounded) {
     const double t0 = now_s();
     auto pending = [&](hipError_t q) {
@@ -1385,8 +1443,13 @@ void DistributedDomain::set_transport_options_live(const TransportOptions &o) {
 
 void DistributedDomain::set_completion(TransportOptions::Completion c) {
   if (c == topt_.completion) return;
+  STENCIL_REQUIRE(!realized_ || c != TransportOptions::Completion::IpcEvent || impl_->ipcEvents ||
+                      exchange_bytes_for_method(MethodFlags::Colocated) == 0,
+                  "Completion::IpcEvent needs its interprocess events: realize() with that completion");
   if (realized_) sync_exchange(); // flag words are monotonic epochs: either method continues where the other left off
   topt_.completion = c;
+  // every rank switches between the same two exchanges: acknowledgements exist from the next epoch on
+  if (c == TransportOptions::Completion::IpcEvent) impl_->ipcEventFirstEpoch = impl_->epoch + 1;
 }
 
 const char *to_string(TransportOptions::Inbox v) {
@@ -1402,7 +1465,14 @@ const char *to_string(TransportOptions::Inbox v) {
 }
 const char *to_string(TransportOptions::Copy v) { return v == TransportOptions::Copy::Engine ? "engine" : "store"; }
 const char *to_string(TransportOptions::Completion v) {
-  return v == TransportOptions::Completion::StreamOp ? "streamop" : "kernel";
+  switch (v) {
+  case TransportOptions::Completion::StreamOp:
+    return "streamop";
+  case TransportOptions::Completion::IpcEvent:
+    return "ipcevent";
+  default:
+    return "kernel";
+  }
 }
 
 void DistributedDomain::exchange() {
@@ -1490,6 +1560,42 @@ void DistributedDomain::prepare_skip_wrapped(int axes) {
     ctx.pipeUnpack[1].upload(ctx.dev);
   }
   I.skipAxes = axes;
+}
+
+void DistributedDomain::set_transport_log(int exchanges) {
+  STENCIL_REQUIRE(realized_, "set_transport_log before realize");
+  if (backend_ != Backend::Device) return;
+  Impl &I = *impl_;
+  sync_exchange();
+  for (auto &ctx : I.devs) {
+    HIP_CHECK(hipSetDevice(ctx.dev));
+    if (ctx.xlog) (void)hipFree(ctx.xlog);
+    ctx.xlog = nullptr;
+    if (exchanges > 0) {
+      const size_t nb = sizeof(uint64_t) * size_t(exchanges) * kTransportLogWords;
+      HIP_CHECK(hipMalloc((void **)&ctx.xlog, nb));
+      HIP_CHECK(hipMemset(ctx.xlog, 0, nb));
+    }
+  }
+  HIP_CHECK(hipDeviceSynchronize());
+  I.xlogCap = std::max(0, exchanges);
+  I.xlogFirstEpoch = I.epoch + 1;
+}
+
+std::vector<std::array<uint64_t, kTransportLogWords>> DistributedDomain::transport_log(size_t dev) {
+  STENCIL_REQUIRE(realized_, "transport_log before realize");
+  Impl &I = *impl_;
+  std::vector<std::array<uint64_t, kTransportLogWords>> out;
+  if (backend_ != Backend::Device || I.xlogCap == 0 || dev >= I.devs.size()) return out;
+  sync_exchange();
+  DevCtx &ctx = I.devs[dev];
+  std::vector<std::array<uint64_t, kTransportLogWords>> ring(size_t(I.xlogCap));
+  HIP_CHECK(hipSetDevice(ctx.dev));
+  HIP_CHECK(hipMemcpy(ring.data(), ctx.xlog, sizeof(uint64_t) * kTransportLogWords * ring.size(), hipMemcpyDeviceToHost));
+  // oldest first: the last min(cap, logged) epochs
+  const uint64_t last = I.epoch, first = std::max(I.xlogFirstEpoch, last >= uint64_t(I.xlogCap) ? last - I.xlogCap + 1 : 1);
+  for (uint64_t e = first; e <= last && e >= I.xlogFirstEpoch; ++e) out.push_back(ring[size_t((e - 1) % uint64_t(I.xlogCap))]);
+  return out;
 }
 
 void DistributedDomain::set_send_gate(uint64_t *counter, uint64_t target) {
@@ -1597,8 +1703,11 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
   // Colocated completion (TransportOptions::completion): bounded spin / release kernels, or command-processor
   // stream operations on the same flag words
   const bool streamOps = topt_.completion == TransportOptions::Completion::StreamOp;
+  // interprocess events + host notify / ack for arrival, credit flags inside the (always fused) transport kernels
+  const bool ipcEvt = topt_.completion == TransportOptions::Completion::IpcEvent;
+  STENCIL_REQUIRE(!ipcEvt || !capturing, "Completion::IpcEvent exchanges cannot be captured into a hipGraph");
   // Colocated flag waits / signals folded into the pack and unpack kernels (TransportOptions::fuseFlags)
-  const bool fused = !streamOps && topt_.fuseFlags;
+  const bool fused = !streamOps && !ipcEvt && topt_.fuseFlags;
   auto wait_flags = [&](const std::vector<uint64_t *> &flags, uint64_t target, int code, hipStream_t st) {
     if (!streamOps) {
       wait_flags_device(flags, target, I.errDev, code, topt_.waitTimeout, st);
@@ -1682,7 +1791,7 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
         const PeerPipe &pp = I.pipes[size_t(ctx.pipesOut[size_t(j)])];
         const size_t nb = size_t(pp.bytes[pv]);
         if (nb == 0) return;
-        if (pp.srcDev == pp.dstDev)
+        if (pp.srcDev == pp.dstDev && !topt_.peerApiSameDevice)
           engine_copy(pp.rbuf, pp.sbuf, nb, cs);
         else
           HIP_CHECK(hipMemcpyPeerAsync(pp.rbuf, pp.dstDev, pp.sbuf, pp.srcDev, nb, cs));
@@ -1717,6 +1826,42 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     if (I.epoch > 2)
       for (int ci : ctx.coloSend) credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownFlag));
     for (int ci : ctx.coloSend) arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteFlag));
+    if (ipcEvt) {
+      // credit wait fused into the pack (or before the engine copies), then per channel: the receiver's Ack of
+      // epoch-2 (its wait on the previous-but-one record is enqueued), record, Notify
+      FlagSyncArgs fa;
+      fa.err = I.errDev;
+      fa.code = 1;
+      fa.timeout_s = topt_.waitTimeout;
+      fa.sharedGpu = ctx.sharedGpu;
+      fa.counter = ctx.syncCounter;
+      if (engine) {
+        ctx.coloPackLocal.run_device(parity, S(ctx), commBlocks_);
+        if (!credits.empty()) wait_flags(credits, I.epoch - 2, 1, S(ctx));
+        forked_copies(ctx, S(ctx), int(ctx.coloSend.size()), [&](int k, hipStream_t cs) {
+          const Channel &c = I.chans[size_t(ctx.coloSend[size_t(k)])];
+          if (c.bytes > 0) engine_copy(c.remoteData + slot * c.slotStride, c.dbuf, size_t(c.bytes), cs);
+        });
+      } else {
+        fa.wait = credits;
+        fa.waitTarget = I.epoch - 2;
+        if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords;
+        ctx.coloPack.run_device_sync(cv, S(ctx), commBlocks_, fa);
+      }
+      for (int ci : ctx.coloSend) {
+        Channel &c = I.chans[size_t(ci)];
+        if (I.epoch >= I.ipcEventFirstEpoch + 2) {
+          uint64_t acked = 0;
+          pg.recv(c.remoteRank, retag(c.tag, comm::MsgKind::Ack), &acked, sizeof(acked));
+          STENCIL_REQUIRE(acked == I.epoch - 2, "IPC-event ack out of order: got epoch " << acked << ", want "
+                                                                                          << I.epoch - 2);
+        }
+        HIP_CHECK(hipEventRecord(c.ipcEvent, S(ctx)));
+        const uint64_t e = I.epoch;
+        pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::Notify), &e, sizeof(e));
+      }
+      continue;
+    }
     if (!engine && fused) { // one launch: credit wait, pack into the peer slots, arrival flags
       FlagSyncArgs fa;
       fa.wait = credits;
@@ -1731,6 +1876,8 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       fa.err = I.errDev;
       fa.code = 1;
       fa.timeout_s = topt_.waitTimeout;
+      fa.sharedGpu = ctx.sharedGpu;
+      if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords;
       ctx.coloPack.run_device_sync(cv, S(ctx), commBlocks_, fa);
       continue;
     }
@@ -1815,7 +1962,31 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       arrived.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].ownFlag));
       credits.push_back(reinterpret_cast<uint64_t *>(I.chans[ci].remoteFlag));
     }
-    if (fused) { // one launch: arrival wait, unpack from our slots, credit flags
+    if (ipcEvt) { // per channel: Notify(epoch) -> wait on the sender's event -> Ack(epoch); unpack + credits
+      for (int ci : ctx.coloRecv) {
+        Channel &c = I.chans[size_t(ci)];
+        uint64_t e = 0;
+        pg.recv(c.remoteRank, retag(c.tag, comm::MsgKind::Notify), &e, sizeof(e));
+        STENCIL_REQUIRE(e == I.epoch, "IPC-event notify out of order: got epoch " << e << ", want " << I.epoch);
+        HIP_CHECK(hipStreamWaitEvent(S(ctx), c.ipcEvent, 0));
+        pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::Ack), &e, sizeof(e));
+      }
+      FlagSyncArgs fa;
+      fa.signal = credits;
+      fa.signalValue = I.epoch;
+      fa.counter = ctx.syncCounter + 1;
+      fa.err = I.errDev;
+      fa.code = 2;
+      fa.timeout_s = topt_.waitTimeout;
+      fa.sharedGpu = ctx.sharedGpu;
+      if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords + 4;
+      ctx.coloUnpack.run_device_sync(cv, S(ctx), commBlocks_, fa);
+      continue;
+    }
+    // Coarse (L2-cached) inboxes keep the arrival wait in its own kernel: the unpack's dispatch then starts after
+    // the wait with the kernel-boundary cache invalidate, where a wait inside the unpack kernel would rely on its
+    // in-kernel acquire dropping L2 lines of local coarse-grained memory written over xGMI
+    if (fused && topt_.inbox != TransportOptions::Inbox::Coarse) { // one launch: arrival wait, unpack, credits
       FlagSyncArgs fa;
       fa.wait = arrived;
       fa.waitTarget = I.epoch;
@@ -1825,6 +1996,8 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       fa.err = I.errDev;
       fa.code = 2;
       fa.timeout_s = topt_.waitTimeout;
+      fa.sharedGpu = ctx.sharedGpu;
+      if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords + 4;
       ctx.coloUnpack.run_device_sync(cv, S(ctx), commBlocks_, fa);
       continue;
     }

@@ -328,6 +328,7 @@ struct FlagSync {
   int *err;
   int code;
   uint64_t timeoutTicks;
+  uint64_t *stamps;     // transport log entry (4 words) or null
 };
 
 // Fused transport step (Colocated sends / receives): wait for the peer's flags, run the copy plan, raise the
@@ -339,6 +340,9 @@ struct FlagSync {
 __global__ __launch_bounds__(1024) void copy_plan_kernel_sync(const CopySeg *__restrict__ segs,
                                                               const CopyWork *__restrict__ work, uint32_t nwork,
                                                               FlagSync fs) {
+  // transport log (FlagSyncArgs::stamps): block 0 records start / after the wait / after its copies
+  const bool stamp = fs.stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
+  const uint64_t tStart = stamp ? __builtin_amdgcn_s_memrealtime() : 0;
   if (fs.wait.n > 0 || fs.gate.n > 0) {
     if (threadIdx.x < 64) {
       poll_flags(fs.wait, fs.waitTarget, fs.err, fs.code, fs.timeoutTicks, int(threadIdx.x));
@@ -347,13 +351,19 @@ __global__ __launch_bounds__(1024) void copy_plan_kernel_sync(const CopySeg *__r
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the peer's slot writes / reads before our copies
     __syncthreads();
   }
+  if (stamp) {
+    fs.stamps[0] = tStart;
+    fs.stamps[1] = __builtin_amdgcn_s_memrealtime();
+  }
   const uint32_t g = threadIdx.x >> 8; // wave-uniform (a group is 4 whole waves)
   for (uint32_t wi = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + g); wi < nwork; wi += gridDim.x * 4) {
     const CopyWork w = work[wi];
     copy_work(segs[w.seg], w, threadIdx.x & 255);
   }
-  if (fs.signal.n == 0) return;
+  if (fs.signal.n == 0 && fs.stamps == nullptr) return;
   __syncthreads();
+  if (stamp) fs.stamps[2] = __builtin_amdgcn_s_memrealtime();
+  if (fs.signal.n == 0) return;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     const uint32_t done = __hip_atomic_fetch_add(fs.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -362,6 +372,7 @@ __global__ __launch_bounds__(1024) void copy_plan_kernel_sync(const CopySeg *__r
       for (int i = 0; i < fs.signal.n; ++i)
         __hip_atomic_store(fs.signal.p[i], fs.signalValue, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(fs.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fs.stamps != nullptr) fs.stamps[3] = __builtin_amdgcn_s_memrealtime();
     }
   }
 }
@@ -406,13 +417,25 @@ void copy_plan_device_sync(const CopyPlan &p, hipStream_t stream, int maxBlocks,
   fs.err = a.err;
   fs.code = a.code;
   fs.timeoutTicks = uint64_t(a.timeout_s * 1e8);
+  fs.stamps = a.stamps;
   STENCIL_REQUIRE(fs.signal.n == 0 || a.counter, "copy_plan_device_sync: signal flags need a block counter");
   // one CU per block (1024 threads): at most maxBlocks and kFusedMaxBlocks (waiting blocks hold their CUs); at
   // least one block, so the flags are waited for and raised even when this device has nothing to copy
-  const int cap = maxBlocks > 0 ? std::min(maxBlocks, kFusedMaxBlocks) : kFusedMaxBlocks;
+  const int shareCap = a.sharedGpu ? kFusedMaxBlocks : (1 << 20);
+  const int cap = maxBlocks > 0 ? std::min(maxBlocks, shareCap) : shareCap;
   const int blocks = std::max(1, std::min(cap, (p.nwork + 3) / 4));
   hipLaunchKernelGGL(copy_plan_kernel_sync, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dwork, uint32_t(p.nwork),
                      fs);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void spin_kernel(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+void spin_device(double seconds, hipStream_t stream) {
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, stream, uint64_t(seconds * 1e8));
   HIP_CHECK(hipGetLastError());
 }
 

@@ -116,6 +116,7 @@ public:
     if (!try_recv(src, tag, buf, n)) LOG_FATAL("single group recv would block forever (tag " << tag << ")");
   }
   void barrier() override {}
+  std::shared_ptr<ProcGroup> fork(double) override { return std::make_shared<SingleGroup>(); }
   void bcast(void *, size_t, int) override {}
   void allgather(const void *in, size_t n, void *out) override { std::memcpy(out, in, n); }
   void gatherv(const void *in, size_t n, std::vector<std::vector<char>> *out, int) override {
@@ -247,6 +248,7 @@ class TcpGroup : public ProcGroup {
   int rank_, size_;
   double timeout_s_;
   std::vector<std::string> hosts_;
+  std::string masterIp_; // the rendezvous address this rank reached rank 0 at (fork() reuses it)
   std::vector<int> fds_;
   std::vector<std::unique_ptr<std::mutex>> sendMu_;
   std::vector<std::thread> readers_;
@@ -419,6 +421,7 @@ public:
     }
     ::close(lfd);
     hosts_ = names;
+    masterIp_ = master;
     for (int k = 0; k < size; ++k)
       if (k != rank) readers_.emplace_back(&TcpGroup::reader, this, k);
     barrier();
@@ -481,6 +484,11 @@ public:
   }
   void set_timeout(double timeout_s) override { timeout_s_ = timeout_s; }
   double timeout() const override { return timeout_s_; }
+  std::shared_ptr<ProcGroup> fork(double timeout_s) override {
+    int32_t port = rank_ == 0 ? find_free_port() : 0;
+    bcast(&port, sizeof(port), 0);
+    return std::make_shared<TcpGroup>(rank_, size_, masterIp_, port, timeout_s);
+  }
   void bcast(void *buf, size_t n, int root) override {
     const uint32_t tag = next_coll_tag();
     if (rank_ == root) {

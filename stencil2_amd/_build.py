@@ -18,7 +18,7 @@ BUILD = os.path.join(REPO, "build")
 
 
 def _sources():
-    pats = ["csrc/**/*.hpp", "csrc/**/*.cpp", "csrc/**/*.hip", "CMakeLists.txt"]
+    pats = ["csrc/**/*.hpp", "csrc/**/*.cpp", "csrc/**/*.hip", "CMakeLists.txt", "cmake/*.cmake"]
     out = []
     for p in pats:
         out += glob.glob(os.path.join(REPO, p), recursive=True)
@@ -82,11 +82,15 @@ def ensure_built() -> None:
     if not is_stale():
         return
     if _artifacts() and not os.path.exists(os.path.join(BUILD, "CMakeFiles", "rules.ninja")):
-        # a snapshot without the configured build tree (a GPU box): the shipped artifacts are what there is to load;
-        # rebuilding here would fail half-way, so load them and say so
-        print("stencil2_amd: native sources differ from the build stamp and no build tree is configured here; "
-              "loading the shipped artifacts", file=sys.stderr)
-        return
+        # a snapshot without the configured build tree (a GPU box): the shipped artifacts were built from other
+        # sources than these. Loading them would run stale native code under tests and benchmarks, so refuse unless
+        # explicitly allowed.
+        msg = ("stencil2_amd: the native sources differ from the build stamp and no build tree is configured here; "
+               "rebuild in-tree (python -m stencil2_amd._build) before shipping")
+        if os.environ.get("STENCIL_ALLOW_STALE") == "1":
+            print(msg + " -- loading the shipped artifacts anyway (STENCIL_ALLOW_STALE=1)", file=sys.stderr)
+            return
+        raise RuntimeError(msg + " (or set STENCIL_ALLOW_STALE=1 to load the stale artifacts)")
     build()
 
 

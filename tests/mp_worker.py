@@ -22,6 +22,9 @@ def transport_from_env():
     t.fuse_flags = e.get("MP_FUSE_FLAGS", "1") == "1"
     t.fail_ipc_probe = e.get("MP_IPC_PROBE_FAIL") == "1"
     t.fail_rccl_init = e.get("MP_RCCL_INIT_FAIL") == "1"
+    t.fail_probe_rank = int(e.get("MP_PROBE_FAIL_RANK", "-1"))
+    if e.get("MP_WAIT_TIMEOUT"):
+        t.wait_timeout = float(e["MP_WAIT_TIMEOUT"])
     return t
 
 
@@ -241,6 +244,16 @@ def scenario_localint(backend, methods, size):
     return bad
 
 
+def scenario_ipcevent():
+    """reference test/test_cuda_mpi_cudaipc.cu:8-45: an interprocess event's handle travels from rank 0 to the other
+    ranks and opens there; here the receivers also wait on it behind 0.2 s of rank 0's GPU work"""
+    g = st.init_process_group()
+    from stencil2_amd import _C
+    r = _C.ipc_event_roundtrip(g, 0, 0.2)
+    print(f"rank {g.rank()} ipcevent {r}", flush=True)
+    return 0 if r["ok"] else 1
+
+
 def main():
     # a stalled rank dumps every thread's Python stack (its C++ frames show as the native call it is in) so a hang
     # names its rank, scenario and phase; repeated, in case the first dump lands before the stall
@@ -259,6 +272,8 @@ def main():
         bad = scenario_selftest(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "localint":
         bad = scenario_localint(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
+    elif sc == "ipcevent":
+        bad = scenario_ipcevent()
     elif sc == "jacobi":
         bad = scenario_jacobi(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     else:

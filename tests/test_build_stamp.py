@@ -22,9 +22,7 @@ def test_mtime_only_change_is_not_stale():
         os.utime(src, (st.st_atime, st.st_mtime))
 
 
-def test_no_build_tree_loads_shipped_artifacts(monkeypatch, tmp_path):
-    """a snapshot whose sources differ from the stamp but that has no configured build tree (a GPU box) must not try
-    to rebuild half-way: ensure_built() leaves the shipped artifacts to be loaded"""
+def _no_tree(monkeypatch, tmp_path):
     monkeypatch.setattr(_build, "BUILD", str(tmp_path))
     monkeypatch.setattr(_build, "is_stale", lambda: True)
 
@@ -32,4 +30,23 @@ def test_no_build_tree_loads_shipped_artifacts(monkeypatch, tmp_path):
         raise AssertionError("build() called without a build tree")
 
     monkeypatch.setattr(_build, "build", no_build)
-    _build.ensure_built()
+
+
+def test_no_build_tree_refuses_stale_artifacts(monkeypatch, tmp_path):
+    """a snapshot whose sources differ from the stamp and that has no configured build tree (a GPU box) must neither
+    rebuild half-way nor silently load native code built from other sources"""
+    import pytest
+    _no_tree(monkeypatch, tmp_path)
+    monkeypatch.delenv("STENCIL_ALLOW_STALE", raising=False)
+    with pytest.raises(RuntimeError, match="differ from the build stamp"):
+        _build.ensure_built()
+
+
+def test_no_build_tree_stale_opt_in(monkeypatch, tmp_path):
+    _no_tree(monkeypatch, tmp_path)
+    monkeypatch.setenv("STENCIL_ALLOW_STALE", "1")
+    _build.ensure_built()  # loads the shipped artifacts, with a warning
+
+
+def test_cmake_helpers_are_hashed():
+    assert any(f.endswith("git_sha.cmake") for f in _build._sources())

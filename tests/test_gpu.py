@@ -39,15 +39,19 @@ def _radii(st):
 
 @pytest.mark.parametrize("method,gpus", [("Kernel", [0]), ("Kernel", [0, 0]), ("PeerCopy", [0, 0]),
                                          ("PeerCopyEngine", [0, 0]), ("PeerCopyEngine", [0, 0, 0]),
+                                         ("PeerCopyPeerApi", [0, 0]), ("PeerCopyPeerApi", [0, 0, 0]),
                                          ("Rccl", [0, 0]), ("Staged", [0, 0]), ("All", [0, 0, 0])])
 @pytest.mark.parametrize("rname", ["r1", "r3", "asym", "fec", "mixed"])
 def test_device_exchange(st, method, gpus, rname):
     """PeerCopyEngine: PeerCopy messages between sub-domains packed, copied by a DMA engine, unpacked
-    (TransportOptions.peer_copy = Engine; self-neighbour messages stay direct stores)."""
+    (TransportOptions.peer_copy = Engine; self-neighbour messages stay direct stores). PeerCopyPeerApi: the same
+    pipes through hipMemcpyPeerAsync(dst, dev, src, dev) -- the cross-GPU call of the reference's PeerCopySender
+    (tx_cuda.cuh:153), executed with both ends on device 0."""
     radius = _radii(st)[rname]
     tr = st.TransportOptions()
-    if method == "PeerCopyEngine":
+    if method in ("PeerCopyEngine", "PeerCopyPeerApi"):
         tr.peer_copy = st.TransportOptions.Copy.Engine
+        tr.peer_api_same_device = method == "PeerCopyPeerApi"
         method = "PeerCopy"
     dd, q = _dd(st, (19, 13, 11), radius, gpus, getattr(st.MethodFlags, method), transport=tr)
     for it in range(2):
@@ -547,13 +551,15 @@ def test_temporal2_row_kernel_lockstep_parts(st, size, fp64):
         assert torch.equal(_gather(m), u), f"after run({n})"
 
 
-@pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy", "PeerCopyEngine"])
+@pytest.mark.parametrize("methods", ["Rccl", "Staged", "PeerCopy", "PeerCopyEngine", "PeerCopyPeerApi"])
 def test_jacobi_temporal2_transports(st, methods):
     """depth-2 exchanges (faces 2, edges 1) over every in-process transport, then fused pairs (PeerCopyEngine: the
-    peer messages over DMA-engine copies, including the in-kernel-wrap subset prepared by prepare_skip_wrapped)"""
+    peer messages over DMA-engine copies, including the in-kernel-wrap subset prepared by prepare_skip_wrapped;
+    PeerCopyPeerApi: those copies through hipMemcpyPeerAsync)"""
     tr = st.TransportOptions()
-    if methods == "PeerCopyEngine":
+    if methods in ("PeerCopyEngine", "PeerCopyPeerApi"):
         tr.peer_copy = st.TransportOptions.Copy.Engine
+        tr.peer_api_same_device = methods == "PeerCopyPeerApi"
         methods = "PeerCopy"
     m = st.Jacobi3D((40, 36, 44), gpus=[0, 0], methods=getattr(st.MethodFlags, methods), temporal=2, transport=tr)
     m.init()
@@ -619,12 +625,15 @@ def test_colocated_ipc_two_ranks_one_gpu(radius):
                                                         ("Uncached", "Store", "Kernel", "0"),
                                                         ("Uncached", "Engine", "Kernel", "0"),
                                                         ("Uncached", "Store", "StreamOp", "1"),
-                                                        ("Coarse", "Engine", "StreamOp", "1")])
+                                                        ("Coarse", "Engine", "StreamOp", "1"),
+                                                        ("Uncached", "Store", "IpcEvent", "1"),
+                                                        ("Coarse", "Store", "IpcEvent", "1"),
+                                                        ("Uncached", "Engine", "IpcEvent", "1")])
 def test_colocated_transport_variants_two_ranks(inbox, copy, completion, fuse):
     """Every TransportOptions variant of the HIP IPC transport (receive-slot memory, kernel stores vs DMA-engine
-    copies, flag waits/signals fused into the pack/unpack kernels or separate spin kernels, or stream wait/write
-    operations): coordinate oracle over faces, edges and corners, then fused Jacobi pairs vs the torch oracle, two
-    ranks sharing one GPU."""
+    copies, flag waits/signals fused into the pack/unpack kernels or separate spin kernels, stream wait/write
+    operations, or interprocess events with host notify/ack -- the reference's design): coordinate oracle over
+    faces, edges and corners, then fused Jacobi pairs vs the torch oracle, two ranks sharing one GPU."""
     env = {"MP_DEVICE": "1", "MP_METHODS": "Colocated|Kernel", "STENCIL_WAIT_TIMEOUT": "20", "MP_INBOX": inbox,
            "MP_COLO_COPY": copy, "MP_COMPLETION": completion, "MP_FUSE_FLAGS": fuse}
     for rc, out in run_ranks(2, WORKER, ["exchange", "fec", "20,12,10"], env_extra=env):
@@ -633,6 +642,16 @@ def test_colocated_transport_variants_two_ranks(inbox, copy, completion, fuse):
     for rc, out in run_ranks(2, WORKER, ["jacobi", "48,48,48"], env_extra=env):
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_ipc_event_handle_roundtrip(ranks):
+    """reference test/test_cuda_mpi_cudaipc.cu:8-45: rank 0's interprocess event handle opens on every other rank,
+    and their hipStreamWaitEvent on it holds their stream until rank 0's recorded work (a 0.2-s spin) is done"""
+    outs = run_ranks(ranks, WORKER, ["ipcevent"], env_extra={"MP_DEVICE": "1"}, timeout=90)
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "'ok': True" in out, out[-2000:]
 
 
 def test_rccl_init_failure_falls_back_to_staged(st):
@@ -734,16 +753,19 @@ def test_ipc_probe_failure_falls_back_on_shared_gpu():
         assert "bytes_Rccl=0 " in out and "bytes_Colocated=0 " in out and "bytes_Staged=0 " not in out, out[-2000:]
 
 
-@pytest.mark.parametrize("methods,copy,fuse", [("Colocated|Kernel", "Store", "1"), ("Colocated|Kernel", "Store", "0"),
-                                               ("Colocated|Kernel", "Engine", "1"), ("Staged|Kernel", "Store", "1")])
-def test_race_canary_two_ranks_one_gpu(methods, copy, fuse):
+@pytest.mark.parametrize("methods,copy,fuse,completion", [("Colocated|Kernel", "Store", "1", "Kernel"),
+                                                          ("Colocated|Kernel", "Store", "0", "Kernel"),
+                                                          ("Colocated|Kernel", "Engine", "1", "Kernel"),
+                                                          ("Colocated|Kernel", "Store", "1", "IpcEvent"),
+                                                          ("Staged|Kernel", "Store", "1", "Kernel")])
+def test_race_canary_two_ranks_one_gpu(methods, copy, fuse, completion):
     """Race canary over HIP IPC (double-buffered inboxes + credits; pack-kernel stores or DMA-engine copies) and the
     staged path, with jitter. Every host wait on a peer is bounded by STENCIL_WAIT_TIMEOUT and a stalled rank dumps
     its stacks (MP_STALL_DUMP_S), so a stall fails with every rank's phase instead of hanging."""
     outs = run_ranks(2, WORKER, ["canary", "fec", "20,12,10"],  # ~2.5 s normally; 90 s: rank outputs on a hang
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": methods, "STENCIL_WAIT_TIMEOUT": "20",
                                 "MP_JITTER_US": "200", "MP_COLO_COPY": copy, "MP_STALL_DUMP_S": "30",
-                                "MP_FUSE_FLAGS": fuse}, timeout=90)
+                                "MP_FUSE_FLAGS": fuse, "MP_COMPLETION": completion}, timeout=90)
     for rc, out in outs:
         assert rc == 0, out[-3000:]
 

@@ -60,3 +60,17 @@ def test_self_test_ladder_host_backend():
         assert rc == 0, out[-3000:]
         assert "selftest bad 0" in out and "report [all" not in out, out[-2000:]
         assert ": ok]" in out, out[-2000:]
+
+
+def test_self_test_one_rank_probe_failure_keeps_ranks_in_step():
+    """One rank's first probe throws (TransportOptions.fail_probe_rank) while the other is inside the probe's
+    exchange: the probe runs on a forked process group, so the healthy rank times out there, both agree that the
+    rung failed, and the ladder goes on to the next rung in step (no desynchronised collectives)."""
+    outs = run_ranks(2, WORKER, ["selftest", "24,20,18"],
+                     env_extra={"MP_METHODS": "All", "MP_PROBE_FAIL_RANK": "1", "MP_WAIT_TIMEOUT": "3"},
+                     timeout=120)
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "selftest bad 0" in out, out[-2000:]
+        rep = out.split("report [")[-1].split("]")[0]
+        assert rep.split(";")[0].endswith("bad") and rep.rstrip().endswith(": ok"), rep
