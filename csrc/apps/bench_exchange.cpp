@@ -12,13 +12,14 @@
 using namespace stencil;
 
 static std::pair<Statistics, uint64_t> bench(comm::ProcGroup &pg, int iters, int nq, const Dim3 &ext, const Radius &r,
-                                             MethodFlags m, PlacementStrategy pl, bool weak) {
+                                             MethodFlags m, PlacementStrategy pl, bool weak, bool xHaloAlign) {
   Dim3 e = ext;
   if (weak) e = Dim3(app::weak_scale(ext.x, pg.size()), app::weak_scale(ext.y, pg.size()), app::weak_scale(ext.z, pg.size()));
   DistributedDomain dd(e.x, e.y, e.z, comm::default_group());
   dd.set_radius(r);
   dd.set_methods(m);
   dd.set_placement(pl);
+  dd.set_x_halo_align(xHaloAlign);
   for (int i = 0; i < nq; ++i) dd.add_data<float>("d" + std::to_string(i));
   dd.realize();
   Statistics st;
@@ -39,12 +40,13 @@ static std::pair<Statistics, uint64_t> bench(comm::ProcGroup &pg, int iters, int
 int main(int argc, char **argv) {
   int iters = 30, nq = 1;
   int64_t x = 128, y = 128, z = 128, fr = 2, er = 1, cr = 1;
-  bool weak = false;
+  bool weak = false, xHaloAlign = false;
   app::MethodArgs ma;
   ArgParser p("halo exchange bandwidth (reference bin/bench_exchange.cu)");
   p.option(&iters, "--iters", "iterations").option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z")
       .option(&nq, "--q", "quantities").option(&fr, "--fr", "face radius").option(&er, "--er", "edge radius")
-      .option(&cr, "--cr", "corner radius").flag(&weak, "--weak", "scale x,y,z by ranks^(1/3)");
+      .option(&cr, "--cr", "corner radius").flag(&weak, "--weak", "scale x,y,z by ranks^(1/3)")
+      .flag(&xHaloAlign, "--x-halo-align", "x halos inside the interior's first / last 64-B sector");
   ma.add(p);
   if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
   auto pg = comm::default_group();
@@ -73,7 +75,7 @@ int main(int argc, char **argv) {
   }
   if (pg->rank() == 0) std::printf("name,count,trimean (S),trimean (B/s),stddev,min,avg,max\n");
   for (auto &pt : pats) {
-    auto res = bench(*pg, iters, nq, ext, pt.r, ma.flags(), ma.placement(), weak);
+    auto res = bench(*pg, iters, nq, ext, pt.r, ma.flags(), ma.placement(), weak, xHaloAlign);
     if (pg->rank() == 0) {
       std::ostringstream n;
       n << x << "-" << y << "-" << z << "/" << pt.name;

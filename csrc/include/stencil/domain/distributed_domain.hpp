@@ -199,6 +199,9 @@ public:
   // write plan_<rank>.txt during realize (reference src/stencil.cu:259-353); default on, off with STENCIL_PLAN_FILE=0
   void set_plan_file(const std::string &prefix) { planPrefix_ = prefix; }
   void set_padding(bool p) { pad_ = p; }
+  // halo-aligned x layout of every local domain (LocalDomain::set_x_halo_align)
+  void set_x_halo_align(bool on) { xHaloAlign_ = on; }
+  bool x_halo_align() const { return xHaloAlign_; }
   // opt-in self-test ladder run by realize() before planning (multi-rank runs): exchange a coordinate-encoded field
   // on a small probe domain built like this one and check every halo cell on every rank; on any wrong cell or
   // error drop Colocated, then Rccl (-> host-staged), i.e. the reference's always-terminating ladder
@@ -344,6 +347,7 @@ private:
   bool backendSet_ = false;
   bool realized_ = false;
   bool pad_ = true;
+  bool xHaloAlign_ = false;
   TransportOptions topt_;
   bool selfTest_ = false;
   std::string selfTestReport_;

@@ -5,7 +5,11 @@
 //   halo_coords / halo_bytes / raw_size / size / origin / gpu / swap / region_to_host / interior_to_host /
 //   quantity_to_host
 // MI355X layout: the x pitch is padded so the first interior x of every row is 64-B aligned and
-// every row starts on a 128-B line; y/z are unpadded. `raw_size()` keeps the reference's logical meaning
+// every row starts on a 128-B line; y/z are unpadded. Halo-aligned x (set_x_halo_align, x halos of at most 48 B):
+// the interior starts 16-B aligned inside the row's first 64-B sector, with the -x halo directly in front of it in
+// that same sector and the +x halo directly behind the interior's last cells, so an x-face copy touches one sector
+// per row end instead of two (the stencil kernels' 16-B chunk grid still starts at the interior; a row then spans
+// one more sector). A 128-B guard before the first row keeps reads left of raw x = 0 inside the allocation. `raw_size()` keeps the reference's logical meaning
 // (interior + halo), `pitch()` is the physical stride. Pointers are swapped on the host only: kernels receive
 // pointers by value, so swap() needs no device-side pointer-table upload (reference local_domain.cu:41-54
 // issues a synchronous cudaMemcpy there).
@@ -59,6 +63,8 @@ public:
   void set_radius(int64_t r) { radius_ = Radius::constant(r); }
   void set_radius(const Radius &r) { radius_ = r; }
   void set_padding(bool pad) { pad_ = pad; }
+  void set_x_halo_align(bool on) { xHaloAlign_ = on; }
+  bool x_halo_align() const { return xHaloAlign_; }
   void realize();
   bool realized() const { return realized_; }
 
@@ -83,6 +89,9 @@ public:
   Dim3 pitch(int64_t qi) const { return Dim3(pitchX_.at(size_t(qi)), raw_size().y, raw_size().z); }
   // elements of padding in front of raw x = 0 in every row
   int64_t pad_x(int64_t qi) const { return padX_.at(size_t(qi)); }
+  // elements in front of raw x = 0 that a kernel may read (ignoring the values) without leaving the allocation:
+  // the row padding, plus the guard before the first row (halo-aligned layout)
+  int64_t front_slack(int64_t qi) const { return padX_.at(size_t(qi)) + guard_ / elem_size(qi); }
   // bytes of one curr (or next) buffer of quantity qi
   int64_t buffer_bytes(int64_t qi) const;
 
@@ -141,6 +150,8 @@ private:
   int dev_;
   Backend backend_;
   bool pad_ = true;
+  bool xHaloAlign_ = false;
+  int64_t guard_ = 0; // bytes before the first row of every buffer (halo-aligned layout)
   bool realized_ = false;
   int parity_ = 0;
   std::vector<int64_t> elemSize_;

@@ -64,6 +64,9 @@ struct StencilModelConfig {
   // overlapped fused pairs: where the slabs at the remote faces run at first (set_overlap_mode: 1 beside the
   // interior sweep on the comm stream, 2 after it on the compute stream)
   int overlapMode = 1;
+  // halo-aligned x layout (DistributedDomain::set_x_halo_align): x halos share the interior's first / last 64-B
+  // sector (x-face copies touch one sector per row end instead of two; every row spans one more sector)
+  bool xHaloAlign = false;
   TransportOptions transport; // DistributedDomain::set_transport_options
   bool selfTest = false;      // DistributedDomain::set_self_test (multi-rank: verified transport ladder)
   bool setBackend = false;

@@ -428,6 +428,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_radius", py::overload_cast<int64_t>(&LocalDomain::set_radius))
       .def("set_radius", py::overload_cast<const Radius &>(&LocalDomain::set_radius))
       .def("set_padding", &LocalDomain::set_padding)
+      .def("set_x_halo_align", &LocalDomain::set_x_halo_align)
+      .def("x_halo_align", &LocalDomain::x_halo_align)
+      .def("front_slack", &LocalDomain::front_slack)
       .def("realize", &LocalDomain::realize)
       .def("swap", &LocalDomain::swap)
       .def("size", &LocalDomain::size)
@@ -579,6 +582,8 @@ PYBIND11_MODULE(_C, m) {
       .def("backend", &DistributedDomain::backend)
       .def("set_plan_file", &DistributedDomain::set_plan_file)
       .def("set_padding", &DistributedDomain::set_padding)
+      .def("set_x_halo_align", &DistributedDomain::set_x_halo_align)
+      .def("x_halo_align", &DistributedDomain::x_halo_align)
       .def("set_transport_options", &DistributedDomain::set_transport_options)
       .def("transport_options", &DistributedDomain::transport_options)
       .def("set_colo_copy", &DistributedDomain::set_colo_copy, py::call_guard<py::gil_scoped_release>())
@@ -719,6 +724,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("forward", &StencilModelConfig::forward)
       .def_readwrite("temporal", &StencilModelConfig::temporal)
       .def_readwrite("wrap_self", &StencilModelConfig::wrapSelf)
+      .def_readwrite("x_halo_align", &StencilModelConfig::xHaloAlign)
       .def_readwrite("wrap_axes_mask", &StencilModelConfig::wrapAxesMask)
       .def_readwrite("local_interior", &StencilModelConfig::localInterior)
       .def_readwrite("overlap_mode", &StencilModelConfig::overlapMode)

@@ -15,7 +15,7 @@ LocalDomain::LocalDomain(const Dim3 &sz, const Dim3 &origin, int dev, Backend ba
 
 LocalDomain::LocalDomain(LocalDomain &&o) noexcept
     : sz_(o.sz_), origin_(o.origin_), radius_(o.radius_), dev_(o.dev_), backend_(o.backend_), pad_(o.pad_),
-      realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
+      xHaloAlign_(o.xHaloAlign_), guard_(o.guard_), realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
       names_(std::move(o.names_)), pitchX_(std::move(o.pitchX_)), padX_(std::move(o.padX_)),
       curr_(std::move(o.curr_)), next_(std::move(o.next_)) {
   base_[0] = std::move(o.base_[0]);
@@ -62,6 +62,9 @@ int64_t LocalDomain::buffer_bytes(int64_t qi) const {
   return p.x * p.y * p.z * elem_size(qi);
 }
 
+// x halos of at most this many bytes go into the interior's first / last 64-B sector (set_x_halo_align)
+static constexpr int64_t kMaxAlignedHaloBytes = 48;
+
 void LocalDomain::realize() {
   STENCIL_REQUIRE(!realized_, "LocalDomain realized twice");
   TraceRange tr("LocalDomain::realize");
@@ -70,17 +73,25 @@ void LocalDomain::realize() {
   pitchX_.assign(size_t(nq), raw.x);
   padX_.assign(size_t(nq), 0);
   int64_t total = 0;
+  const int64_t rxm = radius_.x(-1), rxp = radius_.x(1);
+  const bool haloAligned = xHaloAlign_ && pad_;
+  guard_ = haloAligned ? 128 : 0;
   for (int64_t q = 0; q < nq; ++q) {
     const int64_t es = elemSize_[q];
     if (pad_ && 64 % es == 0) {
       const int64_t perLine = 64 / es; // elements per 64 B
-      padX_[q] = (perLine - (radius_.x(-1) % perLine)) % perLine;
+      if (haloAligned && 16 % es == 0 && rxm * es <= kMaxAlignedHaloBytes && rxp * es <= kMaxAlignedHaloBytes) {
+        // interior at the first 16-B boundary at or after the -x halo (inside the row's first sector)
+        padX_[q] = (round_up(rxm * es, 16) - rxm * es) / es;
+      } else {
+        padX_[q] = (perLine - (rxm % perLine)) % perLine;
+      }
       const int64_t rowAlign = (128 % es == 0) ? 128 / es : 1;
       // tail: one 16-B vector + 1 element so vectorized row sweeps never leave the allocation
       const int64_t tail = (16 % es == 0) ? 16 / es + 1 : 1;
       pitchX_[q] = round_up(padX_[q] + raw.x + tail, rowAlign);
     }
-    total += 2 * buffer_bytes(q);
+    total += 2 * (buffer_bytes(q) + guard_);
   }
   if (backend_ == Backend::Device) {
     set_device();
@@ -95,7 +106,7 @@ void LocalDomain::realize() {
   curr_.assign(size_t(nq), nullptr);
   next_.assign(size_t(nq), nullptr);
   for (int64_t q = 0; q < nq; ++q) {
-    const int64_t bytes = buffer_bytes(q);
+    const int64_t bytes = buffer_bytes(q) + guard_;
     for (int b = 0; b < 2; ++b) {
       void *p = nullptr;
       if (backend_ == Backend::Device) {
@@ -108,9 +119,9 @@ void LocalDomain::realize() {
       }
       base_[b][q] = p;
     }
-    // raw [0,0,0] sits padX elements into the first row
-    curr_[q] = static_cast<char *>(base_[0][q]) + padX_[q] * elemSize_[q];
-    next_[q] = static_cast<char *>(base_[1][q]) + padX_[q] * elemSize_[q];
+    // raw [0,0,0] sits padX elements into the first row (which starts guard_ bytes into the allocation)
+    curr_[q] = static_cast<char *>(base_[0][q]) + guard_ + padX_[q] * elemSize_[q];
+    next_[q] = static_cast<char *>(base_[1][q]) + guard_ + padX_[q] * elemSize_[q];
   }
   realized_ = true;
 }

@@ -111,6 +111,8 @@ def scenario_jacobi(backend, methods, size):
     kw = {"axis_cost": tuple(int(v) for v in cost.split(","))} if cost else {}
     if os.environ.get("MP_PARTITION") == "maxlink":  # bench.py's decomposition of the xGMI mesh (1x1xN slabs)
         kw["partition"] = st.PartitionObjective.MaxLink
+    if os.environ.get("MP_X_HALO_ALIGN") == "1":
+        kw["x_halo_align"] = True
     if kind == "astaroth":
         from stencil2_amd.ops import astaroth_step_reference as ref
         m = st.AstarothSim(size, quantities=1, gpus=gpus, backend=backend, methods=methods, group=g,

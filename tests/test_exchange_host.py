@@ -216,3 +216,32 @@ def test_exchange_x_face_sectors(st, name, size, gpus, dtype):
         dd.exchange()
         assert check_exchange(dd, q, radius, offset=it) == 0
         dd.swap()
+
+
+@pytest.mark.parametrize("name", ["r1", "r2", "+x2-x1", "fec", "mixed"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int64])
+@pytest.mark.parametrize("gpus", [[0], [0, 0, 0]])
+def test_exchange_x_halo_aligned_layout(st, name, dtype, gpus):
+    """Halo-aligned x layout (LocalDomain.set_x_halo_align): the interior starts 16-B aligned inside
+    its row's first 64-B sector with the -x halo directly in front, rows stay 128-B aligned; the exchange is exact."""
+    radius = radius_patterns(st)[name]
+    dd = st.DistributedDomain(13, 11, 9, group=st.make_single_group())
+    dd.set_backend(st.Backend.Host)
+    dd.set_radius(radius)
+    dd.set_gpus(gpus)
+    dd.set_x_halo_align(True)
+    q = dd.add_data("q", dtype)
+    dd.realize()
+    for di in range(dd.num_domains()):
+        d = dd.domain(di)
+        es = d.elem_size(q)
+        rx = d.radius().x(-1)
+        raw0 = d.curr_ptr(q)
+        first = raw0 + rx * es  # first interior cell
+        assert first % 16 == 0 and (first // 64) == ((raw0 - 0) // 64 if rx * es <= 16 else (first - 1) // 64)
+        assert (raw0 - d.pad_x(q) * es) % 128 == 0 and (d.pitch(q).x * es) % 128 == 0
+        assert d.front_slack(q) == d.pad_x(q) + 128 // es
+        assert d.x_halo_align()
+    fill_coords(dd, q)
+    dd.exchange()
+    assert check_exchange(dd, q, radius) == 0

@@ -845,3 +845,71 @@ def test_topology_links(st):
             assert li["source"] in ("amd-smi", "hip", "none") and li["distance"] >= 0.5
     assert _C.gpu_numa_node(0) >= -1
     print("amd-smi:", _C.amdsmi_available(), "numa(0):", _C.gpu_numa_node(0))
+
+
+@pytest.mark.parametrize("kind,size,fp64,gpus,temporal,wrap", [
+    ("jacobi", (512, 20, 18), False, [0], 2, True),      # whole-row kernel, x wrapped in-kernel
+    ("jacobi", (64, 36, 30), False, [0, 0], 2, True),    # column kernel (wrap lanes read left of raw x = 0)
+    ("jacobi", (67, 36, 30), False, [0, 0], 2, True),    # ragged x: x faces copied
+    ("jacobi", (64, 36, 30), True, [0, 0], 2, False),    # fp64, every halo copied
+    ("jacobi", (48, 40, 36), False, [0, 0, 0], 1, True),  # single steps
+    ("astaroth", (512, 16, 24), False, [0], 2, True),    # radius 3 (12-B x halos)
+    ("astaroth", (40, 34, 28), True, [0, 0], 1, False)])  # radius 3 fp64 (24-B x halos)
+def test_x_halo_aligned_layout_models(st, kind, size, fp64, gpus, temporal, wrap):
+    """Halo-aligned x layout (LocalDomain.set_x_halo_align): the interior starts 16-B aligned inside its row's first
+    64-B sector, the x halos share the interior's end sectors. The 16-B chunk kernels (whole-row, column, LDS single
+    step) run on it unchanged: bitwise vs the torch oracle and vs the default layout."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    ms = [cls(size, gpus=gpus, fp64=fp64, temporal=temporal, wrap_self=wrap, x_halo_align=a, **kw)
+          for a in (True, False)]
+    for m in ms:
+        m.init()
+    d = ms[0].domain.domain(0)
+    es = d.elem_size(0)
+    first = d.curr_ptr(0) + d.radius().x(-1) * es
+    assert first % 16 == 0 and first % 64 != 0 and d.x_halo_align()
+    assert ms[0].temporal_blocking() == ms[1].temporal_blocking() == (temporal == 2)
+    assert ms[0].wrap_axes() == ms[1].wrap_axes() and ms[0].step_wrap_axes() == ms[1].step_wrap_axes()
+    u = _gather(ms[0])
+    for n in (5, 4):
+        for m in ms:
+            m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        for m in ms:
+            m.synchronize()
+        assert torch.equal(_gather(ms[0]), u)
+        assert torch.equal(_gather(ms[1]), u)
+
+
+@pytest.mark.parametrize("gpus,methods", [([0], "Kernel"), ([0, 0, 0], "Kernel"), ([0, 0], "PeerCopy"),
+                                          ([0, 0], "Staged")])
+@pytest.mark.parametrize("rname", ["r1", "fec", "asym"])
+def test_x_halo_aligned_layout_exchange(st, gpus, methods, rname):
+    radius = _radii(st)[rname]
+    dd = st.DistributedDomain(19, 13, 11, group=st.make_single_group())
+    dd.set_radius(radius)
+    dd.set_gpus(gpus)
+    dd.set_methods(getattr(st.MethodFlags, methods))
+    dd.set_x_halo_align(True)
+    q = dd.add_data("q", torch.int64)
+    q2 = dd.add_data("f", torch.float32)
+    dd.realize()
+    for it in range(2):
+        fill_coords(dd, q)
+        fill_coords(dd, q2)
+        dd.exchange()
+        assert check_exchange(dd, q, radius) == 0 and check_exchange(dd, q2, radius) == 0
+        dd.swap()
+
+
+def test_x_halo_aligned_two_ranks_ipc():
+    """the layout across ranks sharing one GPU (HIP IPC pack/unpack into the aligned halos), fused pairs bitwise"""
+    outs = run_ranks(2, WORKER, ["jacobi", "512,24,40"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": "2", "MP_RANDOM": "1", "MP_X_HALO_ALIGN": "1"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out
