@@ -11,6 +11,7 @@ enum class HipErrorsFatal { NO, YES };
   do {                                                                                                             \
     hipError_t _e = (stmt);                                                                                        \
     if (_e != hipSuccess) {                                                                                        \
+      (void)hipGetLastError(); /* a caught failure must not resurface in the next hipGetLastError() check */       \
       LOG_FATAL("HIP error " << int(_e) << " (" << hipGetErrorString(_e) << ") in `" #stmt "`");                    \
     }                                                                                                              \
   } while (0)
@@ -19,6 +20,7 @@ enum class HipErrorsFatal { NO, YES };
 #define HIP_TRY(stmt)                                                                                              \
   ([&]() {                                                                                                         \
     hipError_t _e = (stmt);                                                                                        \
+    if (_e != hipSuccess) (void)hipGetLastError();                                                                 \
     if (_e != hipSuccess) LOG_DEBUG("HIP error " << int(_e) << " (" << hipGetErrorString(_e) << ") in `" #stmt "`"); \
     return _e;                                                                                                     \
   }())

@@ -926,7 +926,13 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
     for (int ax = 0; ax < 3; ++ax)
       STENCIL_REQUIRE(!((tune.wrap >> ax) & 1) || (lo[ax] == clo[ax] && hi[ax] == chi[ax]),
                       "region " << region << " does not span wrapped axis " << ax << " of " << cr);
-    STENCIL_REQUIRE(alignedLayout && fits && a.x0 == a.lox, "in-kernel wrap needs the aligned vector layout");
+    STENCIL_REQUIRE(alignedLayout && fits && a.x0 == a.lox,
+                    "in-kernel wrap needs the aligned vector layout (aligned " << alignedLayout << ", fits " << fits
+                                                                               << ", x0 " << a.x0 << ", lox " << a.lox
+                                                                               << ", px " << a.px << ", pad "
+                                                                               << dom.pad_x(qi) << ", src%64 "
+                                                                               << (reinterpret_cast<uintptr_t>(a.src) % 64)
+                                                                               << ", nchunks " << a.nchunks << ")");
     a.wrapm = tune.wrap;
     launch_lds<T, 2, 8, KIND, true>(a, tune, stream);
     return;

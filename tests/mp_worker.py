@@ -256,6 +256,42 @@ def scenario_ipcevent():
     return 0 if r["ok"] else 1
 
 
+def scenario_streamloop(size):
+    """blocking exchanges, then stream-ordered exchange_async on a caller (torch) stream, then on the comm streams,
+    with the coordinate oracle after each phase (TransportOptions from MP_*)"""
+    g = st.init_process_group()
+    r = st.Radius.constant(0)
+    r.set_face(2)
+    dd = st.DistributedDomain(*size, group=g)
+    dd.set_transport_options(transport_from_env())
+    dd.set_radius(r)
+    dd.set_gpus([0])
+    dd.set_methods(getattr(st.MethodFlags, "Colocated") | getattr(st.MethodFlags, "Kernel"))
+    q = dd.add_data("c", torch.int64)
+    dd.realize()
+    bad = 0
+    xs = torch.cuda.Stream()
+    for phase in ("blocking", "caller", "comm"):
+        for it in range(4):
+            fill_coords(dd, q, offset=it)
+            if phase == "blocking":
+                dd.exchange()
+            else:
+                dd.exchange_async(xs.cuda_stream if phase == "caller" else 0, 0)
+                xs.synchronize()
+                dd.sync_exchange()
+            bad += check_exchange(dd, q, r, offset=it)
+            dd.swap()
+        print(f"rank {g.rank()} phase {phase} bad {bad}", flush=True)
+    for it in range(6):  # back to back on the caller stream, one synchronize
+        dd.exchange_async(xs.cuda_stream, 0)
+        dd.swap()
+    xs.synchronize()
+    dd.sync_exchange()
+    print(f"rank {g.rank()} streamloop bad {bad}", flush=True)
+    return bad
+
+
 def main():
     # a stalled rank dumps every thread's Python stack (its C++ frames show as the native call it is in) so a hang
     # names its rank, scenario and phase; repeated, in case the first dump lands before the stall
@@ -274,6 +310,8 @@ def main():
         bad = scenario_selftest(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "localint":
         bad = scenario_localint(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
+    elif sc == "streamloop":
+        bad = scenario_streamloop(tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "ipcevent":
         bad = scenario_ipcevent()
     elif sc == "jacobi":

@@ -654,6 +654,18 @@ def test_ipc_event_handle_roundtrip(ranks):
         assert "'ok': True" in out, out[-2000:]
 
 
+@pytest.mark.parametrize("completion", ["Kernel", "StreamOp", "IpcEvent"])
+def test_colocated_caller_stream_two_ranks(completion):
+    """co-located exchanges blocking, stream-ordered on a caller (torch) stream and on the comm streams, each
+    completion kind (bench.py's exchange loops), coordinate oracle"""
+    outs = run_ranks(2, WORKER, ["streamloop", "64,48,80"],
+                     env_extra={"MP_DEVICE": "1", "STENCIL_WAIT_TIMEOUT": "20", "MP_COMPLETION": completion},
+                     timeout=90)
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "streamloop bad 0" in out, out[-2000:]
+
+
 def test_rccl_init_failure_falls_back_to_staged(st):
     """An RCCL communicator that cannot be created (forced) turns every RCCL channel into a host-staged one
     (agreed on by all ranks) instead of aborting; the fused pairs stay exact."""
@@ -848,7 +860,8 @@ def test_topology_links(st):
 
 
 @pytest.mark.parametrize("kind,size,fp64,gpus,temporal,wrap", [
-    ("jacobi", (512, 20, 18), False, [0], 2, True),      # whole-row kernel, x wrapped in-kernel
+    ("jacobi", (512, 120, 116), False, [0], 2, True),    # whole-row kernel, x wrapped in-kernel
+    ("jacobi", (512, 20, 18), False, [0], 2, True),      # thin grid: spheres at the faces, single steps
     ("jacobi", (64, 36, 30), False, [0, 0], 2, True),    # column kernel (wrap lanes read left of raw x = 0)
     ("jacobi", (67, 36, 30), False, [0, 0], 2, True),    # ragged x: x faces copied
     ("jacobi", (64, 36, 30), True, [0, 0], 2, False),    # fp64, every halo copied
@@ -870,7 +883,7 @@ def test_x_halo_aligned_layout_models(st, kind, size, fp64, gpus, temporal, wrap
     es = d.elem_size(0)
     first = d.curr_ptr(0) + d.radius().x(-1) * es
     assert first % 16 == 0 and first % 64 != 0 and d.x_halo_align()
-    assert ms[0].temporal_blocking() == ms[1].temporal_blocking() == (temporal == 2)
+    assert ms[0].temporal_blocking() == ms[1].temporal_blocking() == (temporal == 2 and size[2] > 20)
     assert ms[0].wrap_axes() == ms[1].wrap_axes() and ms[0].step_wrap_axes() == ms[1].step_wrap_axes()
     u = _gather(ms[0])
     for n in (5, 4):
@@ -907,7 +920,7 @@ def test_x_halo_aligned_layout_exchange(st, gpus, methods, rname):
 
 def test_x_halo_aligned_two_ranks_ipc():
     """the layout across ranks sharing one GPU (HIP IPC pack/unpack into the aligned halos), fused pairs bitwise"""
-    outs = run_ranks(2, WORKER, ["jacobi", "512,24,40"],
+    outs = run_ranks(2, WORKER, ["jacobi", "512,120,232"],
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
                                 "MP_TEMPORAL": "2", "MP_RANDOM": "1", "MP_X_HALO_ALIGN": "1"})
     for rc, out in outs:
