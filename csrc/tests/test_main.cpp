@@ -3,7 +3,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <functional>
 #include <string>
 #include <vector>
@@ -417,6 +419,32 @@ TEST(host_self_test_ladder_single_rank, false) {
 TEST(process_group_bounded_barrier, false) {
   auto g = comm::make_single_group();
   CHECK(g->barrier_for(0.1));
+}
+
+TEST(process_group_fork_abandon, false) {
+  // two ranks (threads) over TCP: a fork is a separate group; one rank abandons it mid-sequence, the other times out
+  // there, and the parent group's collective sequence stays in step (the self-test probe's failure path)
+  const int port = comm::find_free_port();
+  std::atomic<int> ok{0};
+  auto body = [&](int r) {
+    auto g = comm::make_tcp_group(r, 2, "127.0.0.1", port, 30.0);
+    auto f = g->fork(1.0);
+    if (f->size() == 2 && f->rank() == r && f->allreduce_sum_u64(1) == 2) ++ok;
+    if (r == 0) {
+      bool threw = false;
+      try {
+        f->barrier(); // rank 1 never joins
+      } catch (const std::exception &) {
+        threw = true;
+      }
+      if (threw) ++ok;
+    }
+    if (g->allreduce_sum_u64(uint64_t(r + 1)) == 3) ++ok;
+  };
+  std::thread t1(body, 1);
+  body(0);
+  t1.join();
+  CHECK(ok.load() == 5);
 }
 
 int main(int argc, char **argv) {
