@@ -224,7 +224,7 @@ std::vector<LinkInfo> links() {
   const int n = device_count();
   for (int a = 0; a < n; ++a)
     for (int b = 0; b < n; ++b) {
-      LinkInfo li{a, b, "self", 0, distance(a, b)};
+      LinkInfo li{a, b, "self", 0, distance(a, b), -1, -1, -1, "none"};
       li.source = "none";
       if (a != b) {
         amdsmi_link_type_t st{};

@@ -14,6 +14,9 @@
 
 namespace stencil {
 
+// "no forwarding target" marker of the halo-forwarding offsets (-2^62: far outside any allocation)
+constexpr int64_t kNoForward = -(int64_t(1) << 62);
+
 // 2.5D z-march. Lane = one 16-B x-chunk; wave = 64 chunks x TY rows; block = 4 waves stacked in y.
 // Per z step a lane issues TY+2 row loads of plane z+1 (plus the two wave-edge scalars), then emits TY rows of
 // plane z from registers: x-neighbours by ds_bpermute, y-neighbours from the adjacent rows, z from prev/next.
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
     for (int i = 0; i < TY; ++i) {
       const int y = ybase + i;
       fsy[i] = y < a.loy + a.fwm[1] ? -1 : (y >= a.hiy - a.fwp[1] ? 1 : 0);
-      fdy[i] = (fsy[i] != 0 && (a.fmask >> (13 + 3 * fsy[i]) & 1u)) ? a.fd[13 + 3 * fsy[i]] : int64_t(-1) << 62;
+      fdy[i] = (fsy[i] != 0 && (a.fmask >> (13 + 3 * fsy[i]) & 1u)) ? a.fd[13 + 3 * fsy[i]] : kNoForward;
     }
     // any message with two or more non-zero components?
     constexpr uint32_t kFaces = (1u << 4) | (1u << 10) | (1u << 12) | (1u << 14) | (1u << 16) | (1u << 22);
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
 
     const int dzh = z - a.hz, dzc = z - a.cz;
     int fsz = 0;
-    int64_t fdz = int64_t(-1) << 62;
+    int64_t fdz = kNoForward;
     if constexpr (FWD) {
       fsz = z < a.loz + a.fwm[2] ? -1 : (z >= a.hiz - a.fwp[2] ? 1 : 0);
       if (fsz != 0 && (a.fmask >> (13 + 9 * fsz) & 1u)) fdz = a.fd[13 + 9 * fsz];
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
               if (fxmPure >> e & 1u) q[e] = out[e];
           }
           // pure y / pure z: wave-uniform, offsets already in SGPRs
-          const bool yrow = fdy[i] != (int64_t(-1) << 62), zrow = fdz != (int64_t(-1) << 62);
+          const bool yrow = fdy[i] != kNoForward, zrow = fdz != kNoForward;
           if (yrow || zrow) {
             NV v;
 #pragma unroll
