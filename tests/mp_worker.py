@@ -271,8 +271,9 @@ def scenario_streamloop(size):
     dd.realize()
     bad = 0
     xs = torch.cuda.Stream()
+    iters = int(os.environ.get("MP_ITERS", "4"))
     for phase in ("blocking", "caller", "comm"):
-        for it in range(4):
+        for it in range(iters):
             fill_coords(dd, q, offset=it)
             if phase == "blocking":
                 dd.exchange()
@@ -283,12 +284,19 @@ def scenario_streamloop(size):
             bad += check_exchange(dd, q, r, offset=it)
             dd.swap()
         print(f"rank {g.rank()} phase {phase} bad {bad}", flush=True)
-    for it in range(6):  # back to back on the caller stream, one synchronize
+    import time
+    n = max(6, 2 * iters)
+    t0 = time.perf_counter()
+    for it in range(n):  # back to back on the caller stream, one synchronize
         dd.exchange_async(xs.cuda_stream, 0)
         dd.swap()
     xs.synchronize()
     dd.sync_exchange()
-    print(f"rank {g.rank()} streamloop bad {bad}", flush=True)
+    dt = (time.perf_counter() - t0) / n * 1e6
+    fill_coords(dd, q, offset=99)
+    dd.exchange()
+    bad += check_exchange(dd, q, r, offset=99)
+    print(f"rank {g.rank()} streamloop bad {bad} back-to-back {dt:.1f} us per exchange", flush=True)
     return bad
 
 

@@ -654,13 +654,14 @@ def test_ipc_event_handle_roundtrip(ranks):
         assert "'ok': True" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("completion", ["Kernel", "StreamOp", "IpcEvent"])
-def test_colocated_caller_stream_two_ranks(completion):
+@pytest.mark.parametrize("completion,iters", [("Kernel", "4"), ("StreamOp", "4"), ("IpcEvent", "4"), ("Kernel", "24"),
+                                              ("IpcEvent", "24")])
+def test_colocated_caller_stream_two_ranks(completion, iters):
     """co-located exchanges blocking, stream-ordered on a caller (torch) stream and on the comm streams, each
-    completion kind (bench.py's exchange loops), coordinate oracle"""
+    completion kind (bench.py's exchange loops), coordinate oracle; 24 per phase: over 100 event records"""
     outs = run_ranks(2, WORKER, ["streamloop", "64,48,80"],
-                     env_extra={"MP_DEVICE": "1", "STENCIL_WAIT_TIMEOUT": "20", "MP_COMPLETION": completion},
-                     timeout=90)
+                     env_extra={"MP_DEVICE": "1", "STENCIL_WAIT_TIMEOUT": "20", "MP_COMPLETION": completion,
+                                "MP_ITERS": iters}, timeout=90)
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "streamloop bad 0" in out, out[-2000:]
