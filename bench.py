@@ -100,13 +100,15 @@ def transport_sweep(st, torch, dist, args, world, device, red_dev, axis_cost, ob
         rec = {}
         ok = 1.0
         dd = None
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(f"[bench] transport {name}: starting", file=sys.stderr, flush=True)
         try:
             if name == "ref_rule":
                 L = st.models.weak_scaled_size(args.per_gpu, world)
                 g, obj, cost = (L, L, L), st.PartitionObjective.Interface, (1, 1, 1)
             else:
                 g, obj, cost = weak_grid(st, args.per_gpu, world, args.grid, axis_cost, objective), objective, axis_cost
-            grp = st.init_process_group(set_default=False, timeout_s=max(30.0, args.sweep_budget))
+            grp = st.init_process_group(set_default=False, timeout_s=15.0)
             dd = st.DistributedDomain(*g, group=grp)
             r = st.Radius.constant(0)
             r.set_face(2)
@@ -123,7 +125,7 @@ def transport_sweep(st, torch, dist, args, world, device, red_dev, axis_cost, ob
             topt.completion = completion
             topt.fuse_flags = topt_base.fuse_flags
             topt.colo_copy = topt.Copy.Engine if copy == "engine" else topt.Copy.Store
-            topt.wait_timeout = max(30.0, args.sweep_budget)
+            topt.wait_timeout = 10.0  # a failing entry gives up within seconds, not minutes
             dd.set_transport_options(topt)
             dd.realize()
             pd = dd.placement_dim()

@@ -22,4 +22,10 @@ struct IpcEventReport {
 // stream takes to drain. ok: every handle opened and every receiver's wait covered (most of) the spin.
 IpcEventReport ipc_event_roundtrip(comm::ProcGroup &pg, int device, double spinS);
 
+// Repeated records of one interprocess event (rank 0) and waits on it (rank 1), `n` times, each wait followed on
+// the receiver by `after`: 0 nothing, 1 hipStreamSynchronize of the waiting stream, 2 that plus hipEventQuery on
+// the opened event, 3 hipEventSynchronize on the opened event instead of the stream wait. Returns the first
+// iteration whose HIP call failed (-1: none) and that call's error string, as "iteration:error".
+std::string ipc_event_stress(comm::ProcGroup &pg, int device, int n, int after);
+
 } // namespace stencil

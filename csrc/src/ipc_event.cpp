@@ -69,4 +69,65 @@ IpcEventReport ipc_event_roundtrip(comm::ProcGroup &pg, int device, double spinS
   return rep;
 }
 
+std::string ipc_event_stress(comm::ProcGroup &pg, int device, int n, int after) {
+  const int me = pg.rank();
+  const uint32_t tagHandle = comm::make_tag(comm::MsgKind::IpcEvent, 1), tagNotify = comm::make_tag(comm::MsgKind::Notify, 1),
+                 tagAck = comm::make_tag(comm::MsgKind::Ack, 1);
+  HIP_CHECK(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t ev = nullptr;
+  int failedAt = -1;
+  std::string err;
+  auto note = [&](int it, hipError_t e, const char *what) {
+    if (e == hipSuccess || failedAt >= 0) return;
+    (void)hipGetLastError();
+    failedAt = it;
+    err = std::string(what) + ": " + hipGetErrorString(e);
+  };
+  if (me == 0) {
+    HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventInterprocess));
+    hipIpcEventHandle_t h{};
+    HIP_CHECK(hipIpcGetEventHandle(&h, ev));
+    if (pg.size() > 1) pg.send(1, tagHandle, &h, sizeof(h));
+  } else if (me == 1) {
+    hipIpcEventHandle_t h{};
+    pg.recv(0, tagHandle, &h, sizeof(h));
+    note(-1, hipIpcOpenEventHandle(&ev, h), "hipIpcOpenEventHandle");
+  }
+  for (int it = 0; it < n && me <= 1 && pg.size() > 1; ++it) {
+    int64_t st = failedAt;
+    if (me == 0) {
+      spin_device(20e-6, s);
+      note(it, hipEventRecord(ev, s), "hipEventRecord");
+      st = failedAt;
+      pg.send(1, tagNotify, &st, sizeof(st));
+      pg.recv(1, tagAck, &st, sizeof(st));
+      if (st >= 0 && failedAt < 0) failedAt = int(st), err = "peer";
+    } else {
+      pg.recv(0, tagNotify, &st, sizeof(st));
+      if (after == 3) {
+        note(it, hipEventSynchronize(ev), "hipEventSynchronize");
+      } else {
+        note(it, hipStreamWaitEvent(s, ev, 0), "hipStreamWaitEvent");
+        spin_device(0.0, s);
+        if (after >= 1) note(it, hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (after >= 2) {
+          const hipError_t q = hipEventQuery(ev);
+          if (q != hipErrorNotReady) note(it, q, "hipEventQuery");
+          else (void)hipGetLastError();
+        }
+      }
+      st = failedAt;
+      pg.send(0, tagAck, &st, sizeof(st));
+    }
+    if (failedAt >= 0) break;
+  }
+  (void)hipStreamSynchronize(s);
+  pg.barrier();
+  if (ev) (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(s);
+  return std::to_string(failedAt) + ":" + err;
+}
+
 } // namespace stencil

@@ -246,6 +246,17 @@ def scenario_localint(backend, methods, size):
     return bad
 
 
+def scenario_ipcstress():
+    """records / waits of one interprocess event, per receiver-side follow-up mode (lab: where does the HIP
+    implementation refuse a wait?)"""
+    g = st.init_process_group()
+    from stencil2_amd import _C
+    for after in (0, 1, 2, 3):
+        r = _C.ipc_event_stress(g, 0, int(os.environ.get("MP_ITERS", "100")), after)
+        print(f"rank {g.rank()} ipcstress after={after} first_failure={r}", flush=True)
+    return 0
+
+
 def scenario_ipcevent():
     """reference test/test_cuda_mpi_cudaipc.cu:8-45: an interprocess event's handle travels from rank 0 to the other
     ranks and opens there; here the receivers also wait on it behind 0.2 s of rank 0's GPU work"""
@@ -320,6 +331,8 @@ def main():
         bad = scenario_localint(backend, methods, tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "streamloop":
         bad = scenario_streamloop(tuple(int(v) for v in sys.argv[2].split(",")))
+    elif sc == "ipcstress":
+        bad = scenario_ipcstress()
     elif sc == "ipcevent":
         bad = scenario_ipcevent()
     elif sc == "jacobi":
