@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <functional>
 #include <set>
@@ -136,9 +137,24 @@ struct Channel {
   char *ownFlag = nullptr, *ownData = nullptr;
   char *remoteFlag = nullptr, *remoteData = nullptr;
   int64_t slotStride = 0;
-  // Completion::IpcEvent: the sender's interprocess event (send channel) / the opened peer event (receive channel)
+  // Completion::IpcEvent: the sender's interprocess event (send channel) / the opened peer event (receive channel),
+  // the records / waits it has served, and replaced events kept until no wait can still reference them
   hipEvent_t ipcEvent = nullptr;
+  int ipcUses = 0;
+  std::deque<std::pair<hipEvent_t, uint64_t>> ipcRetired; // (event, epoch it was replaced at)
 };
+
+// HIP (ROCm 7.2) refuses hipStreamWaitEvent on an opened interprocess event after 32 records of it ("invalid
+// argument" on the 33rd wait; hipEventSynchronize keeps working: `ipc_event_stress`, profiles/r4/ipcevent/). The
+// sender therefore replaces a channel's event after this many records and ships the new handle with the Notify.
+constexpr int kIpcEventUses = 24;
+struct IpcNotify {
+  uint64_t epoch = 0;
+  uint64_t fresh = 0; // 1: `handle` is the channel's new event from this epoch on
+  hipIpcEventHandle_t handle{};
+};
+// a replaced event is destroyed once this many more exchanges have passed (at most two are ever in flight)
+constexpr uint64_t kIpcRetireEpochs = 8;
 
 // PeerCopy over a DMA engine (TransportOptions::peerCopy == Engine): every message from one local sub-domain to
 // another (on a peer GPU of this process) is packed into sbuf on the source GPU, copied by hipMemcpyPeerAsync into
@@ -257,6 +273,7 @@ DistributedDomain::~DistributedDomain() {
     if (c.dbuf) (void)hipFree(c.dbuf);
     if (c.hbuf) (void)hipHostFree(c.hbuf);
     if (c.ipcEvent) (void)hipEventDestroy(c.ipcEvent);
+    for (auto &r : c.ipcRetired) (void)hipEventDestroy(r.first);
     if (c.remoteFlag) (void)hipIpcCloseMemHandle(c.remoteFlag);
     if (c.remoteData) (void)hipIpcCloseMemHandle(c.remoteData);
   }
@@ -1858,9 +1875,22 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
           STENCIL_REQUIRE(acked == I.epoch - 2, "IPC-event ack out of order: got epoch " << acked << ", want "
                                                                                           << I.epoch - 2);
         }
+        IpcNotify msg;
+        msg.epoch = I.epoch;
+        if (c.ipcUses >= kIpcEventUses) { // a fresh event before HIP's per-event record limit
+          c.ipcRetired.emplace_back(c.ipcEvent, I.epoch);
+          HIP_CHECK(hipEventCreateWithFlags(&c.ipcEvent, hipEventDisableTiming | hipEventInterprocess));
+          HIP_CHECK(hipIpcGetEventHandle(&msg.handle, c.ipcEvent));
+          msg.fresh = 1;
+          c.ipcUses = 0;
+        }
+        while (!c.ipcRetired.empty() && I.epoch - c.ipcRetired.front().second >= kIpcRetireEpochs) {
+          (void)hipEventDestroy(c.ipcRetired.front().first);
+          c.ipcRetired.pop_front();
+        }
         HIP_CHECK(hipEventRecord(c.ipcEvent, S(ctx)));
-        const uint64_t e = I.epoch;
-        pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::Notify), &e, sizeof(e));
+        ++c.ipcUses;
+        pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::Notify), &msg, sizeof(msg));
       }
       continue;
     }
@@ -1967,10 +1997,20 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     if (ipcEvt) { // per channel: Notify(epoch) -> wait on the sender's event -> Ack(epoch); unpack + credits
       for (int ci : ctx.coloRecv) {
         Channel &c = I.chans[size_t(ci)];
-        uint64_t e = 0;
-        pg.recv(c.remoteRank, retag(c.tag, comm::MsgKind::Notify), &e, sizeof(e));
-        STENCIL_REQUIRE(e == I.epoch, "IPC-event notify out of order: got epoch " << e << ", want " << I.epoch);
+        IpcNotify msg;
+        pg.recv(c.remoteRank, retag(c.tag, comm::MsgKind::Notify), &msg, sizeof(msg));
+        STENCIL_REQUIRE(msg.epoch == I.epoch,
+                        "IPC-event notify out of order: got epoch " << msg.epoch << ", want " << I.epoch);
+        if (msg.fresh) { // the sender replaced its event: open the new one, keep the old until no wait needs it
+          c.ipcRetired.emplace_back(c.ipcEvent, I.epoch);
+          HIP_CHECK(hipIpcOpenEventHandle(&c.ipcEvent, msg.handle));
+        }
+        while (!c.ipcRetired.empty() && I.epoch - c.ipcRetired.front().second >= kIpcRetireEpochs) {
+          (void)hipEventDestroy(c.ipcRetired.front().first);
+          c.ipcRetired.pop_front();
+        }
         HIP_CHECK(hipStreamWaitEvent(S(ctx), c.ipcEvent, 0));
+        const uint64_t e = I.epoch;
         pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::Ack), &e, sizeof(e));
       }
       FlagSyncArgs fa;
