@@ -13,13 +13,15 @@ using namespace stencil;
 int main(int argc, char **argv) {
   int64_t x = 512, y = 512, z = 512;
   int iters = 5, nq = 8, temporal = 1;
-  bool noOverlap = false, weak = false, fp64 = false;
+  bool noOverlap = false, weak = false, fp64 = false, noWrap = false;
   app::MethodArgs ma;
   ArgParser p("Astaroth proxy (reference bin/astaroth_sim.cu)");
   p.option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z").option(&iters, "-n,--iters", "iterations")
       .option(&nq, "--q", "quantities")
       .option(&temporal, "--temporal", "steps fused per sweep (1 or 2)")
       .flag(&noOverlap, "--no-overlap", "no overlap")
+      .flag(&noWrap, "--no-wrap", "exchange every periodic self-halo each sweep (the reference's per-iteration "
+                                  "exchange, bin/astaroth_sim.cu:223-274) instead of reading the periodic image")
       .flag(&weak, "--weak", "treat x,y,z as per-GPU sizes").flag(&fp64, "--fp64", "fp64 quantities");
   ma.add(p);
   if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
@@ -40,6 +42,7 @@ int main(int argc, char **argv) {
   cfg.methods = ma.flags();
   cfg.placement = ma.placement();
   cfg.overlap = !noOverlap;
+  cfg.wrapSelf = !noWrap;
   StencilModel m(cfg, pg);
   m.init();
   const int per = m.temporal_blocking() ? 2 : 1; // timed unit = one sweep, reported per step

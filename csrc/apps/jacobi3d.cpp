@@ -16,7 +16,7 @@ using namespace stencil;
 
 int main(int argc, char **argv) {
   bool staged = false, rccl = false, colo = false, peer = false, kernel = false, trivial = false, noOverlap = false,
-       paraview = false, fp64 = false;
+       paraview = false, fp64 = false, noWrap = false;
   std::string prefix;
   int iters = 30, period = -1, warmup = 3, temporal = 1;
   int64_t x = 512, y = 512, z = 512;
@@ -30,6 +30,7 @@ int main(int argc, char **argv) {
       .flag(&noOverlap, "--no-overlap", "do not overlap interior compute with the exchange")
       .flag(&paraview, "--paraview", "dump ParaView CSV files")
       .flag(&fp64, "--fp64", "double precision")
+      .flag(&noWrap, "--no-wrap", "copy every periodic self-halo instead of reading the periodic image in-kernel")
       .option(&prefix, "--prefix", "ParaView file prefix")
       .option(&iters, "-n,--iters", "iterations")
       .option(&warmup, "--warmup", "untimed warmup iterations")
@@ -55,6 +56,7 @@ int main(int argc, char **argv) {
   cfg.radius = 1;
   cfg.fp64 = fp64;
   cfg.temporal = temporal;
+  cfg.wrapSelf = !noWrap;
   MethodFlags m = MethodFlags::None;
   if (staged) m |= MethodFlags::Staged;
   if (rccl) m |= MethodFlags::Rccl;
