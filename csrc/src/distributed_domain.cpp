@@ -1466,9 +1466,24 @@ void DistributedDomain::set_completion(TransportOptions::Completion c) {
                       exchange_bytes_for_method(MethodFlags::Colocated) == 0,
                   "Completion::IpcEvent needs its interprocess events: realize() with that completion");
   if (realized_) sync_exchange(); // flag words are monotonic epochs: either method continues where the other left off
+  Impl &I = *impl_;
+  if (realized_ && topt_.completion == TransportOptions::Completion::IpcEvent && backend_ == Backend::Device) {
+    // leaving IpcEvent: take the acknowledgements of the last two exchanges that no later record will consume, so a
+    // later switch back finds no stale Ack queued
+    for (auto &ctx : I.devs)
+      for (int ci : ctx.coloSend) {
+        Channel &ch = I.chans[size_t(ci)];
+        for (uint64_t e = I.epoch >= 1 ? I.epoch - 1 : 0; e <= I.epoch; ++e) {
+          if (e == 0 || e < I.ipcEventFirstEpoch) continue;
+          uint64_t acked = 0;
+          pg_->recv(ch.remoteRank, retag(ch.tag, comm::MsgKind::Ack), &acked, sizeof(acked));
+          STENCIL_REQUIRE(acked == e, "IPC-event ack out of order: got epoch " << acked << ", want " << e);
+        }
+      }
+  }
   topt_.completion = c;
   // every rank switches between the same two exchanges: acknowledgements exist from the next epoch on
-  if (c == TransportOptions::Completion::IpcEvent) impl_->ipcEventFirstEpoch = impl_->epoch + 1;
+  if (c == TransportOptions::Completion::IpcEvent) I.ipcEventFirstEpoch = I.epoch + 1;
 }
 
 const char *to_string(TransportOptions::Inbox v) {

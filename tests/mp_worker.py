@@ -307,6 +307,16 @@ def scenario_streamloop(size):
     fill_coords(dd, q, offset=99)
     dd.exchange()
     bad += check_exchange(dd, q, r, offset=99)
+    if os.environ.get("MP_SWITCH") == "1":  # completion switched between exchanges (every rank at the same point)
+        C = st.TransportOptions.Completion
+        for k, c in enumerate((C.Kernel, C.IpcEvent, C.StreamOp, C.IpcEvent, C.Kernel)):
+            dd.set_completion(c)
+            for it in range(30 if c == C.IpcEvent else 3):
+                fill_coords(dd, q, offset=1000 * k + it)
+                dd.exchange()
+                bad += check_exchange(dd, q, r, offset=1000 * k + it)
+                dd.swap()
+        print(f"rank {g.rank()} switch bad {bad}", flush=True)
     print(f"rank {g.rank()} streamloop bad {bad} back-to-back {dt:.1f} us per exchange", flush=True)
     return bad
 

@@ -667,6 +667,17 @@ def test_colocated_caller_stream_two_ranks(completion, iters):
         assert "streamloop bad 0" in out, out[-2000:]
 
 
+def test_colocated_completion_switching_two_ranks():
+    """set_completion between exchanges: interprocess events (realized with them) -> spin kernels -> events again
+    (30 exchanges: past the event replacement) -> stream ops -> events -> kernels; coordinate oracle throughout"""
+    outs = run_ranks(2, WORKER, ["streamloop", "64,48,80"],
+                     env_extra={"MP_DEVICE": "1", "STENCIL_WAIT_TIMEOUT": "20", "MP_COMPLETION": "IpcEvent",
+                                "MP_SWITCH": "1"}, timeout=120)
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "switch bad 0" in out, out[-2000:]
+
+
 def test_rccl_init_failure_falls_back_to_staged(st):
     """An RCCL communicator that cannot be created (forced) turns every RCCL channel into a host-staged one
     (agreed on by all ranks) instead of aborting; the fused pairs stay exact."""
