@@ -509,6 +509,9 @@ def main():
     for _ in range(3):  # untimed: the first full exchanges after wrapped pairs touch cold halo lines
         dd.exchange()
         dd.swap()
+    colo_log = colo and topt.completion != topt.Completion.StreamOp
+    if colo_log:  # device timestamps of the fused co-located kernels (wait vs copy), no host cost
+        dd.set_transport_log(args.exchange_iters)
     barrier()
     t1 = time.perf_counter()
     for _ in range(args.exchange_iters):
@@ -516,6 +519,9 @@ def main():
         dd.swap()
     torch.cuda.synchronize()
     xel = time.perf_counter() - t1
+    colo_phases = colo_breakdown(dd.transport_log(0)) if colo_log else None
+    if colo_log:
+        dd.set_transport_log(0)
     tx = torch.tensor([xel], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tx, op=dist.ReduceOp.MAX)
@@ -583,7 +589,8 @@ def main():
             "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_exchange_stream_GBps": round(xgbs_stream, 3),
                       "halo_bytes_per_exchange": int(xbytes),
                       "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
-                      "gcells_per_gpu": round(gcells / n, 3), "transports": transports},
+                      "gcells_per_gpu": round(gcells / n, 3), "colo_kernels_us": colo_phases,
+                      "transports": transports},
         }
         print(json.dumps(out), flush=True)
     if world > 1:
