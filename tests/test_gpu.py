@@ -938,3 +938,36 @@ def test_x_halo_aligned_two_ranks_ipc():
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out
+
+
+def test_exchange_random_radius_maps_device(st):
+    """property test on the device: random radius maps, sizes, 1-4 sub-domains per GPU, element
+    types and x layouts, through a random same-process transport (direct stores, DMA-engine pipes, host-staged)"""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as hs
+    from test_exchange_property import exchange_case, _radius
+
+    @settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+    @given(exchange_case(), hs.sampled_from(["Kernel", "PeerCopy", "PeerCopyEngine", "Staged"]))
+    def run(case, method):
+        radii, n, size, dtype, align = case
+        radius = _radius(st, radii)
+        tr = st.TransportOptions()
+        if method == "PeerCopyEngine":
+            tr.peer_copy = st.TransportOptions.Copy.Engine
+            method = "PeerCopy"
+        dd = st.DistributedDomain(*size, group=st.make_single_group())
+        dd.set_transport_options(tr)
+        dd.set_radius(radius)
+        dd.set_gpus([0] * n)
+        dd.set_methods(getattr(st.MethodFlags, method))
+        dd.set_x_halo_align(align)
+        q = dd.add_data("q", dtype)
+        dd.realize()
+        for it in range(2):
+            fill_coords(dd, q, offset=it)
+            dd.exchange()
+            assert check_exchange(dd, q, radius, offset=it) == 0, (case, method)
+            dd.swap()
+
+    run()
