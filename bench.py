@@ -304,6 +304,8 @@ def main():
     ap.add_argument("--x-halo-align", type=int, default=0,
                     help="x halos inside the interior's first / last 64-B sector (LocalDomain::set_x_halo_align): "
                          "one sector per row end for x-face copies; every row spans one more sector")
+    ap.add_argument("--interior-align", type=int, default=64, choices=[64, 128],
+                    help="byte alignment of every row's first interior cell (128: whole L2 lines per 512-cell row)")
     ap.add_argument("--axis-cost", default="4,3,2",
                     help="NodeAware partition cost per interface cell of x,y,z cuts (1,1,1 = the reference's rule)")
     ap.add_argument("--partition", choices=["maxlink", "interface"], default="maxlink",
@@ -418,7 +420,8 @@ def main():
     model = st.Jacobi3D(grid, gpus=[device], methods=methods, overlap=overlap,
                         auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
                         axis_cost=axis_cost, partition=objective, wrap_self=bool(args.wrap), transport=topt,
-                        self_test=bool(args.self_test) and world > 1, x_halo_align=bool(args.x_halo_align))
+                        self_test=bool(args.self_test) and world > 1, x_halo_align=bool(args.x_halo_align),
+                        interior_align=args.interior_align)
     model.init()
     methods = model.domain.methods()
     preflight = model.domain.self_test_report() or "skipped"
@@ -552,7 +555,7 @@ def main():
     model_cfg = {
         "decomposition": f"{pdim.x}x{pdim.y}x{pdim.z}", "methods": st.methods_to_string(methods), "preflight": preflight,
         "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
-        "x_halo_align": bool(args.x_halo_align),
+        "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
         "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
         "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched,
         "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,

@@ -20,6 +20,7 @@
 
 #include "stencil/core/geometry.hpp"
 #include "stencil/kernels/copy.hpp"
+#include "stencil/rt/logging.hpp"
 
 namespace stencil {
 
@@ -64,6 +65,13 @@ public:
   void set_radius(const Radius &r) { radius_ = r; }
   void set_padding(bool pad) { pad_ = pad; }
   void set_x_halo_align(bool on) { xHaloAlign_ = on; }
+  // byte alignment of the first interior x of every row (64 = one sector, default; 128 = one L2 line: a 512-cell fp32
+  // row then spans 16 lines instead of 17)
+  void set_interior_align(int64_t bytes) {
+    STENCIL_REQUIRE(bytes == 64 || bytes == 128, "interior alignment must be 64 or 128 B");
+    interiorAlign_ = bytes;
+  }
+  int64_t interior_align() const { return interiorAlign_; }
   bool x_halo_align() const { return xHaloAlign_; }
   void realize();
   bool realized() const { return realized_; }
@@ -151,6 +159,7 @@ private:
   Backend backend_;
   bool pad_ = true;
   bool xHaloAlign_ = false;
+  int64_t interiorAlign_ = 64;
   int64_t guard_ = 0; // bytes before the first row of every buffer (halo-aligned layout)
   bool realized_ = false;
   int parity_ = 0;

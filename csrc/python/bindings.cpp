@@ -432,6 +432,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_padding", &LocalDomain::set_padding)
       .def("set_x_halo_align", &LocalDomain::set_x_halo_align)
       .def("x_halo_align", &LocalDomain::x_halo_align)
+      .def("set_interior_align", &LocalDomain::set_interior_align)
+      .def("interior_align", &LocalDomain::interior_align)
       .def("front_slack", &LocalDomain::front_slack)
       .def("realize", &LocalDomain::realize)
       .def("swap", &LocalDomain::swap)
@@ -586,6 +588,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_padding", &DistributedDomain::set_padding)
       .def("set_x_halo_align", &DistributedDomain::set_x_halo_align)
       .def("x_halo_align", &DistributedDomain::x_halo_align)
+      .def("set_interior_align", &DistributedDomain::set_interior_align)
+      .def("interior_align", &DistributedDomain::interior_align)
       .def("set_transport_options", &DistributedDomain::set_transport_options)
       .def("transport_options", &DistributedDomain::transport_options)
       .def("set_colo_copy", &DistributedDomain::set_colo_copy, py::call_guard<py::gil_scoped_release>())
@@ -727,6 +731,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("temporal", &StencilModelConfig::temporal)
       .def_readwrite("wrap_self", &StencilModelConfig::wrapSelf)
       .def_readwrite("x_halo_align", &StencilModelConfig::xHaloAlign)
+      .def_readwrite("interior_align", &StencilModelConfig::interiorAlign)
       .def_readwrite("wrap_axes_mask", &StencilModelConfig::wrapAxesMask)
       .def_readwrite("local_interior", &StencilModelConfig::localInterior)
       .def_readwrite("overlap_mode", &StencilModelConfig::overlapMode)

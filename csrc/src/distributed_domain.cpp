@@ -378,6 +378,7 @@ int64_t DistributedDomain::probe_transports(MethodFlags m) {
     p.set_transport_options(topt_);
     p.set_plan_file("");
     p.set_x_halo_align(xHaloAlign_);
+    p.set_interior_align(interiorAlign_);
     p.add_data(4, "probe", DType::I32);
     try {
       p.realize();
@@ -664,6 +665,7 @@ void DistributedDomain::realize() {
     d.set_radius(radius_);
     d.set_padding(pad_);
     d.set_x_halo_align(xHaloAlign_);
+    d.set_interior_align(interiorAlign_);
     for (size_t q = 0; q < elemSize_.size(); ++q) d.add_data(elemSize_[q], names_[q], dtypes_[q]);
     LOG_INFO("rank " << myRank << " domain " << di << " idx " << idx << " size " << d.size() << " origin " << d.origin()
                      << " device " << device);

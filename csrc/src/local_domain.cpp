@@ -15,7 +15,7 @@ LocalDomain::LocalDomain(const Dim3 &sz, const Dim3 &origin, int dev, Backend ba
 
 LocalDomain::LocalDomain(LocalDomain &&o) noexcept
     : sz_(o.sz_), origin_(o.origin_), radius_(o.radius_), dev_(o.dev_), backend_(o.backend_), pad_(o.pad_),
-      xHaloAlign_(o.xHaloAlign_), guard_(o.guard_), realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
+      xHaloAlign_(o.xHaloAlign_), interiorAlign_(o.interiorAlign_), guard_(o.guard_), realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
       names_(std::move(o.names_)), pitchX_(std::move(o.pitchX_)), padX_(std::move(o.padX_)),
       curr_(std::move(o.curr_)), next_(std::move(o.next_)) {
   base_[0] = std::move(o.base_[0]);
@@ -78,8 +78,8 @@ void LocalDomain::realize() {
   guard_ = haloAligned ? 128 : 0;
   for (int64_t q = 0; q < nq; ++q) {
     const int64_t es = elemSize_[q];
-    if (pad_ && 64 % es == 0) {
-      const int64_t perLine = 64 / es; // elements per 64 B
+    if (pad_ && interiorAlign_ % es == 0) {
+      const int64_t perLine = interiorAlign_ / es; // elements per interior alignment unit (64 or 128 B)
       if (haloAligned && 16 % es == 0 && rxm * es <= kMaxAlignedHaloBytes && rxp * es <= kMaxAlignedHaloBytes) {
         // interior at the first 16-B boundary at or after the -x halo (inside the row's first sector)
         padX_[q] = (round_up(rxm * es, 16) - rxm * es) / es;

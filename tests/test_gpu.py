@@ -971,3 +971,23 @@ def test_exchange_random_radius_maps_device(st):
             dd.swap()
 
     run()
+
+
+@pytest.mark.parametrize("kind,size,gpus,temporal", [("jacobi", (512, 120, 116), [0], 2), ("jacobi", (64, 36, 30), [0, 0], 2),
+                                                     ("astaroth", (512, 16, 24), [0], 2), ("jacobi", (48, 40, 36), [0, 0, 0], 1)])
+def test_interior_align_128_models(st, kind, size, gpus, temporal):
+    """interior_align=128: every row's first interior cell on an L2-line boundary; kernels unchanged, bitwise"""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    m = cls(size, gpus=gpus, temporal=temporal, interior_align=128, **kw)
+    m.init()
+    d = m.domain.domain(0)
+    assert (d.curr_ptr(0) + d.radius().x(-1) * d.elem_size(0)) % 128 == 0
+    assert m.temporal_blocking() == (temporal == 2)
+    u = _gather(m)
+    m.run(5)
+    for _ in range(5):
+        u = ref(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
