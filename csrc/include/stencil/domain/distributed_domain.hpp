@@ -202,7 +202,7 @@ public:
   // halo-aligned x layout of every local domain (LocalDomain::set_x_halo_align)
   void set_x_halo_align(bool on) { xHaloAlign_ = on; }
   bool x_halo_align() const { return xHaloAlign_; }
-  // LocalDomain::set_interior_align of every local domain (64 or 128 B)
+  // LocalDomain::set_interior_align of every local domain (128 B default, or 64)
   void set_interior_align(int64_t bytes) { interiorAlign_ = bytes; }
   int64_t interior_align() const { return interiorAlign_; }
   // opt-in self-test ladder run by realize() before planning (multi-rank runs): exchange a coordinate-encoded field
@@ -351,7 +351,7 @@ private:
   bool realized_ = false;
   bool pad_ = true;
   bool xHaloAlign_ = false;
-  int64_t interiorAlign_ = 64;
+  int64_t interiorAlign_ = 128;
   TransportOptions topt_;
   bool selfTest_ = false;
   std::string selfTestReport_;

@@ -4,8 +4,9 @@
 //   add_data / set_radius / realize / get_curr / get_next / accessors / halo_pos / halo_extent /
 //   halo_coords / halo_bytes / raw_size / size / origin / gpu / swap / region_to_host / interior_to_host /
 //   quantity_to_host
-// MI355X layout: the x pitch is padded so the first interior x of every row is 64-B aligned and
-// every row starts on a 128-B line; y/z are unpadded. Halo-aligned x (set_x_halo_align, x halos of at most 48 B):
+// MI355X layout: the x pitch is padded so the first interior x of every row is 128-B aligned (one
+// L2 line; set_interior_align(64) for the rounds-1-3 sector alignment) and every row starts on a 128-B line; y/z are
+// unpadded. Halo-aligned x (set_x_halo_align, x halos of at most 48 B):
 // the interior starts 16-B aligned inside the row's first 64-B sector, with the -x halo directly in front of it in
 // that same sector and the +x halo directly behind the interior's last cells, so an x-face copy touches one sector
 // per row end instead of two (the stencil kernels' 16-B chunk grid still starts at the interior; a row then spans
@@ -65,8 +66,9 @@ public:
   void set_radius(const Radius &r) { radius_ = r; }
   void set_padding(bool pad) { pad_ = pad; }
   void set_x_halo_align(bool on) { xHaloAlign_ = on; }
-  // byte alignment of the first interior x of every row (64 = one sector, default; 128 = one L2 line: a 512-cell fp32
-  // row then spans 16 lines instead of 17)
+  // byte alignment of the first interior x of every row: 128 (default) = one L2 line, so a 512-cell fp32 row spans 16
+  // lines instead of 17 (one MI355X, fused pairs at 512^3: 1150-1194 -> 1285-1287 Gcells/s, FETCH_SIZE 296 -> 279 MB
+  // per pair; profiles/r4/i/); 64 = one sector (rounds 1-3)
   void set_interior_align(int64_t bytes) {
     STENCIL_REQUIRE(bytes == 64 || bytes == 128, "interior alignment must be 64 or 128 B");
     interiorAlign_ = bytes;
@@ -159,7 +161,7 @@ private:
   Backend backend_;
   bool pad_ = true;
   bool xHaloAlign_ = false;
-  int64_t interiorAlign_ = 64;
+  int64_t interiorAlign_ = 128;
   int64_t guard_ = 0; // bytes before the first row of every buffer (halo-aligned layout)
   bool realized_ = false;
   int parity_ = 0;

@@ -67,7 +67,7 @@ struct StencilModelConfig {
   // halo-aligned x layout (DistributedDomain::set_x_halo_align): x halos share the interior's first / last 64-B
   // sector (x-face copies touch one sector per row end instead of two; every row spans one more sector)
   bool xHaloAlign = false;
-  int64_t interiorAlign = 64; // DistributedDomain::set_interior_align (64 or 128 B)
+  int64_t interiorAlign = 128; // DistributedDomain::set_interior_align (128 B default, or 64)
   TransportOptions transport; // DistributedDomain::set_transport_options
   bool selfTest = false;      // DistributedDomain::set_self_test (multi-rank: verified transport ladder)
   bool setBackend = false;

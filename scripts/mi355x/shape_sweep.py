@@ -16,7 +16,7 @@ ap.add_argument("--x2sched", default="1")
 ap.add_argument("--x2row", default="1,0", help="whole-row kernel on/off (StencilTune.x2row)")
 ap.add_argument("--x2xfast", default="0", help="fused-pair column order: 1 x-major, 0 y-major (list)")
 ap.add_argument("--x2pf", default="3", help="fused-pair planes of lookahead (list)")
-ap.add_argument("--interior-align", default="64", help="LocalDomain interior alignment in bytes (list: 64,128)")
+ap.add_argument("--interior-align", default="128", help="LocalDomain interior alignment in bytes (list: 64,128)")
 ap.add_argument("--fp64", action="store_true")
 args = ap.parse_args()
 for sched, row, xf, pf, al in ((int(a), int(b), int(c), int(d), int(e)) for a in args.x2sched.split(",")

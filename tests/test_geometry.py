@@ -84,13 +84,14 @@ def test_packed_layout_264_bytes(st):
 
 
 def test_padded_pitch_alignment(st):
-    """x pitch padded so the first interior x of every row is 64-B aligned."""
+    """x pitch padded so the first interior x of every row is 128-B aligned (one L2 line), or 64-B
+    with set_interior_align(64)."""
     for rx in (1, 2, 3, 5):
         ld = _ld(st, (37, 5, 4), st.Radius.constant(rx), ((4, "F32"), (8, "F64")))
         for q, es in ((0, 4), (1, 8)):
             p = ld.pitch(q)
             assert (p.x * es) % 128 == 0
-            assert ((ld.pad_x(q) + rx) * es) % 64 == 0
+            assert ((ld.pad_x(q) + rx) * es) % 128 == 0
             assert p.x >= ld.pad_x(q) + ld.raw_size().x + 16 // es + 1
 
 
@@ -112,3 +113,16 @@ def test_x2_lockstep_schedule(st):
     assert f(256, 512, 1024) == (1, 256, 2)   # fp64 1024^3: 4 x 128 columns, 2 rounds
     assert f(256, 64, 40) == (0, 0, 1)        # thin grids: balanced split
     assert f(256, 17, 200) == (0, 0, 1)       # 15 parts of 13 planes: too short
+
+
+def test_interior_align_64_option(st):
+    """set_interior_align(64): the rounds-1-3 layout, first interior x on a 64-B sector"""
+    from stencil2_amd import _C
+    for rx in (1, 2, 3):
+        ld = _C.LocalDomain(st.Dim3(37, 5, 4), st.Dim3(0, 0, 0), -1, st.Backend.Host)
+        ld.set_radius(st.Radius.constant(rx))
+        ld.set_interior_align(64)
+        ld.add_data(4, "", st.DType.F32)
+        ld.realize()
+        assert ld.interior_align() == 64
+        assert ((ld.pad_x(0) + rx) * 4) % 64 == 0 and ld.pad_x(0) < 16 and (ld.pitch(0).x * 4) % 128 == 0
