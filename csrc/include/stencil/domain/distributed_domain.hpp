@@ -205,6 +205,7 @@ public:
   // LocalDomain::set_interior_align of every local domain (128 B default, or 64)
   void set_interior_align(int64_t bytes) { interiorAlign_ = bytes; }
   int64_t interior_align() const { return interiorAlign_; }
+  void set_row_pad_lines(int n) { rowPadLines_ = n; } // LocalDomain::set_row_pad_lines of every local domain
   // opt-in self-test ladder run by realize() before planning (multi-rank runs): exchange a coordinate-encoded field
   // on a small probe domain built like this one and check every halo cell on every rank; on any wrong cell or
   // error drop Colocated, then Rccl (-> host-staged), i.e. the reference's always-terminating ladder
@@ -352,6 +353,7 @@ private:
   bool pad_ = true;
   bool xHaloAlign_ = false;
   int64_t interiorAlign_ = 128;
+  int rowPadLines_ = 0;
   TransportOptions topt_;
   bool selfTest_ = false;
   std::string selfTestReport_;

@@ -74,6 +74,9 @@ public:
     interiorAlign_ = bytes;
   }
   int64_t interior_align() const { return interiorAlign_; }
+  // extra 128-B lines appended to every row's pitch (measurement knob: row / plane strides vs HBM channel mapping)
+  void set_row_pad_lines(int n) { rowPadLines_ = n; }
+  int row_pad_lines() const { return rowPadLines_; }
   bool x_halo_align() const { return xHaloAlign_; }
   void realize();
   bool realized() const { return realized_; }
@@ -162,6 +165,7 @@ private:
   bool pad_ = true;
   bool xHaloAlign_ = false;
   int64_t interiorAlign_ = 128;
+  int rowPadLines_ = 0;
   int64_t guard_ = 0; // bytes before the first row of every buffer (halo-aligned layout)
   bool realized_ = false;
   int parity_ = 0;

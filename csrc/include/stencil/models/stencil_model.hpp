@@ -68,6 +68,7 @@ struct StencilModelConfig {
   // sector (x-face copies touch one sector per row end instead of two; every row spans one more sector)
   bool xHaloAlign = false;
   int64_t interiorAlign = 128; // DistributedDomain::set_interior_align (128 B default, or 64)
+  int rowPadLines = 0;          // DistributedDomain::set_row_pad_lines (measurement knob)
   TransportOptions transport; // DistributedDomain::set_transport_options
   bool selfTest = false;      // DistributedDomain::set_self_test (multi-rank: verified transport ladder)
   bool setBackend = false;

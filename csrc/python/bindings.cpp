@@ -433,6 +433,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_x_halo_align", &LocalDomain::set_x_halo_align)
       .def("x_halo_align", &LocalDomain::x_halo_align)
       .def("set_interior_align", &LocalDomain::set_interior_align)
+      .def("set_row_pad_lines", &LocalDomain::set_row_pad_lines)
       .def("interior_align", &LocalDomain::interior_align)
       .def("front_slack", &LocalDomain::front_slack)
       .def("realize", &LocalDomain::realize)
@@ -589,6 +590,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_x_halo_align", &DistributedDomain::set_x_halo_align)
       .def("x_halo_align", &DistributedDomain::x_halo_align)
       .def("set_interior_align", &DistributedDomain::set_interior_align)
+      .def("set_row_pad_lines", &DistributedDomain::set_row_pad_lines)
       .def("interior_align", &DistributedDomain::interior_align)
       .def("set_transport_options", &DistributedDomain::set_transport_options)
       .def("transport_options", &DistributedDomain::transport_options)
@@ -732,6 +734,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("wrap_self", &StencilModelConfig::wrapSelf)
       .def_readwrite("x_halo_align", &StencilModelConfig::xHaloAlign)
       .def_readwrite("interior_align", &StencilModelConfig::interiorAlign)
+      .def_readwrite("row_pad_lines", &StencilModelConfig::rowPadLines)
       .def_readwrite("wrap_axes_mask", &StencilModelConfig::wrapAxesMask)
       .def_readwrite("local_interior", &StencilModelConfig::localInterior)
       .def_readwrite("overlap_mode", &StencilModelConfig::overlapMode)

@@ -666,6 +666,7 @@ void DistributedDomain::realize() {
     d.set_padding(pad_);
     d.set_x_halo_align(xHaloAlign_);
     d.set_interior_align(interiorAlign_);
+    d.set_row_pad_lines(rowPadLines_);
     for (size_t q = 0; q < elemSize_.size(); ++q) d.add_data(elemSize_[q], names_[q], dtypes_[q]);
     LOG_INFO("rank " << myRank << " domain " << di << " idx " << idx << " size " << d.size() << " origin " << d.origin()
                      << " device " << device);

@@ -15,7 +15,7 @@ LocalDomain::LocalDomain(const Dim3 &sz, const Dim3 &origin, int dev, Backend ba
 
 LocalDomain::LocalDomain(LocalDomain &&o) noexcept
     : sz_(o.sz_), origin_(o.origin_), radius_(o.radius_), dev_(o.dev_), backend_(o.backend_), pad_(o.pad_),
-      xHaloAlign_(o.xHaloAlign_), interiorAlign_(o.interiorAlign_), guard_(o.guard_), realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
+      xHaloAlign_(o.xHaloAlign_), interiorAlign_(o.interiorAlign_), rowPadLines_(o.rowPadLines_), guard_(o.guard_), realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
       names_(std::move(o.names_)), pitchX_(std::move(o.pitchX_)), padX_(std::move(o.padX_)),
       curr_(std::move(o.curr_)), next_(std::move(o.next_)) {
   base_[0] = std::move(o.base_[0]);
@@ -89,7 +89,7 @@ void LocalDomain::realize() {
       const int64_t rowAlign = (128 % es == 0) ? 128 / es : 1;
       // tail: one 16-B vector + 1 element so vectorized row sweeps never leave the allocation
       const int64_t tail = (16 % es == 0) ? 16 / es + 1 : 1;
-      pitchX_[q] = round_up(padX_[q] + raw.x + tail, rowAlign);
+      pitchX_[q] = round_up(padX_[q] + raw.x + tail, rowAlign) + int64_t(rowPadLines_) * rowAlign;
     }
     total += 2 * (buffer_bytes(q) + guard_);
   }

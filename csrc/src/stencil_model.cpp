@@ -35,6 +35,7 @@ StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::
   dd_->set_transport_options(cfg.transport);
   dd_->set_x_halo_align(cfg.xHaloAlign);
   dd_->set_interior_align(cfg.interiorAlign);
+  dd_->set_row_pad_lines(cfg.rowPadLines);
   dd_->set_self_test(cfg.selfTest);
   for (int q = 0; q < cfg.quantities; ++q) {
     const std::string name = cfg.kind == StencilKind::Jacobi && cfg.quantities == 1 ? "d" : "d" + std::to_string(q);

@@ -18,10 +18,12 @@ ap.add_argument("--x2xfast", default="0", help="fused-pair column order: 1 x-maj
 ap.add_argument("--x2pf", default="3", help="fused-pair planes of lookahead (list)")
 ap.add_argument("--interior-align", default="128", help="LocalDomain interior alignment in bytes (list: 64,128)")
 ap.add_argument("--fp64", action="store_true")
+ap.add_argument("--row-pad-lines", default="0", help="extra 128-B lines per row pitch (list)")
 args = ap.parse_args()
-for sched, row, xf, pf, al in ((int(a), int(b), int(c), int(d), int(e)) for a in args.x2sched.split(",")
-                               for b in args.x2row.split(",") for c in args.x2xfast.split(",")
-                               for d in args.x2pf.split(",") for e in args.interior_align.split(",")):
+for sched, row, xf, pf, al, rp in ((int(a), int(b), int(c), int(d), int(e), int(f)) for a in args.x2sched.split(",")
+                                   for b in args.x2row.split(",") for c in args.x2xfast.split(",")
+                                   for d in args.x2pf.split(",") for e in args.interior_align.split(",")
+                                   for f in args.row_pad_lines.split(",")):
     for sh in args.shapes.split(","):
         L = tuple(int(v) for v in sh.split("x"))
         t = st.StencilTune()
@@ -29,7 +31,7 @@ for sched, row, xf, pf, al in ((int(a), int(b), int(c), int(d), int(e)) for a in
         t.x2row = row
         t.x2xfast = xf
         t.x2pf = pf
-        m = st.Jacobi3D(L, gpus=[0], temporal=2, tune=t, interior_align=al, fp64=args.fp64)
+        m = st.Jacobi3D(L, gpus=[0], temporal=2, tune=t, interior_align=al, fp64=args.fp64, row_pad_lines=rp)
         m.init()
         m.run(8)
         m.synchronize()
@@ -38,7 +40,7 @@ for sched, row, xf, pf, al in ((int(a), int(b), int(c), int(d), int(e)) for a in
         m.synchronize()
         dt = time.perf_counter() - t0
         cells = L[0] * L[1] * L[2]
-        print(json.dumps({"shape": sh, "x2sched": sched, "x2row": row, "x2xfast": xf, "x2pf": pf, "interior_align": al, "fp64": args.fp64, "us_per_step": round(dt / args.steps * 1e6, 1),
+        print(json.dumps({"shape": sh, "x2sched": sched, "x2row": row, "x2xfast": xf, "x2pf": pf, "interior_align": al, "row_pad_lines": rp, "fp64": args.fp64, "us_per_step": round(dt / args.steps * 1e6, 1),
                           "gcells": round(cells * args.steps / dt / 1e9, 1)}), flush=True)
         del m
         torch.cuda.empty_cache()
