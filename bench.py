@@ -342,10 +342,6 @@ def main():
                          "and of the reference-rule cube (auto: only with N > 1)")
     ap.add_argument("--sweep-budget", type=float, default=30.0,
                     help="seconds after which the transport sweep starts no further entry")
-    ap.add_argument("--settle-ms", type=float, default=0,
-                    help="before the model is built, keep the GPU busy with a plain HBM copy loop (torch, not the "
-                         "stencil) for this long, so the timed steps do not run while clocks and power ramp up; "
-                         "reported as config.gpu_settle_ms")
     ap.add_argument("--launch-timeout", type=float, default=3000,
                     help="--gpus N>1 without a launcher: seconds before the spawned ranks are stopped (0 = none)")
     args = ap.parse_args()
@@ -372,18 +368,6 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
     red_dev = "cpu" if shared else "cuda"
-
-    if args.settle_ms > 0:  # GPU settle: a torch copy loop, nothing of the model (its W warm-up steps stay W)
-        a = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
-        b = torch.empty_like(a)
-        torch.cuda.synchronize()
-        t_settle = time.perf_counter()
-        while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-            for _ in range(8):
-                b.copy_(a)
-            torch.cuda.synchronize()
-        del a, b
-        torch.cuda.empty_cache()
 
     import stencil2_amd as st
 
@@ -572,7 +556,7 @@ def main():
     model_cfg = {
         "decomposition": f"{pdim.x}x{pdim.y}x{pdim.z}", "methods": st.methods_to_string(methods), "preflight": preflight,
         "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
-        "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align, "gpu_settle_ms": args.settle_ms,
+        "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
         "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
         "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched,
         "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
