@@ -304,6 +304,8 @@ def main():
     ap.add_argument("--x-halo-align", type=int, default=0,
                     help="x halos inside the interior's first / last 64-B sector (LocalDomain::set_x_halo_align): "
                          "one sector per row end for x-face copies; every row spans one more sector")
+    ap.add_argument("--x-face-lines", type=int, default=0,
+                    help="same-GPU x-face copies as whole 128-B lines (TransportOptions.x_face_sectors)")
     ap.add_argument("--interior-align", type=int, default=128, choices=[64, 128],
                     help="byte alignment of every row's first interior cell: 128 = whole L2 lines per 512-cell row "
                          "(1150-1194 -> 1285-1287 Gcells/s on one MI355X, profiles/r4/i/), 64 = one sector (r1-r3)")
@@ -401,6 +403,7 @@ def main():
     topt.completion = {"kernel": topt.Completion.Kernel, "streamop": topt.Completion.StreamOp,
                        "ipcevent": topt.Completion.IpcEvent}[args.completion]
     topt.fuse_flags = bool(args.fuse_flags)
+    topt.x_face_sectors = bool(args.x_face_lines)
     if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # rehearses the fallback (scripts): IPC probe reports failure
         topt.fail_ipc_probe = True
 
@@ -557,6 +560,7 @@ def main():
         "decomposition": f"{pdim.x}x{pdim.y}x{pdim.z}", "methods": st.methods_to_string(methods), "preflight": preflight,
         "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
         "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
+        "x_face_lines": bool(args.x_face_lines),
         "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
         "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched,
         "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,

@@ -142,9 +142,10 @@ struct TransportOptions {
   // device backend: when every GPU of this process sits on one NUMA node, realize() binds the calling thread to that
   // node's CPUs and allocates the host-staged (pinned) buffers there
   bool numaAffinity = true;
-  // same-GPU x faces (translates) copied as whole 64-B sectors (4 lanes per row, the extra cells land in the
-  // receiver's row padding) instead of w-cell pieces of one sector per lane (build_translate_segs_q). Measured no
-  // gain (same probe: stream-ordered 26.2 vs 24.9 us for faces 2, 26.8 vs 27.8 us with depth-1 edges): off
+  // same-GPU x faces (translates) copied as whole interior-alignment units -- 128-B L2 lines with the default
+  // layout, 64-B sectors with interior_align 64 -- (8 / 4 lanes per row, the extra cells land in the receiver's row
+  // padding) instead of w-cell pieces of one line per lane (build_translate_segs_q). With 64-B sectors it measured
+  // no gain (stream-ordered 26.2 vs 24.9 us for faces 2, 26.8 vs 27.8 us with depth-1 edges)
   bool xFaceSectors = false;
 };
 const char *to_string(TransportOptions::Inbox v);

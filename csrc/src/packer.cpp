@@ -62,17 +62,19 @@ void build_unpack_segs(const LocalDomain &dom, const std::vector<Message> &msgs,
     }
 }
 
-// An x face (dir = (+-1, 0, 0)) is a strided column of w-cell row pieces: each row touches one 64-B sector of the
-// source and one of the receiver, the latter only partly written. Widened to whole sectors (S = 64 B / element)
-// the copy reads the same sectors and writes whole ones (the extra S - w cells land in the receiver's x padding in
-// front of its -x halo or behind its +x halo, which nothing reads). Needs both rows 64-B aligned at the interior (the
-// padded layout), interiors a multiple of S long and at least S long, and room for the sector in the receiver's row.
+// An x face (dir = (+-1, 0, 0)) is a strided column of w-cell row pieces: each row touches one line of the source
+// and one of the receiver, the latter only partly written. Widened to whole interior-alignment units (S = 128 B / element
+// with the default 128-B interior alignment: whole L2 lines; 64 B: sectors) the copy reads the same lines and writes
+// whole ones (the extra S - w cells land in the receiver's x padding in front of its -x halo or behind its +x halo,
+// which nothing reads). Needs both rows aligned at the interior (the padded layout), interiors a multiple of S long
+// and at least S long, and room for the unit in the receiver's row.
 static bool widen_x_face(const LocalDomain &src, const LocalDomain &dst, const Dim3 &dir, int64_t q, Dim3 *sp, Dim3 *dp,
                          Dim3 *ext) {
   if (dir.y != 0 || dir.z != 0 || dir.x == 0) return false;
   const int64_t es = src.elem_size(q);
-  if (es != dst.elem_size(q) || 64 % es != 0) return false;
-  const int64_t S = 64 / es, w = ext->x;
+  const int64_t unit = std::min(src.interior_align(), dst.interior_align());
+  if (es != dst.elem_size(q) || unit % es != 0 || src.x_halo_align() || dst.x_halo_align()) return false;
+  const int64_t S = unit / es, w = ext->x;
   if (w > S || src.size().x % S || dst.size().x % S || src.size().x < S) return false;
   const int64_t srxm = src.radius().x(-1), drxm = dst.radius().x(-1);
   if ((src.pad_x(q) + srxm) % S || (dst.pad_x(q) + drxm) % S) return false; // interiors not sector aligned

@@ -205,8 +205,9 @@ def test_select_method_priority_and_shared_gpu(st):
                                        ((30, 10, 9), [0])])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_exchange_x_face_sectors(st, name, size, gpus, dtype):
-    """TransportOptions.x_face_sectors: same-process x faces copied as whole 64-B sectors (the extra cells go to the
-    receiver's row padding) give exactly the same halos; x extents that are no multiple of a sector fall back."""
+    """TransportOptions.x_face_sectors: same-process x faces copied as whole 128-B lines (the interior-alignment unit;
+    the extra cells go to the receiver's row padding) give exactly the same halos; x extents that are no multiple of
+    a line fall back."""
     radius = radius_patterns(st)[name]
     tr = st.TransportOptions()
     tr.x_face_sectors = True

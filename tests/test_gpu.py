@@ -991,3 +991,19 @@ def test_interior_align_128_models(st, kind, size, gpus, temporal):
         u = ref(u)
     m.synchronize()
     assert torch.equal(_gather(m), u)
+
+
+@pytest.mark.parametrize("rname", ["r1", "r3", "fec", "asym"])
+@pytest.mark.parametrize("gpus,size", [([0], (64, 13, 11)), ([0, 0], (128, 13, 11)), ([0, 0, 0], (32, 13, 11))])
+def test_x_face_lines_device(st, rname, gpus, size):
+    """TransportOptions.x_face_sectors on the device: same-GPU x faces as whole 128-B lines, exact halos"""
+    radius = _radii(st)[rname]
+    tr = st.TransportOptions()
+    tr.x_face_sectors = True
+    for dtype in (torch.float32, torch.float64):
+        dd, q = _dd(st, size, radius, gpus, st.MethodFlags.Kernel, dtype=dtype, transport=tr)
+        for it in range(2):
+            fill_coords(dd, q, offset=it)
+            dd.exchange()
+            assert check_exchange(dd, q, radius, offset=it) == 0
+            dd.swap()
