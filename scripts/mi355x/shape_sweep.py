@@ -20,12 +20,14 @@ ap.add_argument("--interior-align", default="128", help="LocalDomain interior al
 ap.add_argument("--fp64", action="store_true")
 ap.add_argument("--row-pad-lines", default="0", help="extra 128-B lines per row pitch (list)")
 ap.add_argument("--x2nw", default="12", help="waves per fused-pair block (list: 8,12,16)")
+ap.add_argument("--altz", default="0", help="alternate the z-march direction every pair (list: 0,1)")
 args = ap.parse_args()
-for sched, row, xf, pf, al, rp, nw in ((int(a), int(b), int(c), int(d), int(e), int(f), int(g))
-                                       for a in args.x2sched.split(",") for b in args.x2row.split(",")
-                                       for c in args.x2xfast.split(",") for d in args.x2pf.split(",")
-                                       for e in args.interior_align.split(",") for f in args.row_pad_lines.split(",")
-                                       for g in args.x2nw.split(",")):
+for sched, row, xf, pf, al, rp, nw, az in ((int(a), int(b), int(c), int(d), int(e), int(f), int(g), int(h))
+                                           for a in args.x2sched.split(",") for b in args.x2row.split(",")
+                                           for c in args.x2xfast.split(",") for d in args.x2pf.split(",")
+                                           for e in args.interior_align.split(",")
+                                           for f in args.row_pad_lines.split(",") for g in args.x2nw.split(",")
+                                           for h in args.altz.split(",")):
     for sh in args.shapes.split(","):
         L = tuple(int(v) for v in sh.split("x"))
         t = st.StencilTune()
@@ -34,6 +36,7 @@ for sched, row, xf, pf, al, rp, nw in ((int(a), int(b), int(c), int(d), int(e), 
         t.x2xfast = xf
         t.x2pf = pf
         t.x2nw = nw
+        t.alternate_z = bool(az)
         m = st.Jacobi3D(L, gpus=[0], temporal=2, tune=t, interior_align=al, fp64=args.fp64, row_pad_lines=rp)
         m.init()
         m.run(8)
@@ -43,7 +46,7 @@ for sched, row, xf, pf, al, rp, nw in ((int(a), int(b), int(c), int(d), int(e), 
         m.synchronize()
         dt = time.perf_counter() - t0
         cells = L[0] * L[1] * L[2]
-        print(json.dumps({"shape": sh, "x2sched": sched, "x2row": row, "x2xfast": xf, "x2pf": pf, "interior_align": al, "row_pad_lines": rp, "x2nw": nw, "fp64": args.fp64, "us_per_step": round(dt / args.steps * 1e6, 1),
+        print(json.dumps({"shape": sh, "x2sched": sched, "x2row": row, "x2xfast": xf, "x2pf": pf, "interior_align": al, "row_pad_lines": rp, "x2nw": nw, "altz": az, "fp64": args.fp64, "us_per_step": round(dt / args.steps * 1e6, 1),
                           "gcells": round(cells * args.steps / dt / 1e9, 1)}), flush=True)
         del m
         torch.cuda.empty_cache()
