@@ -279,8 +279,9 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--methods", default="all")
     ap.add_argument("--nt", type=int, default=1, help="non-temporal stencil stores")
-    ap.add_argument("--altz", type=int, default=0,
-                    help="alternate the z-march direction every step (fused pairs: 1164 with vs 1202 Gcells/s without)")
+    ap.add_argument("--altz", type=int, default=1,
+                    help="alternate the z-march direction every pair (128-B-aligned rows: 1276-1290 with vs 1256-1272 "
+                         "Gcells/s without, profiles/r4/q)")
     ap.add_argument("--ty", type=int, default=2, help="rows per lane of the stencil kernel (2/4/8)")
     ap.add_argument("--variant", type=int, default=2,
                     help="single-step kernel variant (2: VALU LDS z-march, 8: MFMA x-line update; needs --temporal 1)")

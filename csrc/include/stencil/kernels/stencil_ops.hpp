@@ -77,7 +77,11 @@ struct StencilTune {
   bool nontemporal = true;
   // reverse the z-march of every block on odd buffer parities: each step then starts on the planes the previous
   // step wrote last, which are still in the MALL / L2
-  bool alternateZ = false; // r2s3: with lockstep quarters the per-step flip costs the fused pairs 3 % (1164 vs 1202)
+  // flip the z-march direction every pair (each sweep starts on the planes the previous one wrote last). r2s3, rows
+  // 64-B aligned: -3 % (1164 vs 1202); r4, rows on whole 128-B lines: +2-6 % at 512^3 (interleaved bench.py
+  // 1276-1290 vs 1256-1272, shape sweep 1321 / 1392 vs 1247 / 1311), +3-4 % at 645x645x323 and 1024x512x256, neutral
+  // at 813-cell rows and fp64 (profiles/r4/q, profiles/r4/r): on
+  bool alternateZ = true;
   // bitmask of axes (1 = x, 2 = y, 4 = z) along which the sub-domain is its own periodic
   // neighbour and the kernels read the periodic image in place of the halo (StencilModel sets it together with
   // DistributedDomain::exchange_async(.., skipWrapped), which then skips those same-GPU self copies). Needs the

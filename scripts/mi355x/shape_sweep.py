@@ -20,7 +20,7 @@ ap.add_argument("--interior-align", default="128", help="LocalDomain interior al
 ap.add_argument("--fp64", action="store_true")
 ap.add_argument("--row-pad-lines", default="0", help="extra 128-B lines per row pitch (list)")
 ap.add_argument("--x2nw", default="12", help="waves per fused-pair block (list: 8,12,16)")
-ap.add_argument("--altz", default="0", help="alternate the z-march direction every pair (list: 0,1)")
+ap.add_argument("--altz", default="1", help="alternate the z-march direction every pair (list: 0,1)")
 args = ap.parse_args()
 for sched, row, xf, pf, al, rp, nw, az in ((int(a), int(b), int(c), int(d), int(e), int(f), int(g), int(h))
                                            for a in args.x2sched.split(",") for b in args.x2row.split(",")

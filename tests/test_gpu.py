@@ -509,7 +509,7 @@ def test_temporal2_row_kernel_lockstep_quarters(st, fake, reserve, lockstep, alt
     t = st.StencilTune()
     t.x2lockstep = lockstep == "1"
     t.x2reserve = reserve
-    t.alternate_z = alt  # per-step z-direction flip (off by default)
+    t.alternate_z = alt  # per-pair z-direction flip (on by default since r4)
     tr = st.TransportOptions()
     tr.fake_remote_axes = int(fake or 0)
     m = st.AstarothSim((512, 512, 72), quantities=1, gpus=[0], temporal=2, tune=t, axis_cost=(64, 3, 2),
