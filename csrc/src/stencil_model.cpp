@@ -371,6 +371,10 @@ void StencilModel::enqueue_step(int k) {
     if (pub) {
       ti.publish = pubCounter_;
       ti.publishDepth = 2;
+      // fixed march directions: the lockstep schedule's outer z parts march away from the domain's z faces, so the
+      // boundary planes the next exchange waits for come out at the start of every sweep; the per-pair flip
+      // (alternateZ) would write them last on every other pair and leave that exchange nothing to overlap
+      ti.alternateZ = false;
     }
     for (int64_t q = 0; q < doms[0].num_data(); ++q)
       stencil7x2_apply(doms[0], q, c, cfg_.kind, sph_, compute_[0].get(), ti);
