@@ -232,13 +232,21 @@ static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
   return out;
 }
 
+static uint32_t gNarrowBlockItems = 256 * kItemsMax, gWideBlockItems = 256 * kItemsMax;
+
+void set_copy_block_items(uint32_t narrow, uint32_t wide) {
+  STENCIL_REQUIRE(narrow >= 1 && narrow <= 256 * kItemsMax && wide >= 1 && wide <= 256 * kItemsMax,
+                  "items per block must be 1.." << 256 * kItemsMax);
+  gNarrowBlockItems = narrow;
+  gWideBlockItems = wide;
+}
+
 CopyPlan make_copy_plan(const std::vector<CopySeg> &segsIn, int device) {
   CopyPlan p;
   p.device = device;
   std::vector<CopySeg> segs = pair_narrow_segs(segsIn);
   finalize_segs(segs);
   std::vector<CopyWork> work;
-  const uint32_t perBlockUnits = 256 * 4; // items per block
   for (uint32_t si = 0; si < segs.size(); ++si) {
     const CopySeg &s = segs[si];
     if (!s.units) continue;
@@ -246,6 +254,7 @@ CopyPlan make_copy_plan(const std::vector<CopySeg> &segsIn, int device) {
     const bool rows = s.row_units <= kNarrowMaxUnits && !(s.flags & kSegWide);
     const uint64_t items = rows ? s.units / s.row_units : s.units;
     STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
+    const uint32_t perBlockUnits = rows ? gNarrowBlockItems : gWideBlockItems; // items per block
     for (uint64_t f = 0; f < items; f += perBlockUnits)
       work.push_back({si, uint32_t(f), uint32_t(std::min<uint64_t>(perBlockUnits, items - f)), rows ? 1u : 0u});
   }
