@@ -232,7 +232,11 @@ static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
   return out;
 }
 
-static uint32_t gNarrowBlockItems = 256 * kItemsMax, gWideBlockItems = 256 * kItemsMax;
+// 512 16-B units per block for wide rows (two per thread) and 1024 rows per block for narrow ones: the 512^3
+// radius-2-face self-exchange (bench_exchange config 3) on one MI355X, interleaved over 6 rounds
+// (scripts/mi355x/copy_items_probe.py, profiles/r4/x/): wide 1024 -> 512 blocking 280.7-293.1 -> 332.5-345.3 GB/s,
+// stream-ordered 438-440 -> 526-537; wide 384 / 640 in between, 128 worse; narrow below 1024 worse (768: 272)
+static uint32_t gNarrowBlockItems = 256 * kItemsMax, gWideBlockItems = 512;
 
 void set_copy_block_items(uint32_t narrow, uint32_t wide) {
   STENCIL_REQUIRE(narrow >= 1 && narrow <= 256 * kItemsMax && wide >= 1 && wide <= 256 * kItemsMax,

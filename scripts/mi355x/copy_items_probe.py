@@ -26,7 +26,7 @@ for n, w in combos:
     d.add_data("q", torch.float32)
     d.realize()
     doms[(n, w)] = d
-st._C.set_copy_block_items(1024, 1024)
+st._C.set_copy_block_items(1024, 512)  # the library default
 xs = torch.cuda.Stream()
 best = {}
 for rnd in range(a.rounds):
