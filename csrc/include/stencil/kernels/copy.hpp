@@ -84,6 +84,8 @@ CopyPlan make_copy_plan(const std::vector<CopySeg> &segs, int device);
 // items per work-table entry (= per 256-thread block of copy_plan_kernel) for narrow-row segments (x faces: one row
 // per item) and for wide segments (one 16-B unit per item); plans built afterwards use them. Defaults 1024 / 512.
 void set_copy_block_items(uint32_t narrow, uint32_t wide);
+// interleave the row (narrow) and unit (wide) work entries in dispatch order instead of segment order (experiment)
+void set_copy_interleave(bool on);
 void free_copy_plan(CopyPlan &p);
 // maxBlocks > 0: at most that many 1024-thread blocks (one CU each) walk the work table (see copy.hip)
 void copy_plan_device(const CopyPlan &p, hipStream_t stream, int maxBlocks = 0);

@@ -238,6 +238,9 @@ static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
 // stream-ordered 438-440 -> 526-537; wide 384 / 640 in between, 128 worse; narrow below 1024 worse (768: 272)
 static uint32_t gNarrowBlockItems = 256 * kItemsMax, gWideBlockItems = 512;
 
+static bool gInterleaveWork = false;
+void set_copy_interleave(bool on) { gInterleaveWork = on; }
+
 void set_copy_block_items(uint32_t narrow, uint32_t wide) {
   STENCIL_REQUIRE(narrow >= 1 && narrow <= 256 * kItemsMax && wide >= 1 && wide <= 256 * kItemsMax,
                   "items per block must be 1.." << 256 * kItemsMax);
@@ -261,6 +264,21 @@ CopyPlan make_copy_plan(const std::vector<CopySeg> &segsIn, int device) {
     const uint32_t perBlockUnits = rows ? gNarrowBlockItems : gWideBlockItems; // items per block
     for (uint64_t f = 0; f < items; f += perBlockUnits)
       work.push_back({si, uint32_t(f), uint32_t(std::min<uint64_t>(perBlockUnits, items - f)), rows ? 1u : 0u});
+  }
+  if (gInterleaveWork) { // spread the row (x-face) entries evenly among the unit entries in dispatch order
+    std::vector<CopyWork> rowsW, unitsW;
+    for (const CopyWork &w : work) (w.rows ? rowsW : unitsW).push_back(w);
+    std::vector<CopyWork> merged;
+    merged.reserve(work.size());
+    size_t i = 0, j = 0;
+    while (i < rowsW.size() || j < unitsW.size()) {
+      // take a row entry while rows are behind their share of the entries placed so far
+      if (i < rowsW.size() && (j >= unitsW.size() || i * unitsW.size() <= j * rowsW.size()))
+        merged.push_back(rowsW[i++]);
+      else
+        merged.push_back(unitsW[j++]);
+    }
+    work.swap(merged);
   }
   p.nsegs = int(segs.size());
   p.nwork = int(work.size());
