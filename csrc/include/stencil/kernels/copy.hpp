@@ -73,9 +73,11 @@ struct CopyWork {
 };
 struct CopyPlan {
   CopySeg *dsegs = nullptr;
-  CopyWork *dwork = nullptr;
+  CopyWork *dwork = nullptr;  // entries for one block each (copy_plan_kernel)
+  CopyWork *dworkG = nullptr; // entries of 1024 items for the grid-stride kernels (few-CU and fused transport)
   int nsegs = 0;
   int nwork = 0;
+  int nworkG = 0;
   int device = -1;
   uint64_t bytes = 0;
 };
@@ -83,9 +85,8 @@ struct CopyPlan {
 CopyPlan make_copy_plan(const std::vector<CopySeg> &segs, int device);
 // items per work-table entry (= per 256-thread block of copy_plan_kernel) for narrow-row segments (x faces: one row
 // per item) and for wide segments (one 16-B unit per item); plans built afterwards use them. Defaults 1024 / 512.
+// The grid-stride kernels (copy_plan_device with maxBlocks, copy_plan_device_sync) always use 1024-item entries.
 void set_copy_block_items(uint32_t narrow, uint32_t wide);
-// interleave the row (narrow) and unit (wide) work entries in dispatch order instead of segment order (experiment)
-void set_copy_interleave(bool on);
 void free_copy_plan(CopyPlan &p);
 // maxBlocks > 0: at most that many 1024-thread blocks (one CU each) walk the work table (see copy.hip)
 void copy_plan_device(const CopyPlan &p, hipStream_t stream, int maxBlocks = 0);

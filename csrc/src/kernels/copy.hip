@@ -238,9 +238,6 @@ static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
 // stream-ordered 438-440 -> 526-537; wide 384 / 640 in between, 128 worse; narrow below 1024 worse (768: 272)
 static uint32_t gNarrowBlockItems = 256 * kItemsMax, gWideBlockItems = 512;
 
-static bool gInterleaveWork = false;
-void set_copy_interleave(bool on) { gInterleaveWork = on; }
-
 void set_copy_block_items(uint32_t narrow, uint32_t wide) {
   STENCIL_REQUIRE(narrow >= 1 && narrow <= 256 * kItemsMax && wide >= 1 && wide <= 256 * kItemsMax,
                   "items per block must be 1.." << 256 * kItemsMax);
@@ -248,62 +245,62 @@ void set_copy_block_items(uint32_t narrow, uint32_t wide) {
   gWideBlockItems = wide;
 }
 
+// work table of `segs` with at most `narrow` rows / `wide` units per entry
+static std::vector<CopyWork> work_table(const std::vector<CopySeg> &segs, uint32_t narrow, uint32_t wide) {
+  std::vector<CopyWork> work;
+  for (uint32_t si = 0; si < segs.size(); ++si) {
+    const CopySeg &s = segs[si];
+    if (!s.units) continue;
+    const bool rows = s.row_units <= kNarrowMaxUnits && !(s.flags & kSegWide);
+    const uint64_t items = rows ? s.units / s.row_units : s.units;
+    STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
+    const uint32_t per = rows ? narrow : wide;
+    for (uint64_t f = 0; f < items; f += per)
+      work.push_back({si, uint32_t(f), uint32_t(std::min<uint64_t>(per, items - f)), rows ? 1u : 0u});
+  }
+  return work;
+}
+
 CopyPlan make_copy_plan(const std::vector<CopySeg> &segsIn, int device) {
   CopyPlan p;
   p.device = device;
   std::vector<CopySeg> segs = pair_narrow_segs(segsIn);
   finalize_segs(segs);
-  std::vector<CopyWork> work;
-  for (uint32_t si = 0; si < segs.size(); ++si) {
-    const CopySeg &s = segs[si];
-    if (!s.units) continue;
-    p.bytes += s.units * s.vec * (s.src2 ? 2 : 1);
-    const bool rows = s.row_units <= kNarrowMaxUnits && !(s.flags & kSegWide);
-    const uint64_t items = rows ? s.units / s.row_units : s.units;
-    STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
-    const uint32_t perBlockUnits = rows ? gNarrowBlockItems : gWideBlockItems; // items per block
-    for (uint64_t f = 0; f < items; f += perBlockUnits)
-      work.push_back({si, uint32_t(f), uint32_t(std::min<uint64_t>(perBlockUnits, items - f)), rows ? 1u : 0u});
-  }
-  if (gInterleaveWork) { // spread the row (x-face) entries evenly among the unit entries in dispatch order
-    std::vector<CopyWork> rowsW, unitsW;
-    for (const CopyWork &w : work) (w.rows ? rowsW : unitsW).push_back(w);
-    std::vector<CopyWork> merged;
-    merged.reserve(work.size());
-    size_t i = 0, j = 0;
-    while (i < rowsW.size() || j < unitsW.size()) {
-      // take a row entry while rows are behind their share of the entries placed so far
-      if (i < rowsW.size() && (j >= unitsW.size() || i * unitsW.size() <= j * rowsW.size()))
-        merged.push_back(rowsW[i++]);
-      else
-        merged.push_back(unitsW[j++]);
-    }
-    work.swap(merged);
-  }
+  for (const CopySeg &s : segs) p.bytes += s.units * s.vec * (s.src2 ? 2 : 1);
+  // one block per entry (copy_plan_kernel): the tuned sizes; grid-stride kernels (few-CU and fused transport
+  // kernels) walk entries of 1024 items, four in flight per thread, which their fixed number of groups needs
+  const std::vector<CopyWork> work = work_table(segs, gNarrowBlockItems, gWideBlockItems);
+  const std::vector<CopyWork> workG = work_table(segs, 256 * kItemsMax, 256 * kItemsMax);
   p.nsegs = int(segs.size());
   p.nwork = int(work.size());
+  p.nworkG = int(workG.size());
   if (p.nwork == 0) return p;
   HIP_CHECK(hipMalloc(&p.dsegs, sizeof(CopySeg) * segs.size()));
   HIP_CHECK(hipMemcpy(p.dsegs, segs.data(), sizeof(CopySeg) * segs.size(), hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&p.dwork, sizeof(CopyWork) * work.size()));
   HIP_CHECK(hipMemcpy(p.dwork, work.data(), sizeof(CopyWork) * work.size(), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMalloc(&p.dworkG, sizeof(CopyWork) * workG.size()));
+  HIP_CHECK(hipMemcpy(p.dworkG, workG.data(), sizeof(CopyWork) * workG.size(), hipMemcpyHostToDevice));
   return p;
 }
 
 void free_copy_plan(CopyPlan &p) {
   if (p.dsegs) (void)hipFree(p.dsegs);
   if (p.dwork) (void)hipFree(p.dwork);
+  if (p.dworkG) (void)hipFree(p.dworkG);
   p.dsegs = nullptr;
   p.dwork = nullptr;
+  p.dworkG = nullptr;
   p.nwork = 0;
+  p.nworkG = 0;
 }
 
 void copy_plan_device(const CopyPlan &p, hipStream_t stream, int maxBlocks) {
   if (!p.nwork) return;
   if (maxBlocks > 0) {
-    const int blocks = std::min(maxBlocks, (p.nwork + 3) / 4);
-    hipLaunchKernelGGL(copy_plan_kernel_narrow, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dwork,
-                       uint32_t(p.nwork));
+    const int blocks = std::min(maxBlocks, (p.nworkG + 3) / 4);
+    hipLaunchKernelGGL(copy_plan_kernel_narrow, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dworkG,
+                       uint32_t(p.nworkG));
   } else {
     hipLaunchKernelGGL(copy_plan_kernel, dim3(p.nwork), dim3(256), 0, stream, p.dsegs, p.dwork);
   }
@@ -454,8 +451,8 @@ void copy_plan_device_sync(const CopyPlan &p, hipStream_t stream, int maxBlocks,
   // least one block, so the flags are waited for and raised even when this device has nothing to copy
   const int shareCap = a.sharedGpu ? kFusedMaxBlocks : (1 << 20);
   const int cap = maxBlocks > 0 ? std::min(maxBlocks, shareCap) : shareCap;
-  const int blocks = std::max(1, std::min(cap, (p.nwork + 3) / 4));
-  hipLaunchKernelGGL(copy_plan_kernel_sync, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dwork, uint32_t(p.nwork),
+  const int blocks = std::max(1, std::min(cap, (p.nworkG + 3) / 4));
+  hipLaunchKernelGGL(copy_plan_kernel_sync, dim3(blocks), dim3(1024), 0, stream, p.dsegs, p.dworkG, uint32_t(p.nworkG),
                      fs);
   HIP_CHECK(hipGetLastError());
 }
