@@ -120,6 +120,7 @@ def transport_sweep(st, torch, dist, args, world, device, red_dev, axis_cost, ob
             dd.set_partition_objective(obj)
             dd.set_plan_file("")
             dd.set_x_halo_align(bool(args.x_halo_align))
+            dd.set_interior_align(args.interior_align)
             topt = st.TransportOptions()
             topt.inbox = topt_base.inbox
             topt.completion = completion
