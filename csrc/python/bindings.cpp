@@ -681,6 +681,19 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("dd"), py::arg("domain"), py::arg("qi"), py::arg("region"), py::arg("kind"), py::arg("spheres"),
         py::arg("stream") = 0);
+  m.def("stencil7x2_supported",
+        [](DistributedDomain &dd, size_t di, int64_t q) { return stencil7x2_supported(dd.domains().at(di), q); },
+        py::arg("dd"), py::arg("domain"), py::arg("qi"));
+  m.def("stencil7x2_apply",
+        [](DistributedDomain &dd, size_t di, int64_t q, const Rect3 &region, StencilKind kind, bool spheres,
+           uintptr_t stream, const StencilTune &tune) {
+          STENCIL_REQUIRE(stencil7x2_supported(dd.domains().at(di), q),
+                          "fused pairs need a device fp32/fp64 quantity, face radii >= 2 and the aligned layout");
+          const Spheres s = spheres ? Spheres::jacobi(dd.get_compute_region()) : Spheres();
+          stencil7x2_apply(dd.domains().at(di), q, region, kind, s, reinterpret_cast<hipStream_t>(stream), tune);
+        },
+        py::arg("dd"), py::arg("domain"), py::arg("qi"), py::arg("region"), py::arg("kind"), py::arg("spheres"),
+        py::arg("stream"), py::arg("tune"), py::call_guard<py::gil_scoped_release>());
   m.def(
       "x2_lockstep_schedule",
       [](int64_t slots, int64_t cols, int64_t nz) {

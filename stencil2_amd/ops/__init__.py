@@ -6,4 +6,4 @@ from .reference import (  # noqa: F401
     jacobi_step_reference,
     periodic_gather,
 )
-from .kernels import stencil7_apply  # noqa: F401
+from .kernels import stencil7_apply, stencil7x2_apply, stencil7x2_supported  # noqa: F401

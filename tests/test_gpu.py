@@ -1007,3 +1007,33 @@ def test_x_face_lines_device(st, rname, gpus, size):
             dd.exchange()
             assert check_exchange(dd, q, radius, offset=it) == 0
             dd.swap()
+
+
+@pytest.mark.parametrize("kind,fp64", [("jacobi", False), ("astaroth", False), ("jacobi", True)])
+def test_ops_stencil7x2_apply_on_a_domain(st, kind, fp64):
+    """ops.stencil7x2_apply on a user's DistributedDomain: exchange the depth-2 halos, one fused call = two steps of
+    the torch oracle, bitwise; the same with the periodic image read in-kernel (tune.wrap = 7, no exchange)"""
+    from stencil2_amd.ops import astaroth_step_reference, stencil7x2_apply, stencil7x2_supported
+    K = st.StencilKind.Jacobi if kind == "jacobi" else st.StencilKind.Astaroth
+    ref = jacobi_step_reference if kind == "jacobi" else astaroth_step_reference
+    dtype = torch.float64 if fp64 else torch.float32
+    L = (64, 48, 40)
+    for wrap in (0, 7):
+        dd = st.DistributedDomain(*L, group=st.make_single_group())
+        dd.set_radius(st.Radius.face_edge_corner(2, 1, 0))
+        dd.set_gpus([0])
+        q = dd.add_data("u", dtype)
+        dd.realize()
+        assert stencil7x2_supported(dd, 0, q)
+        u = torch.rand((L[2], L[1], L[0]), generator=torch.Generator().manual_seed(5), dtype=torch.float64).to(dtype)
+        dd.curr_interior(0, q).copy_(u.cuda())
+        torch.cuda.synchronize()
+        if wrap == 0:
+            dd.exchange()
+        t = st.StencilTune()
+        t.wrap = wrap
+        stencil7x2_apply(dd, 0, q, dd.domain(0).get_compute_region(), K, spheres=kind == "jacobi", tune=t)
+        torch.cuda.synchronize()
+        dd.swap()
+        want = ref(ref(u.cuda()))
+        assert torch.equal(dd.curr_interior(0, q), want), f"wrap {wrap}"
