@@ -39,6 +39,7 @@ for sched, row, xf, pf, al, rp, nw, az in ((int(a), int(b), int(c), int(d), int(
         t.alternate_z = bool(az)
         m = st.Jacobi3D(L, gpus=[0], temporal=2, tune=t, interior_align=al, fp64=args.fp64, row_pad_lines=rp)
         m.init()
+        m.prepare()  # graph blocks instantiated outside the timed region (the first instantiation in a process is slow)
         m.run(8)
         m.synchronize()
         t0 = time.perf_counter()
