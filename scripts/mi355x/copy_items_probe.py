@@ -14,6 +14,7 @@ ap.add_argument("--combos", default="1024:1024,256:1024,64:1024,1024:256,256:256
 ap.add_argument("--iters", type=int, default=40)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--edges", type=int, default=0, help="depth of the edge halos too (bench.py's fused pairs: 1)")
+ap.add_argument("--edges", type=int, default=0, help="depth of the edge halos too (bench.py's fused pairs: 1)")
 a = ap.parse_args()
 r = st.Radius.constant(0)
 r.set_face(2)
