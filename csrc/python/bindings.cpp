@@ -294,7 +294,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_default_group", &comm::set_default_group);
   m.def("find_free_port", &comm::find_free_port);
   m.def("set_copy_block_items", &set_copy_block_items, py::arg("narrow"), py::arg("wide"));
-  m.def("set_copy_rows_first", &set_copy_rows_first, py::arg("on"));
   m.def("ipc_event_stress", &ipc_event_stress, py::arg("group"), py::arg("device"), py::arg("n"), py::arg("after"),
         py::call_guard<py::gil_scoped_release>());
   m.def(

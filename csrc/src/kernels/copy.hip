@@ -238,9 +238,6 @@ static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
 // stream-ordered 438-440 -> 526-537; wide 384 / 640 in between, 128 worse; narrow below 1024 worse (768: 272)
 static uint32_t gNarrowBlockItems = 256 * kItemsMax, gWideBlockItems = 512;
 
-static bool gRowsFirst = false;
-void set_copy_rows_first(bool on) { gRowsFirst = on; }
-
 void set_copy_block_items(uint32_t narrow, uint32_t wide) {
   STENCIL_REQUIRE(narrow >= 1 && narrow <= 256 * kItemsMax && wide >= 1 && wide <= 256 * kItemsMax,
                   "items per block must be 1.." << 256 * kItemsMax);
@@ -261,8 +258,6 @@ static std::vector<CopyWork> work_table(const std::vector<CopySeg> &segs, uint32
     for (uint64_t f = 0; f < items; f += per)
       work.push_back({si, uint32_t(f), uint32_t(std::min<uint64_t>(per, items - f)), rows ? 1u : 0u});
   }
-  if (gRowsFirst) // row entries (scattered, latency-bound) dispatched before the streaming unit entries
-    std::stable_partition(work.begin(), work.end(), [](const CopyWork &w) { return w.rows != 0; });
   return work;
 }
 

@@ -14,18 +14,16 @@ ap.add_argument("--combos", default="1024:1024,256:1024,64:1024,1024:256,256:256
 ap.add_argument("--iters", type=int, default=40)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--edges", type=int, default=0, help="depth of the edge halos too (bench.py's fused pairs: 1)")
-ap.add_argument("--edges", type=int, default=0, help="depth of the edge halos too (bench.py's fused pairs: 1)")
 a = ap.parse_args()
 r = st.Radius.constant(0)
 r.set_face(2)
 if a.edges:
     r.set_edge(a.edges)
-combos = [tuple(int(v) for v in c.split(":")) for c in a.combos.split(",")]  # narrow:wide[:rows_first]
+combos = [tuple(int(v) for v in c.split(":")) for c in a.combos.split(",")]  # narrow:wide
 doms = {}
 for c in combos:
     n, w = c[0], c[1]
     st._C.set_copy_block_items(n, w)
-    st._C.set_copy_rows_first(len(c) > 2 and c[2] == 1)
     d = st.DistributedDomain(512, 512, 512, group=st.make_single_group())
     d.set_radius(r)
     d.set_gpus([0])
@@ -33,7 +31,6 @@ for c in combos:
     d.realize()
     doms[c] = d
 st._C.set_copy_block_items(1024, 512)  # the library default
-st._C.set_copy_rows_first(False)
 xs = torch.cuda.Stream()
 best = {}
 for rnd in range(a.rounds):
@@ -60,5 +57,5 @@ for rnd in range(a.rounds):
         b[0], b[1] = min(b[0], blk), min(b[1], asy)
 xb = next(iter(doms.values())).exchange_bytes_for_method(st.MethodFlags.All)
 for c, (blk, asy) in best.items():
-    print(json.dumps({"narrow_items": c[0], "wide_items": c[1], "rows_first": len(c) > 2 and c[2] == 1,  "block_us": round(blk, 1), "block_GBps": round(xb / blk / 1e3, 1),
+    print(json.dumps({"narrow_items": c[0], "wide_items": c[1],  "block_us": round(blk, 1), "block_GBps": round(xb / blk / 1e3, 1),
                       "stream_us": round(asy, 1), "stream_GBps": round(xb / asy / 1e3, 1)}), flush=True)
