@@ -87,6 +87,8 @@ CopyPlan make_copy_plan(const std::vector<CopySeg> &segs, int device);
 // per item) and for wide segments (one 16-B unit per item); plans built afterwards use them. Defaults 1024 / 512.
 // The grid-stride kernels (copy_plan_device with maxBlocks, copy_plan_device_sync) always use 1024-item entries.
 void set_copy_block_items(uint32_t narrow, uint32_t wide);
+// row segments of at most maxItems rows (edges) get entries of perEntry rows (plans built afterwards; 4096 / 64)
+void set_copy_small_rows(uint32_t maxItems, uint32_t perEntry);
 void free_copy_plan(CopyPlan &p);
 // maxBlocks > 0: at most that many 1024-thread blocks (one CU each) walk the work table (see copy.hip)
 void copy_plan_device(const CopyPlan &p, hipStream_t stream, int maxBlocks = 0);

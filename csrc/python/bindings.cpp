@@ -294,6 +294,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_default_group", &comm::set_default_group);
   m.def("find_free_port", &comm::find_free_port);
   m.def("set_copy_block_items", &set_copy_block_items, py::arg("narrow"), py::arg("wide"));
+  m.def("set_copy_small_rows", &set_copy_small_rows, py::arg("max_items"), py::arg("per_entry"));
   m.def("ipc_event_stress", &ipc_event_stress, py::arg("group"), py::arg("device"), py::arg("n"), py::arg("after"),
         py::call_guard<py::gil_scoped_release>());
   m.def(

@@ -238,6 +238,13 @@ static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
 // stream-ordered 438-440 -> 526-537; wide 384 / 640 in between, 128 worse; narrow below 1024 worse (768: 272)
 static uint32_t gNarrowBlockItems = 256 * kItemsMax, gWideBlockItems = 512;
 
+static uint32_t gSmallRowSeg = 4096, gSmallRowItems = 64;
+void set_copy_small_rows(uint32_t maxItems, uint32_t perEntry) {
+  STENCIL_REQUIRE(perEntry >= 1, "items per entry must be positive");
+  gSmallRowSeg = maxItems;
+  gSmallRowItems = perEntry;
+}
+
 void set_copy_block_items(uint32_t narrow, uint32_t wide) {
   STENCIL_REQUIRE(narrow >= 1 && narrow <= 256 * kItemsMax && wide >= 1 && wide <= 256 * kItemsMax,
                   "items per block must be 1.." << 256 * kItemsMax);
@@ -254,7 +261,9 @@ static std::vector<CopyWork> work_table(const std::vector<CopySeg> &segs, uint32
     const bool rows = s.row_units <= kNarrowMaxUnits && !(s.flags & kSegWide);
     const uint64_t items = rows ? s.units / s.row_units : s.units;
     STENCIL_REQUIRE(items < (1ull << 32), "copy segment too large");
-    const uint32_t per = rows ? narrow : wide;
+    // small row segments (edges: a few hundred scattered cells) are split finer, so their latency-bound items run
+    // on many blocks at once instead of trailing behind the faces in one
+    const uint32_t per = rows ? (items <= gSmallRowSeg ? std::min<uint32_t>(narrow, gSmallRowItems) : narrow) : wide;
     for (uint64_t f = 0; f < items; f += per)
       work.push_back({si, uint32_t(f), uint32_t(std::min<uint64_t>(per, items - f)), rows ? 1u : 0u});
   }

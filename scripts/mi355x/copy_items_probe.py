@@ -19,18 +19,20 @@ r = st.Radius.constant(0)
 r.set_face(2)
 if a.edges:
     r.set_edge(a.edges)
-combos = [tuple(int(v) for v in c.split(":")) for c in a.combos.split(",")]  # narrow:wide
+combos = [tuple(int(v) for v in c.split(":")) for c in a.combos.split(",")]  # narrow:wide[:small_row_items]
 doms = {}
 for c in combos:
     n, w = c[0], c[1]
     st._C.set_copy_block_items(n, w)
+    st._C.set_copy_small_rows(4096, c[2] if len(c) > 2 else 64)
     d = st.DistributedDomain(512, 512, 512, group=st.make_single_group())
     d.set_radius(r)
     d.set_gpus([0])
     d.add_data("q", torch.float32)
     d.realize()
     doms[c] = d
-st._C.set_copy_block_items(1024, 512)  # the library default
+st._C.set_copy_block_items(1024, 512)  # the library defaults
+st._C.set_copy_small_rows(4096, 64)
 xs = torch.cuda.Stream()
 best = {}
 for rnd in range(a.rounds):
@@ -57,5 +59,5 @@ for rnd in range(a.rounds):
         b[0], b[1] = min(b[0], blk), min(b[1], asy)
 xb = next(iter(doms.values())).exchange_bytes_for_method(st.MethodFlags.All)
 for c, (blk, asy) in best.items():
-    print(json.dumps({"narrow_items": c[0], "wide_items": c[1],  "block_us": round(blk, 1), "block_GBps": round(xb / blk / 1e3, 1),
+    print(json.dumps({"narrow_items": c[0], "wide_items": c[1], "small_row_items": c[2] if len(c) > 2 else 64,  "block_us": round(blk, 1), "block_GBps": round(xb / blk / 1e3, 1),
                       "stream_us": round(asy, 1), "stream_GBps": round(xb / asy / 1e3, 1)}), flush=True)
