@@ -12,13 +12,15 @@ using namespace stencil;
 
 struct MethodArgs {
   bool staged = false, rccl = false, colo = false, peer = false, kernel = false, trivial = false;
+  int interiorAlign = 128; // bytes; the row-start alignment of every interior (LocalDomain::set_interior_align)
   void add(ArgParser &p) {
     p.flag(&staged, "--staged,--remote", "host-staged transport (reference CudaMpi)")
         .flag(&rccl, "--rccl,--cuda-aware,--cuda-aware-mpi", "RCCL transport (reference CudaAwareMpi)")
         .flag(&colo, "--colo,--colocated", "HIP-IPC colocated transport")
         .flag(&peer, "--peer", "same-process peer (xGMI) transport")
         .flag(&kernel, "--kernel", "same-GPU kernel transport")
-        .flag(&trivial, "--trivial,--naive", "trivial placement");
+        .flag(&trivial, "--trivial,--naive", "trivial placement")
+        .option(&interiorAlign, "--interior-align", "interior row alignment in bytes (64 or 128)");
   }
   MethodFlags flags() const {
     MethodFlags m = MethodFlags::None;

@@ -30,6 +30,7 @@ int main(int argc, char **argv) {
   dd.set_radius(radius);
   dd.set_methods(ma.flags());
   dd.set_placement(ma.placement());
+  dd.set_interior_align(ma.interiorAlign);
   for (int i = 0; i < nq; ++i) {
     if (fp64)
       dd.add_data<double>("d" + std::to_string(i));
