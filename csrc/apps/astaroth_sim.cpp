@@ -41,6 +41,7 @@ int main(int argc, char **argv) {
   cfg.temporal = temporal;
   cfg.methods = ma.flags();
   cfg.placement = ma.placement();
+  cfg.interiorAlign = ma.interiorAlign;
   cfg.overlap = !noOverlap;
   cfg.wrapSelf = !noWrap;
   StencilModel m(cfg, pg);

@@ -23,6 +23,7 @@ int main(int argc, char **argv) {
   dd.set_radius(3);
   dd.set_methods(ma.flags());
   dd.set_placement(ma.placement());
+  dd.set_interior_align(ma.interiorAlign);
   for (int i = 0; i < nq; ++i) dd.add_data<float>("d" + std::to_string(i));
   dd.realize();
   dd.exchange();
