@@ -342,102 +342,6 @@ static void build_translate(const LocalDomain &src, const LocalDomain &dst, cons
   build_translate_segs(src, dst, dir, curr, out, xSectors);
 }
 
-// ------------------------------------------------------------------------------------------------
-// transport self-test (opt-in): coordinate oracle on a probe domain, ladder Colocated -> Rccl -> Staged
-// ------------------------------------------------------------------------------------------------
-namespace {
-constexpr int32_t kProbePoison = -1;
-int32_t probe_key(int64_t gx, int64_t gy, int64_t gz, const Dim3 &L, int32_t offset) {
-  return int32_t((gx + L.x * (gy + L.y * gz)) % 1000000007) + offset;
-}
-} // namespace
-
-int64_t DistributedDomain::probe_transports(MethodFlags m) {
-  // same group, radius, boundary, placement, cut costs, devices, backend and transport options; every axis
-  // shrunk ~16x (at least 6 cells per stencil reach) so the probe is cheap but spans the same rank pairs
-  int64_t rmax = 1;
-  for (int i = 0; i < 27; ++i) rmax = std::max<int64_t>(rmax, radius_.dir(dir_from_index(i)));
-  auto shrink = [&](int64_t n) { return std::min<int64_t>(n, std::max<int64_t>((n + 15) / 16, 6 * rmax + 2)); };
-  // the probe runs on a fork of the group: a rank whose probe fails (an exception anywhere in realize / exchange)
-  // abandons the fork mid-sequence and goes straight to the verdict below; the other ranks' next receive on the
-  // fork then times out after waitTimeout, they fail too and join the verdict, and this group's own collective
-  // sequence never goes out of step
-  const double forkTimeout = std::max(1.0, topt_.waitTimeout);
-  std::shared_ptr<comm::ProcGroup> grp = pg_->size() > 1 ? pg_->fork(forkTimeout) : pg_;
-  int64_t bad = 0;
-  {
-    DistributedDomain p(shrink(size_.x), shrink(size_.y), shrink(size_.z), grp);
-    p.set_radius(radius_);
-    p.set_boundary(boundary_);
-    p.set_methods(m);
-    p.set_placement(strategy_);
-    p.set_axis_cost(axisCost_);
-    p.set_partition_objective(objective_);
-    if (!gpus_.empty()) p.set_gpus(gpus_);
-    if (backendSet_) p.set_backend(backend_);
-    p.set_transport_options(topt_);
-    p.set_plan_file("");
-    p.set_x_halo_align(xHaloAlign_);
-    p.set_interior_align(interiorAlign_);
-    p.add_data(4, "probe", DType::I32);
-    try {
-      p.realize();
-      if (topt_.failProbeRank == rank() && probeFailures_++ == 0) // test hook: this rank's first probe fails alone
-        LOG_FATAL("TransportOptions::failProbeRank: probe failure forced on rank " << rank());
-      const Dim3 L = p.size();
-      for (int it = 0; it < 2; ++it) {
-        const int32_t off = 7 * it;
-        for (auto &d : p.domains_) {
-          const Dim3 raw = d.raw_size(), org = d.accessor_origin();
-          std::vector<int32_t> v(size_t(raw.flatten()), kProbePoison);
-          const Rect3 cr = d.get_compute_region();
-          for (int64_t z = 0; z < raw.z; ++z)
-            for (int64_t y = 0; y < raw.y; ++y)
-              for (int64_t x = 0; x < raw.x; ++x)
-                if (cr.contains(Dim3(org.x + x, org.y + y, org.z + z)))
-                  v[size_t(x + raw.x * (y + raw.y * z))] = probe_key(org.x + x, org.y + y, org.z + z, L, off);
-          d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), true);
-          d.region_from_host(Dim3(0, 0, 0), raw, 0, v.data(), false);
-        }
-        p.exchange();
-        for (auto &d : p.domains_) {
-          const Dim3 raw = d.raw_size(), org = d.accessor_origin();
-          const Rect3 cr = d.get_compute_region();
-          const auto bytes = d.region_to_host(Dim3(0, 0, 0), raw, 0, true);
-          const int32_t *got = reinterpret_cast<const int32_t *>(bytes.data());
-          for (int64_t z = 0; z < raw.z; ++z)
-            for (int64_t y = 0; y < raw.y; ++y)
-              for (int64_t x = 0; x < raw.x; ++x) {
-                const int64_t g[3] = {org.x + x, org.y + y, org.z + z};
-                const int64_t lo[3] = {cr.lo.x, cr.lo.y, cr.lo.z}, hi[3] = {cr.hi.x, cr.hi.y, cr.hi.z};
-                const int64_t n[3] = {L.x, L.y, L.z};
-                int dd[3];
-                bool crossesClosed = false;
-                for (int a = 0; a < 3; ++a) {
-                  dd[a] = g[a] >= hi[a] ? 1 : (g[a] < lo[a] ? -1 : 0);
-                  if ((g[a] < 0 || g[a] >= n[a]) &&
-                      !boundary_.face_periodic(a == 0 ? dd[a] : 0, a == 1 ? dd[a] : 0, a == 2 ? dd[a] : 0))
-                    crossesClosed = true;
-                }
-                const bool filled = (dd[0] == 0 && dd[1] == 0 && dd[2] == 0) ||
-                                    (radius_.dir(Dim3(dd[0], dd[1], dd[2])) != 0 && !crossesClosed);
-                const int32_t want =
-                    filled ? probe_key(((g[0] % n[0]) + n[0]) % n[0], ((g[1] % n[1]) + n[1]) % n[1],
-                                       ((g[2] % n[2]) + n[2]) % n[2], L, off)
-                           : kProbePoison;
-                bad += got[size_t(x + raw.x * (y + raw.y * z))] != want;
-              }
-        }
-        p.swap();
-      }
-    } catch (const std::exception &e) {
-      LOG_WARN("rank " << rank() << ": transport probe with " << to_string(m) << " failed: " << e.what());
-      bad += int64_t(1) << 40;
-      p.poison("transport probe failed"); // its destructor must not wait on work stuck behind an absent peer
-    }
-  } // the probe domain (and its bounded destructor barrier on the fork) is gone before the verdict
-  return int64_t(pg_->allreduce_sum_u64(uint64_t(bad)));
-}
 
 // ------------------------------------------------------------------------------------------------
 // RCCL communicator (or the host-staged fallback)
@@ -2089,152 +1993,6 @@ void DistributedDomain::swap() {
   TraceRange tr("swap");
   for (auto &d : domains_) d.swap();
   if (exchangeStats_) timeSwap_ += pg_->allreduce_max(now_s() - t0);
-}
-
-// ------------------------------------------------------------------------------------------------
-// ParaView CSV (reference src/stencil.cu:866-939), quantity names preserved
-// ------------------------------------------------------------------------------------------------
-void DistributedDomain::write_paraview(const std::string &prefix, bool zeroNaNs) {
-  TraceRange tr("write_paraview");
-  if (backend_ == Backend::Device) sync_exchange();
-  for (size_t di = 0; di < domains_.size(); ++di) {
-    const LocalDomain &d = domains_[di];
-    const int64_t id = int64_t(rank()) * int64_t(domains_.size()) + int64_t(di);
-    const std::string path = prefix + "_" + std::to_string(id) + ".txt";
-    std::vector<std::vector<unsigned char>> qs;
-    for (int64_t q = 0; q < d.num_data(); ++q) qs.push_back(d.interior_to_host(q));
-    FILE *f = std::fopen(path.c_str(), "w");
-    STENCIL_REQUIRE(f, "cannot open " << path);
-    std::fprintf(f, "Z,Y,X");
-    for (int64_t q = 0; q < d.num_data(); ++q) {
-      std::string n = d.name(q);
-      if (n.empty()) n = "data" + std::to_string(q);
-      std::fprintf(f, ",%s", n.c_str());
-    }
-    std::fprintf(f, "\n");
-    const Dim3 sz = d.size(), o = d.origin();
-    std::string line;
-    char buf[64];
-    for (int64_t z = 0; z < sz.z; ++z)
-      for (int64_t y = 0; y < sz.y; ++y)
-        for (int64_t x = 0; x < sz.x; ++x) {
-          line.clear();
-          std::snprintf(buf, sizeof(buf), "%ld,%ld,%ld", long(o.z + z), long(o.y + y), long(o.x + x));
-          line += buf;
-          const int64_t li = x + sz.x * (y + sz.y * z);
-          for (int64_t q = 0; q < d.num_data(); ++q) {
-            const unsigned char *p = qs[q].data() + li * d.elem_size(q);
-            switch (d.dtype(q)) {
-            case DType::F64: {
-              double v;
-              std::memcpy(&v, p, 8);
-              if (zeroNaNs && std::isnan(v)) v = 0;
-              std::snprintf(buf, sizeof(buf), ",%f", v);
-              break;
-            }
-            case DType::I32: {
-              int32_t v;
-              std::memcpy(&v, p, 4);
-              std::snprintf(buf, sizeof(buf), ",%d", v);
-              break;
-            }
-            case DType::I64: {
-              int64_t v;
-              std::memcpy(&v, p, 8);
-              std::snprintf(buf, sizeof(buf), ",%ld", long(v));
-              break;
-            }
-            default: {
-              if (d.elem_size(q) == 8) {
-                double v;
-                std::memcpy(&v, p, 8);
-                if (zeroNaNs && std::isnan(v)) v = 0;
-                std::snprintf(buf, sizeof(buf), ",%f", v);
-              } else {
-                float v = 0;
-                std::memcpy(&v, p, std::min<int64_t>(4, d.elem_size(q)));
-                if (zeroNaNs && std::isnan(v)) v = 0;
-                std::snprintf(buf, sizeof(buf), ",%f", double(v));
-              }
-            }
-            }
-            line += buf;
-          }
-          line += "\n";
-          std::fputs(line.c_str(), f);
-        }
-    std::fclose(f);
-  }
-}
-
-} // namespace stencil
-
-namespace stencil {
-
-namespace {
-struct CkptHeader {
-  uint64_t magic;
-  int64_t global[3];
-  int64_t idx[3];
-  int64_t origin[3];
-  int64_t size[3];
-  int64_t nq;
-};
-constexpr uint64_t kCkptMagic = 0x53544e434b505432ull; // "STNCKPT2"
-} // namespace
-
-void DistributedDomain::save_checkpoint(const std::string &prefix) const {
-  STENCIL_REQUIRE(realized_, "save_checkpoint before realize");
-  const_cast<DistributedDomain *>(this)->sync_exchange();
-  for (size_t di = 0; di < domains_.size(); ++di) {
-    const LocalDomain &d = domains_[di];
-    const std::string path = prefix + "_" + std::to_string(rank()) + "_" + std::to_string(di) + ".ckpt";
-    FILE *f = std::fopen(path.c_str(), "wb");
-    STENCIL_REQUIRE(f, "cannot open " << path);
-    const Dim3 idx = placement_->get_idx(rank(), int(di));
-    CkptHeader h{kCkptMagic, {size_.x, size_.y, size_.z}, {idx.x, idx.y, idx.z}, {d.origin().x, d.origin().y, d.origin().z},
-                 {d.size().x, d.size().y, d.size().z}, d.num_data()};
-    std::fwrite(&h, sizeof(h), 1, f);
-    for (int64_t q = 0; q < d.num_data(); ++q) {
-      const int64_t es = d.elem_size(q);
-      std::fwrite(&es, sizeof(es), 1, f);
-    }
-    for (int64_t q = 0; q < d.num_data(); ++q) {
-      auto v = d.interior_to_host(q);
-      std::fwrite(v.data(), 1, v.size(), f);
-    }
-    std::fclose(f);
-  }
-  pg_->barrier();
-}
-
-void DistributedDomain::load_checkpoint(const std::string &prefix) {
-  STENCIL_REQUIRE(realized_, "load_checkpoint before realize");
-  sync_exchange();
-  for (size_t di = 0; di < domains_.size(); ++di) {
-    LocalDomain &d = domains_[di];
-    const std::string path = prefix + "_" + std::to_string(rank()) + "_" + std::to_string(di) + ".ckpt";
-    FILE *f = std::fopen(path.c_str(), "rb");
-    STENCIL_REQUIRE(f, "cannot open " << path);
-    CkptHeader h{};
-    STENCIL_REQUIRE(std::fread(&h, sizeof(h), 1, f) == 1 && h.magic == kCkptMagic, "bad checkpoint " << path);
-    const Dim3 idx = placement_->get_idx(rank(), int(di));
-    STENCIL_REQUIRE(h.global[0] == size_.x && h.global[1] == size_.y && h.global[2] == size_.z && h.idx[0] == idx.x &&
-                        h.idx[1] == idx.y && h.idx[2] == idx.z && h.size[0] == d.size().x && h.size[1] == d.size().y &&
-                        h.size[2] == d.size().z && h.nq == d.num_data(),
-                    "checkpoint " << path << " does not match this decomposition");
-    for (int64_t q = 0; q < d.num_data(); ++q) {
-      int64_t es = 0;
-      STENCIL_REQUIRE(std::fread(&es, sizeof(es), 1, f) == 1 && es == d.elem_size(q), "element size mismatch in " << path);
-    }
-    for (int64_t q = 0; q < d.num_data(); ++q) {
-      std::vector<unsigned char> v(size_t(d.size().flatten() * d.elem_size(q)));
-      STENCIL_REQUIRE(std::fread(v.data(), 1, v.size(), f) == v.size(), "truncated checkpoint " << path);
-      d.region_from_host(d.halo_pos(Dim3(0, 0, 0), true), d.size(), q, v.data());
-    }
-    std::fclose(f);
-  }
-  pg_->barrier();
 }
 
 } // namespace stencil
