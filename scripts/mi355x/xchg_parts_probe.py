@@ -11,6 +11,7 @@ import stencil2_amd as st
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1024)
+ap.add_argument("--shape", default="", help="x,y,z instead of the --n cube")
 ap.add_argument("--radius", type=int, default=3)
 ap.add_argument("--fp64", type=int, default=1)
 ap.add_argument("--iters", type=int, default=20)
@@ -18,6 +19,7 @@ ap.add_argument("--parts", default="x,y,z,faces,all")
 ap.add_argument("--narrow", default="1024", help="comma list: x-face rows per block (set_copy_block_items)")
 a = ap.parse_args()
 R = a.radius
+X, Y, Z = (int(v) for v in a.shape.split(",")) if a.shape else (a.n, a.n, a.n)
 
 
 def radius_for(part):
@@ -39,7 +41,7 @@ dt = torch.float64 if a.fp64 else torch.float32
 xs = torch.cuda.Stream()
 for part, narrow in [(p, int(n)) for n in a.narrow.split(",") for p in a.parts.split(",")]:
     st._C.set_copy_block_items(narrow, 512)
-    d = st.DistributedDomain(a.n, a.n, a.n, group=st.make_single_group())
+    d = st.DistributedDomain(X, Y, Z, group=st.make_single_group())
     d.set_radius(radius_for(part))
     d.set_gpus([0])
     d.add_data("q", dt)
@@ -56,7 +58,7 @@ for part, narrow in [(p, int(n)) for n in a.narrow.split(",") for p in a.parts.s
     d.sync_exchange()
     us = (time.perf_counter() - t) / a.iters * 1e6
     b = d.exchange_bytes_for_method(st.MethodFlags.All)
-    print(json.dumps({"part": part, "narrow": narrow, "n": a.n, "radius": R, "fp64": bool(a.fp64), "bytes": b, "us": round(us, 1),
+    print(json.dumps({"part": part, "narrow": narrow, "shape": [X, Y, Z], "radius": R, "fp64": bool(a.fp64), "bytes": b, "us": round(us, 1),
                       "GBps": round(b / us / 1e3, 1)}), flush=True)
     del d
     torch.cuda.empty_cache()
