@@ -13,6 +13,7 @@ using namespace stencil;
 struct MethodArgs {
   bool staged = false, rccl = false, colo = false, peer = false, kernel = false, trivial = false;
   int interiorAlign = 128; // bytes; the row-start alignment of every interior (LocalDomain::set_interior_align)
+  bool xFaceLines = false; // TransportOptions::xFaceSectors: same-GPU x faces copied as whole lines
   void add(ArgParser &p) {
     p.flag(&staged, "--staged,--remote", "host-staged transport (reference CudaMpi)")
         .flag(&rccl, "--rccl,--cuda-aware,--cuda-aware-mpi", "RCCL transport (reference CudaAwareMpi)")
@@ -20,7 +21,8 @@ struct MethodArgs {
         .flag(&peer, "--peer", "same-process peer (xGMI) transport")
         .flag(&kernel, "--kernel", "same-GPU kernel transport")
         .flag(&trivial, "--trivial,--naive", "trivial placement")
-        .option(&interiorAlign, "--interior-align", "interior row alignment in bytes (64 or 128)");
+        .option(&interiorAlign, "--interior-align", "interior row alignment in bytes (64 or 128)")
+        .flag(&xFaceLines, "--x-face-lines", "same-GPU x faces copied as whole 128-B lines");
   }
   MethodFlags flags() const {
     MethodFlags m = MethodFlags::None;

@@ -42,6 +42,7 @@ int main(int argc, char **argv) {
   cfg.methods = ma.flags();
   cfg.placement = ma.placement();
   cfg.interiorAlign = ma.interiorAlign;
+  cfg.transport.xFaceSectors = ma.xFaceLines;
   cfg.overlap = !noOverlap;
   cfg.wrapSelf = !noWrap;
   StencilModel m(cfg, pg);

@@ -45,14 +45,13 @@ static std::pair<Statistics, uint64_t> bench(comm::ProcGroup &pg, int iters, int
 int main(int argc, char **argv) {
   int iters = 30, nq = 1;
   int64_t x = 128, y = 128, z = 128, fr = 2, er = 1, cr = 1;
-  bool weak = false, xHaloAlign = false, xFaceLines = false;
+  bool weak = false, xHaloAlign = false;
   app::MethodArgs ma;
   ArgParser p("halo exchange bandwidth (reference bin/bench_exchange.cu)");
   p.option(&iters, "--iters", "iterations").option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z")
       .option(&nq, "--q", "quantities").option(&fr, "--fr", "face radius").option(&er, "--er", "edge radius")
       .option(&cr, "--cr", "corner radius").flag(&weak, "--weak", "scale x,y,z by ranks^(1/3)")
-      .flag(&xHaloAlign, "--x-halo-align", "x halos inside the interior's first / last 64-B sector")
-      .flag(&xFaceLines, "--x-face-lines", "same-GPU x faces copied as whole 128-B lines");
+      .flag(&xHaloAlign, "--x-halo-align", "x halos inside the interior's first / last 64-B sector");
   ma.add(p);
   if (!p.parse(argc, argv)) return p.need_help() ? 0 : 1;
   auto pg = comm::default_group();
@@ -81,7 +80,7 @@ int main(int argc, char **argv) {
   }
   if (pg->rank() == 0) std::printf("name,count,trimean (S),trimean (B/s),stddev,min,avg,max\n");
   for (auto &pt : pats) {
-    auto res = bench(*pg, iters, nq, ext, pt.r, ma.flags(), ma.placement(), weak, xHaloAlign, xFaceLines, ma.interiorAlign);
+    auto res = bench(*pg, iters, nq, ext, pt.r, ma.flags(), ma.placement(), weak, xHaloAlign, ma.xFaceLines, ma.interiorAlign);
     if (pg->rank() == 0) {
       std::ostringstream n;
       n << x << "-" << y << "-" << z << "/" << pt.name;

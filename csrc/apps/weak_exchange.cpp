@@ -24,6 +24,9 @@ int main(int argc, char **argv) {
   dd.set_methods(ma.flags());
   dd.set_placement(ma.placement());
   dd.set_interior_align(ma.interiorAlign);
+  TransportOptions topt;
+  topt.xFaceSectors = ma.xFaceLines;
+  dd.set_transport_options(topt);
   for (int i = 0; i < nq; ++i) dd.add_data<float>("d" + std::to_string(i));
   dd.realize();
   dd.exchange();

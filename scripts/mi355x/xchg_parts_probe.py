@@ -11,6 +11,7 @@ import stencil2_amd as st
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1024)
+ap.add_argument("--x-face-sectors", type=int, default=0, help="TransportOptions.x_face_sectors")
 ap.add_argument("--shape", default="", help="x,y,z instead of the --n cube")
 ap.add_argument("--radius", type=int, default=3)
 ap.add_argument("--fp64", type=int, default=1)
@@ -43,6 +44,9 @@ for part, narrow in [(p, int(n)) for n in a.narrow.split(",") for p in a.parts.s
     st._C.set_copy_block_items(narrow, 512)
     d = st.DistributedDomain(X, Y, Z, group=st.make_single_group())
     d.set_radius(radius_for(part))
+    topt = st.TransportOptions()
+    topt.x_face_sectors = bool(a.x_face_sectors)
+    d.set_transport_options(topt)
     d.set_gpus([0])
     d.add_data("q", dt)
     d.realize()
@@ -58,7 +62,7 @@ for part, narrow in [(p, int(n)) for n in a.narrow.split(",") for p in a.parts.s
     d.sync_exchange()
     us = (time.perf_counter() - t) / a.iters * 1e6
     b = d.exchange_bytes_for_method(st.MethodFlags.All)
-    print(json.dumps({"part": part, "narrow": narrow, "shape": [X, Y, Z], "radius": R, "fp64": bool(a.fp64), "bytes": b, "us": round(us, 1),
+    print(json.dumps({"part": part, "narrow": narrow, "shape": [X, Y, Z], "radius": R, "fp64": bool(a.fp64), "x_face_sectors": a.x_face_sectors, "bytes": b, "us": round(us, 1),
                       "GBps": round(b / us / 1e3, 1)}), flush=True)
     del d
     torch.cuda.empty_cache()
