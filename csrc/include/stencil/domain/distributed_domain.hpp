@@ -147,6 +147,13 @@ struct TransportOptions {
   // padding) instead of w-cell pieces of one line per lane (build_translate_segs_q). With 64-B sectors it measured
   // no gain (stream-ordered 26.2 vs 24.9 us for faces 2, 26.8 vs 27.8 us with depth-1 edges)
   bool xFaceSectors = false;
+  // ... and switched on automatically for a GPU whose same-GPU x faces cover at least this many bytes of lines per
+  // exchange (rows x 1.5 lines of 128 B per face: the read line plus the halo line two rows share; 0 = never). Below
+  // the last-level cache's size the repeated exchange stays cache-resident and partial-line halo writes cost
+  // nothing (config 3, 512^2 rows x 1 quantity: 353 -> 303 GB/s with whole lines); beyond it they go to HBM as
+  // partial-line writes, and whole lines win (config 5a, 1024^2 rows x 4 fp64: 0.69-0.74 -> 0.55-0.57 ms; config 4,
+  // 512^2 rows x 8: 68.9 -> 74.1 Gcells/s x 8; profiles/r4/aq/)
+  int64_t xFaceLinesAutoBytes = int64_t(256) << 20;
 };
 const char *to_string(TransportOptions::Inbox v);
 const char *to_string(TransportOptions::Copy v);

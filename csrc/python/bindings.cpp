@@ -515,6 +515,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("spin_wait", &TransportOptions::spinWait)
       .def_readwrite("numa_affinity", &TransportOptions::numaAffinity)
       .def_readwrite("x_face_sectors", &TransportOptions::xFaceSectors)
+      .def_readwrite("x_face_lines_auto_bytes", &TransportOptions::xFaceLinesAutoBytes)
       .def_readwrite("null_stream_producers", &TransportOptions::nullStreamProducers)
       .def("__repr__", [](const TransportOptions &o) {
         return std::string("TransportOptions(inbox=") + to_string(o.inbox) + ", colo_copy=" + to_string(o.coloCopy) +

@@ -682,12 +682,27 @@ void DistributedDomain::realize() {
     // host-staged transport (the reference's ladder also ends at the MPI path, src/stencil.cu:185-194).
     init_rccl(shared_dev);
 
-    // same-process direct stores
+    // same-process direct stores; x faces as whole lines where asked for or where their lines outgrow the cache
     I.localTranslates = localTranslates;
+    {
+      std::map<int, int64_t> xLineBytes;
+      for (const auto &t : localTranslates) {
+        const LocalDomain &s = domains_[std::get<0>(t)];
+        const Dim3 dir = std::get<2>(t);
+        if (dir.x != 0 && dir.y == 0 && dir.z == 0 && s.gpu() == domains_[std::get<1>(t)].gpu())
+          xLineBytes[s.gpu()] += s.size().y * s.size().z * s.num_data() * 192;
+      }
+      for (auto &kv : xLineBytes)
+        if (topt_.xFaceSectors || (topt_.xFaceLinesAutoBytes > 0 && kv.second >= topt_.xFaceLinesAutoBytes))
+          I.xLineDevs.insert(kv.first);
+      if (!I.xLineDevs.empty() && !topt_.xFaceSectors)
+        LOG_DEBUG("x faces as whole lines (auto) on " << I.xLineDevs.size() << " device(s)");
+    }
     for (const auto &t : localTranslates) {
       const LocalDomain &s = domains_[std::get<0>(t)], &d = domains_[std::get<1>(t)];
       DevCtx &ctx = I.devs[I.devIndex[s.gpu()]];
-      for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, ctx.translate.host[p], topt_.xFaceSectors);
+      const bool lines = I.xLineDevs.count(s.gpu()) > 0;
+      for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, ctx.translate.host[p], lines);
       if (d.gpu() != s.gpu()) I.devs[I.devIndex[d.gpu()]].peerWriters.insert(s.gpu());
     }
     for (auto &kv : pipeMsgs) {

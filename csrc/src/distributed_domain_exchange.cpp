@@ -276,7 +276,7 @@ void DistributedDomain::prepare_skip_wrapped(int axes) {
     if (((axes & 1) && dir.x != 0) || ((axes & 2) && dir.y != 0) || ((axes & 4) && dir.z != 0)) continue;
     const LocalDomain &sd = domains_[std::get<0>(t)], &dd = domains_[std::get<1>(t)];
     DevCtx &ctx = I.devs[I.devIndex[sd.gpu()]];
-    for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p], topt_.xFaceSectors);
+    for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p], I.xLineDevs.count(sd.gpu()) > 0);
   }
   for (auto &ctx : I.devs) ctx.translateSkip.upload(ctx.dev);
   // PeerCopy pipes: the same subset, packed compactly

@@ -191,6 +191,7 @@ struct DistributedDomain::Impl {
                                     // were never sent)
   int xlogCap = 0;                  // set_transport_log ring size (exchanges)
   uint64_t xlogFirstEpoch = 0;      // first epoch logged since the last set_transport_log
+  std::set<int> xLineDevs;          // devices whose same-GPU x faces are copied as whole lines (xFaceSectors, or auto)
 };
 
 

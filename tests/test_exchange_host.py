@@ -200,6 +200,12 @@ def test_select_method_priority_and_shared_gpu(st):
     assert sel(M.Kernel, device=False) == M.None_
 
 
+def test_x_face_lines_auto_default(st):
+    """whole-line x faces switch on by themselves beyond 256 MiB of x-face lines per GPU (the last-level cache)"""
+    tr = st.TransportOptions()
+    assert tr.x_face_lines_auto_bytes == 256 << 20 and not tr.x_face_sectors
+
+
 @pytest.mark.parametrize("name", ["r1", "r2", "+x2", "-x1", "+x2-x1", "fec", "mixed"])
 @pytest.mark.parametrize("size,gpus", [((64, 12, 10), [0]), ((64, 12, 10), [0, 0]), ((32, 10, 9), [0, 0, 0]),
                                        ((30, 10, 9), [0])])

@@ -1009,6 +1009,23 @@ def test_x_face_lines_device(st, rname, gpus, size):
             dd.swap()
 
 
+@pytest.mark.parametrize("rname", ["r1", "r3", "fec"])
+@pytest.mark.parametrize("gpus,size", [([0], (64, 13, 11)), ([0, 0], (128, 13, 11))])
+def test_x_face_lines_auto_device(st, rname, gpus, size):
+    """TransportOptions.x_face_lines_auto_bytes: a GPU's same-GPU x faces switch to whole lines once their lines
+    reach the threshold (1 B here, so always; prepare_skip_wrapped's subset too), exact halos"""
+    radius = _radii(st)[rname]
+    tr = st.TransportOptions()
+    tr.x_face_lines_auto_bytes = 1
+    for dtype in (torch.float32, torch.float64):
+        dd, q = _dd(st, size, radius, gpus, st.MethodFlags.Kernel, dtype=dtype, transport=tr)
+        for it in range(2):
+            fill_coords(dd, q, offset=it)
+            dd.exchange()
+            assert check_exchange(dd, q, radius, offset=it) == 0
+            dd.swap()
+
+
 @pytest.mark.parametrize("kind,fp64", [("jacobi", False), ("astaroth", False), ("jacobi", True)])
 def test_ops_stencil7x2_apply_on_a_domain(st, kind, fp64):
     """ops.stencil7x2_apply on a user's DistributedDomain: exchange the depth-2 halos, one fused call = two steps of
