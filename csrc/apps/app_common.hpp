@@ -14,6 +14,7 @@ struct MethodArgs {
   bool staged = false, rccl = false, colo = false, peer = false, kernel = false, trivial = false;
   int interiorAlign = 128; // bytes; the row-start alignment of every interior (LocalDomain::set_interior_align)
   bool xFaceLines = false; // TransportOptions::xFaceSectors: same-GPU x faces copied as whole lines
+  int xFaceLinesAutoMiB = 256; // TransportOptions::xFaceLinesAutoBytes in MiB (0 = never by themselves)
   void add(ArgParser &p) {
     p.flag(&staged, "--staged,--remote", "host-staged transport (reference CudaMpi)")
         .flag(&rccl, "--rccl,--cuda-aware,--cuda-aware-mpi", "RCCL transport (reference CudaAwareMpi)")
@@ -22,7 +23,8 @@ struct MethodArgs {
         .flag(&kernel, "--kernel", "same-GPU kernel transport")
         .flag(&trivial, "--trivial,--naive", "trivial placement")
         .option(&interiorAlign, "--interior-align", "interior row alignment in bytes (64 or 128)")
-        .flag(&xFaceLines, "--x-face-lines", "same-GPU x faces copied as whole 128-B lines");
+        .flag(&xFaceLines, "--x-face-lines", "same-GPU x faces copied as whole 128-B lines")
+        .option(&xFaceLinesAutoMiB, "--x-face-lines-auto", "MiB of x-face lines from which whole lines switch on (0 never)");
   }
   MethodFlags flags() const {
     MethodFlags m = MethodFlags::None;
@@ -32,6 +34,12 @@ struct MethodArgs {
     if (peer) m |= MethodFlags::PeerCopy;
     if (kernel) m |= MethodFlags::Kernel;
     return any(m) ? m : MethodFlags::All;
+  }
+  // the transport options these flags set, on top of `o`
+  TransportOptions transport(TransportOptions o = {}) const {
+    o.xFaceSectors = xFaceLines;
+    o.xFaceLinesAutoBytes = int64_t(xFaceLinesAutoMiB) << 20;
+    return o;
   }
   PlacementStrategy placement() const { return trivial ? PlacementStrategy::Trivial : PlacementStrategy::NodeAware; }
 };

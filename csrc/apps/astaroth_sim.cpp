@@ -42,7 +42,7 @@ int main(int argc, char **argv) {
   cfg.methods = ma.flags();
   cfg.placement = ma.placement();
   cfg.interiorAlign = ma.interiorAlign;
-  cfg.transport.xFaceSectors = ma.xFaceLines;
+  cfg.transport = ma.transport(cfg.transport);
   cfg.overlap = !noOverlap;
   cfg.wrapSelf = !noWrap;
   StencilModel m(cfg, pg);

@@ -13,7 +13,7 @@ using namespace stencil;
 
 static std::pair<Statistics, uint64_t> bench(comm::ProcGroup &pg, int iters, int nq, const Dim3 &ext, const Radius &r,
                                              MethodFlags m, PlacementStrategy pl, bool weak, bool xHaloAlign,
-                                             bool xFaceLines, int interiorAlign) {
+                                             const app::MethodArgs &ma) {
   Dim3 e = ext;
   if (weak) e = Dim3(app::weak_scale(ext.x, pg.size()), app::weak_scale(ext.y, pg.size()), app::weak_scale(ext.z, pg.size()));
   DistributedDomain dd(e.x, e.y, e.z, comm::default_group());
@@ -21,10 +21,8 @@ static std::pair<Statistics, uint64_t> bench(comm::ProcGroup &pg, int iters, int
   dd.set_methods(m);
   dd.set_placement(pl);
   dd.set_x_halo_align(xHaloAlign);
-  dd.set_interior_align(interiorAlign);
-  TransportOptions topt;
-  topt.xFaceSectors = xFaceLines;
-  dd.set_transport_options(topt);
+  dd.set_interior_align(ma.interiorAlign);
+  dd.set_transport_options(ma.transport());
   for (int i = 0; i < nq; ++i) dd.add_data<float>("d" + std::to_string(i));
   dd.realize();
   Statistics st;
@@ -80,7 +78,7 @@ int main(int argc, char **argv) {
   }
   if (pg->rank() == 0) std::printf("name,count,trimean (S),trimean (B/s),stddev,min,avg,max\n");
   for (auto &pt : pats) {
-    auto res = bench(*pg, iters, nq, ext, pt.r, ma.flags(), ma.placement(), weak, xHaloAlign, ma.xFaceLines, ma.interiorAlign);
+    auto res = bench(*pg, iters, nq, ext, pt.r, ma.flags(), ma.placement(), weak, xHaloAlign, ma);
     if (pg->rank() == 0) {
       std::ostringstream n;
       n << x << "-" << y << "-" << z << "/" << pt.name;

@@ -31,9 +31,7 @@ int main(int argc, char **argv) {
   dd.set_methods(ma.flags());
   dd.set_placement(ma.placement());
   dd.set_interior_align(ma.interiorAlign);
-  TransportOptions topt;
-  topt.xFaceSectors = ma.xFaceLines;
-  dd.set_transport_options(topt);
+  dd.set_transport_options(ma.transport());
   for (int i = 0; i < nq; ++i) {
     if (fp64)
       dd.add_data<double>("d" + std::to_string(i));
