@@ -14,7 +14,7 @@ struct MethodArgs {
   bool staged = false, rccl = false, colo = false, peer = false, kernel = false, trivial = false;
   int interiorAlign = 128; // bytes; the row-start alignment of every interior (LocalDomain::set_interior_align)
   bool xFaceLines = false; // TransportOptions::xFaceSectors: same-GPU x faces copied as whole lines
-  int xFaceLinesAutoMiB = 256; // TransportOptions::xFaceLinesAutoBytes in MiB (0 = never by themselves)
+  int xFaceLinesAutoMiB = 128; // TransportOptions::xFaceLinesAutoBytes in MiB (0 = never by themselves)
   void add(ArgParser &p) {
     p.flag(&staged, "--staged,--remote", "host-staged transport (reference CudaMpi)")
         .flag(&rccl, "--rccl,--cuda-aware,--cuda-aware-mpi", "RCCL transport (reference CudaAwareMpi)")

@@ -152,8 +152,9 @@ struct TransportOptions {
   // the last-level cache's size the repeated exchange stays cache-resident and partial-line halo writes cost
   // nothing (config 3, 512^2 rows x 1 quantity: 353 -> 303 GB/s with whole lines); beyond it they go to HBM as
   // partial-line writes, and whole lines win (config 5a, 1024^2 rows x 4 fp64: 0.69-0.74 -> 0.55-0.57 ms; config 4,
-  // 512^2 rows x 8: 68.9 -> 74.1 Gcells/s x 8; profiles/r4/aq/)
-  int64_t xFaceLinesAutoBytes = int64_t(256) << 20;
+  // 512^2 rows x 8: 68.9 -> 74.1 Gcells/s x 8; profiles/r4/aq/). Crossover (bench_exchange 512^3 radius-2 faces,
+  // profiles/r4/au/): 1 quantity = 96 MiB of lines 337 vs 293 GB/s (stay), 2 = 192 MiB 240 vs 338 (switch)
+  int64_t xFaceLinesAutoBytes = int64_t(128) << 20;
 };
 const char *to_string(TransportOptions::Inbox v);
 const char *to_string(TransportOptions::Copy v);

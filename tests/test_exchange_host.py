@@ -201,9 +201,10 @@ def test_select_method_priority_and_shared_gpu(st):
 
 
 def test_x_face_lines_auto_default(st):
-    """whole-line x faces switch on by themselves beyond 256 MiB of x-face lines per GPU (the last-level cache)"""
+    """whole-line x faces switch on by themselves from 128 MiB of x-face lines per GPU (measured crossover between
+    96 and 192 MiB, below the 256-MB last-level cache)"""
     tr = st.TransportOptions()
-    assert tr.x_face_lines_auto_bytes == 256 << 20 and not tr.x_face_sectors
+    assert tr.x_face_lines_auto_bytes == 128 << 20 and not tr.x_face_sectors
 
 
 @pytest.mark.parametrize("name", ["r1", "r2", "+x2", "-x1", "+x2-x1", "fec", "mixed"])
