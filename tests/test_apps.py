@@ -118,6 +118,19 @@ def test_weak_and_weak_exchange_csv():
     assert re.search(rf"^weak_exchange,[a-z/]+,1,16,16,16,2,{NUM},{NUM}$", out, re.M), out[-2000:]
 
 
+def test_layout_and_x_face_flags_on_every_exchange_app():
+    """--interior-align, --x-face-lines and --x-face-lines-auto (app::MethodArgs) are accepted by every exchange
+    app; a bad alignment is refused with the LocalDomain message."""
+    flags = ["--interior-align", 64, "--x-face-lines", "--x-face-lines-auto", 0]
+    run_app("weak", 16, 16, 16, 2, *flags)
+    run_app("weak_exchange", 16, 16, 16, 2, *flags)
+    run_app("astaroth_sim", "--x", 16, "--y", 16, "--z", 16, "--q", 2, "-n", 2, "--no-wrap", *flags)
+    run_app("bench_exchange", "--x", 16, "--y", 16, "--z", 16, "--fr", 1, "--iters", 2, *flags)
+    p = subprocess.run([os.path.join(BIN, "weak"), "16", "16", "16", "2", "--interior-align", "96"], env=_env(),
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=60, cwd="/tmp")
+    assert p.returncode != 0 and "interior alignment must be 64 or 128" in p.stdout, p.stdout[-2000:]
+
+
 def test_bench_qap_and_pack():
     out = run_app("bench_qap")
     for name in ("random", "matched", "blockdiag"):

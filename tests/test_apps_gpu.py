@@ -72,6 +72,15 @@ def test_weak_and_weak_exchange_device():
     assert re.search(rf"^weak_exchange,[a-z/]+,1,64,64,64,2,{NUM},{NUM}$", out, re.M), out[-2000:]
 
 
+@pytest.mark.parametrize("flags", [["--x-face-lines"], ["--x-face-lines-auto", 0], ["--interior-align", 64]])
+def test_exchange_apps_layout_flags_device(flags):
+    """The layout / x-face flags on the device path (astaroth_sim --no-wrap exchanges every halo each step)."""
+    out = run_app("astaroth_sim", "--x", 96, "--y", 96, "--z", 96, "--q", 2, "-n", 2, "--no-wrap", *flags)
+    assert re.search(rf"^astaroth,[a-z/]+,1,96,96,96,2,{NUM},{NUM},{NUM},{NUM}$", out, re.M), out[-2000:]
+    out = run_app("bench_exchange", "--x", 64, "--y", 64, "--z", 64, "--fr", 2, "--iters", 3, *flags)
+    assert re.search(r"^64-64-64/faces/2,3,", out, re.M), out[-2000:]
+
+
 def test_bench_pack_device():
     out = run_app("bench_pack", "--n", 64, "--iters", 2)
     assert re.search(rf"^64,\[0;0;1\],{NUM},{NUM},{NUM},{NUM},{NUM}$", out, re.M), out[-2000:]
