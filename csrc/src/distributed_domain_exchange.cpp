@@ -1,5 +1,7 @@
 // DistributedDomain exchange engine: stream bookkeeping, blocking and stream-ordered exchange over every transport,
-// completion modes, transport log and swap (split out of distributed_domain.cpp).
+// completion modes, transport log and swap (split out of distributed_domain.cpp). Reference
+// counterparts: DistributedDomain::exchange() and swap() in src/stencil.cu:670-864 and :541-565 (there one
+// blocking host loop over the senders / receivers; here one stream-ordered enqueue per device).
 #include "stencil/domain/distributed_domain.hpp"
 
 #include <hip/hip_runtime_api.h>

@@ -1,4 +1,5 @@
-// DistributedDomain output and restart: ParaView CSV dumps and checkpoints (split out of distributed_domain.cpp).
+// DistributedDomain output and restart: ParaView CSV dumps (reference src/stencil.cu:866-939) and checkpoints (no
+// reference counterpart), split out of distributed_domain.cpp.
 #include "stencil/domain/distributed_domain.hpp"
 
 #include <hip/hip_runtime_api.h>
