@@ -66,126 +66,216 @@ def weak_grid(st, per_gpu: int, n: int, rule: str, axis_cost, objective) -> tupl
     return grid
 
 
-def transport_sweep(st, torch, dist, args, world, device, red_dev, axis_cost, objective, topt_base):
-    """Exchange-only GB/s of the headline decomposition with each transport set in turn, plus the reference-rule
-    point (the cbrt cube cut by the reference's greedy Interface rule with equal axis costs: 2x2x2 at N = 8, the
-    bench_exchange --x 1024 --y 1024 --z 1024 --fr 2 config), so one multi-GPU run yields the whole ladder
-    (reference: src/stencil.cu:163-194 method ladder; scripts/summit/weak_256n.sh:26-30 per-method sweeps).
+class Env:
+    """What the bench needs from the device side, with a host-backend stand-in (--cpu: the CPU path of BASELINE.json
+    config 1, and the CPU tests of this script's control flow)."""
 
-    Radius-2 faces, one fp32 quantity (the depth-2 exchange of a fused pair), blocking exchange()+swap() as in
-    bin/bench_exchange.cu:39-63 and the same exchanges stream-ordered. Each entry realizes its own domain on a fresh
-    native process group with a short timeout, so a transport that fails on one rank costs that entry (an "error"
-    string), not the run. The number of timed exchanges is agreed over ranks from a timed probe exchange, and the
-    whole section stops starting entries after --sweep-budget seconds."""
-    M = st.MethodFlags
-    C = st.TransportOptions.Completion
-    sets = [("colo_store", M.Colocated | M.Kernel, "store", C.Kernel),
-            ("colo_engine", M.Colocated | M.Kernel, "engine", C.Kernel),
-            ("colo_ipcevent", M.Colocated | M.Kernel, "store", C.IpcEvent),
-            ("rccl", M.Rccl | M.Kernel, "store", C.Kernel), ("staged", M.Staged | M.Kernel, "store", C.Kernel),
-            ("ref_rule", M.All, "store", C.Kernel)]
-    out = {}
-    t_start = time.perf_counter()
+    def __init__(self, torch, dist, cpu: bool, world: int, red_dev: str):
+        self.torch, self.dist, self.cpu, self.world, self.red_dev = torch, dist, cpu, world, red_dev
 
-    def agreed_max(v):
-        t = torch.tensor([float(v)], dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    def sync(self):
+        if not self.cpu:
+            self.torch.cuda.synchronize()
+
+    def barrier(self):
+        self.sync()
+        if self.world > 1:
+            self.dist.barrier()
+        self.sync()
+
+    def agreed_max(self, v: float) -> float:
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64, device=self.red_dev)
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
-    for name, m, copy, completion in sets:
-        if agreed_max(time.perf_counter() - t_start) > args.sweep_budget:
+    def stream(self):
+        return None if self.cpu else self.torch.cuda.Stream()
+
+
+def time_exchanges(env, dd, iters: int, xbytes: int, log: bool = False) -> dict:
+    """Blocking exchange()+swap() (bin/bench_exchange.cu:39-63) and the same exchanges stream-ordered on one stream,
+    max over ranks; GB/s = aggregate halo bytes over all ranks / time (the reference's definition). log: device
+    timestamps of the fused co-located kernels (wait vs copy) over the blocking loop."""
+    for _ in range(3):  # untimed: the first full exchanges after wrapped pairs touch cold halo lines
+        dd.exchange()
+        dd.swap()
+    if log:
+        dd.set_transport_log(iters)
+    env.barrier()
+    t = time.perf_counter()
+    for _ in range(iters):
+        dd.exchange()
+        dd.swap()
+    env.sync()
+    el = env.agreed_max(time.perf_counter() - t)
+    rec = {"iters": iters, "halo_bytes": int(xbytes), "exchange_ms": round(el / iters * 1e3, 4),
+           "GBps": round(xbytes * iters / el / 1e9, 3)}
+    if log:
+        rec["colo_kernels_us"] = colo_breakdown(dd.transport_log(0))
+        dd.set_transport_log(0)
+    xs = env.stream()
+    if xs is not None:
+        for _ in range(3):  # untimed: the first launches on a new stream create its hardware queue (~ms)
+            dd.exchange_async(xs.cuda_stream, 0)
+            dd.swap()
+        xs.synchronize()
+        dd.sync_exchange()
+        env.barrier()
+        t = time.perf_counter()
+        for _ in range(iters):
+            dd.exchange_async(xs.cuda_stream, 0)
+            dd.swap()
+        xs.synchronize()
+        dd.sync_exchange()
+        el2 = env.agreed_max(time.perf_counter() - t)
+        rec["stream_GBps"] = round(xbytes * iters / el2 / 1e9, 3)
+    return rec
+
+
+def used_methods(st, dd) -> str:
+    """The transports that carry halo bytes in this realized domain (methods() is the enabled set)."""
+    M = st.MethodFlags
+    used = M.None_
+    for f in (M.Kernel, M.PeerCopy, M.Colocated, M.Rccl, M.Staged):
+        if dd.exchange_bytes_for_method(f) > 0:
+            used = used | f
+    return st.methods_to_string(used)
+
+
+def probe_iters(env, dd, cap: int) -> int:
+    """Timed exchanges of a sweep entry: as many as fit in ~1 s (agreed over ranks), at most cap."""
+    for _ in range(2):
+        dd.exchange()
+        dd.swap()
+    env.sync()
+    t = time.perf_counter()
+    dd.exchange()
+    dd.swap()
+    probe = env.agreed_max(time.perf_counter() - t)
+    return int(max(1, min(cap, 1.0 / max(probe, 1e-6))))
+
+
+def transport_sweep(st, env, args, world, rank, device, ndev, axis_cost, objective, topt_base, methods_base) -> dict:
+    """Exchange-only GB/s of the headline decomposition with each transport set in turn, then the entries no
+    per-rank transport covers, so one multi-GPU run yields the whole ladder (reference: src/stencil.cu:163-194
+    method ladder; scripts/summit/weak_256n.sh:26-30 per-method sweeps):
+
+      colo_store / colo_engine / colo_ipcevent / rccl / staged   the headline decomposition, one transport set each
+                                                                 (rccl at N = 1: the RCCL loopback, methods Rccl only)
+      ref_rule     the cbrt cube cut by the reference's greedy Interface rule (2x2x2 at N = 8: the
+                   bench_exchange --x 1024 --y 1024 --z 1024 --fr 2 config)
+      astaroth_q8  BASELINE config 4's exchange: 8 fp32 quantities, radius 3 in all 26 directions, on the
+                   reference-rule cube, with the headline's transports (bin/astaroth_sim.cu:184-195)
+      peer_store / peer_engine   the reference's default single-process multi-GPU run: rank 0 alone realizes the
+                   headline decomposition over devices 0..N-1 (include/stencil/stencil.hpp:192-198) with
+                   PeerCopy|Kernel -- direct xGMI stores into the peer's halo, then pack + hipMemcpyPeerAsync +
+                   unpack (include/stencil/tx_cuda.cuh:106-170); the other ranks wait at a barrier. On a box with
+                   fewer GPUs than ranks the devices repeat, and `devices_used` says how many were really used.
+
+    Radius-2 faces, one fp32 quantity (the depth-2 exchange of a fused pair) unless stated. Each entry realizes its
+    own domain on a fresh native process group with a short timeout, so a transport that fails on one rank costs that
+    entry (an "error" string), not the run; an RCCL communicator that cannot be created is bounded by the same timeout
+    (non-blocking creation + abort) and reported as `rccl_status`. The section stops starting entries after
+    --sweep-budget seconds (agreed over ranks)."""
+    M = st.MethodFlags
+    C = st.TransportOptions.Completion
+    rccl_set = M.Rccl if world == 1 else M.Rccl | M.Kernel
+    sets = [("colo_store", M.Colocated | M.Kernel, {"copy": "store", "completion": C.Kernel}),
+            ("colo_engine", M.Colocated | M.Kernel, {"copy": "engine", "completion": C.Kernel}),
+            ("colo_ipcevent", M.Colocated | M.Kernel, {"copy": "store", "completion": C.IpcEvent}),
+            ("rccl", rccl_set, {}), ("staged", M.Staged | M.Kernel, {}),
+            ("ref_rule", M.All, {"grid": "ref"}),
+            ("astaroth_q8", methods_base, {"grid": "ref", "q": 8, "radius": 3}),
+            ("peer_store", M.PeerCopy | M.Kernel, {"peer": "store"}),
+            ("peer_engine", M.PeerCopy | M.Kernel, {"peer": "engine"})]
+    if args.cpu:  # host backend: only Staged and same-rank copies exist
+        sets = [s for s in sets if s[0] in ("staged", "ref_rule", "astaroth_q8", "peer_store")]
+    out = {}
+    t_start = time.perf_counter()
+    stall = os.environ.get("STENCIL_RCCL_STALL_RANK")
+    if os.environ.get("STENCIL_BENCH_SWEEP_HANG"):  # test hook: a sweep entry that never returns (arm_deadline)
+        time.sleep(1e6)
+    for name, m, o in sets:
+        if env.agreed_max(time.perf_counter() - t_start) > args.sweep_budget:
             out[name] = {"skipped": f"sweep budget {args.sweep_budget:.0f} s spent"}
             continue
         rec = {}
         ok = 1.0
         dd = None
-        if int(os.environ.get("RANK", "0")) == 0:
+        peer = "peer" in o
+        if rank == 0:
             print(f"[bench] transport {name}: starting", file=sys.stderr, flush=True)
         try:
-            if name == "ref_rule":
+            if o.get("grid") == "ref":
                 L = st.models.weak_scaled_size(args.per_gpu, world)
                 g, obj, cost = (L, L, L), st.PartitionObjective.Interface, (1, 1, 1)
             else:
                 g, obj, cost = weak_grid(st, args.per_gpu, world, args.grid, axis_cost, objective), objective, axis_cost
-            grp = st.init_process_group(set_default=False, timeout_s=15.0)
-            dd = st.DistributedDomain(*g, group=grp)
-            r = st.Radius.constant(0)
-            r.set_face(2)
-            dd.set_radius(r)
-            dd.add_data("q", torch.float32)
-            dd.set_methods(m)
-            dd.set_gpus([device])
-            dd.set_axis_cost(st.Dim3(*cost))
-            dd.set_partition_objective(obj)
-            dd.set_plan_file("")
-            dd.set_x_halo_align(bool(args.x_halo_align))
-            dd.set_interior_align(args.interior_align)
-            topt = st.TransportOptions()
-            topt.inbox = topt_base.inbox
-            topt.completion = completion
-            topt.fuse_flags = topt_base.fuse_flags
-            topt.colo_copy = topt.Copy.Engine if copy == "engine" else topt.Copy.Store
-            topt.wait_timeout = 10.0  # a failing entry gives up within seconds, not minutes
-            dd.set_transport_options(topt)
-            dd.realize()
-            pd = dd.placement_dim()
-            rec["grid"] = list(g)
-            rec["decomposition"] = f"{pd.x}x{pd.y}x{pd.z}"
-            rec["asked"] = st.methods_to_string(m)
-            rec["realized"] = st.methods_to_string(dd.methods())
-            rec["bytes_by_method"] = {st.methods_to_string(f): int(dd.exchange_bytes_for_method(f))
-                                      for f in (M.Kernel, M.PeerCopy, M.Colocated, M.Rccl, M.Staged)
-                                      if dd.exchange_bytes_for_method(f) > 0}
-            xbytes = dd.exchange_bytes_for_method(M.All)
-            for _ in range(2):
-                dd.exchange()
-                dd.swap()
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            dd.exchange()
-            dd.swap()
-            probe = agreed_max(time.perf_counter() - t)
-            iters = int(max(1, min(args.exchange_iters, 1.0 / max(probe, 1e-6))))
-            colo = dd.exchange_bytes_for_method(M.Colocated) > 0 and completion != C.StreamOp
-            if colo:
-                dd.set_transport_log(iters)
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            t = time.perf_counter()
-            for _ in range(iters):
-                dd.exchange()
-                dd.swap()
-            el = agreed_max(time.perf_counter() - t)
-            if colo:
-                rec["colo_kernels_us"] = colo_breakdown(dd.transport_log(0))
-                dd.set_transport_log(0)
-            xs = torch.cuda.Stream()
-            dd.exchange_async(xs.cuda_stream, 0)
-            dd.swap()
-            xs.synchronize()
-            dd.sync_exchange()
-            if world > 1:
-                dist.barrier()
-            t = time.perf_counter()
-            for _ in range(iters):
-                dd.exchange_async(xs.cuda_stream, 0)
-                dd.swap()
-            xs.synchronize()
-            dd.sync_exchange()
-            el2 = agreed_max(time.perf_counter() - t)
-            rec.update({"iters": iters, "halo_bytes": int(xbytes), "exchange_ms": round(el / iters * 1e3, 4),
-                        "GBps": round(xbytes * iters / el / 1e9, 3),
-                        "stream_GBps": round(xbytes * iters / el2 / 1e9, 3)})
+            if peer and rank != 0:
+                rec["by"] = "rank 0"
+            else:
+                grp = st.make_single_group() if peer else st.init_process_group(set_default=False, timeout_s=15.0)
+                dd = st.DistributedDomain(*g, group=grp)
+                if args.cpu:
+                    dd.set_backend(st.Backend.Host)
+                r = st.Radius.constant(o.get("radius", 0))
+                if "radius" not in o:
+                    r.set_face(2)
+                dd.set_radius(r)
+                for q in range(o.get("q", 1)):
+                    dd.add_data(f"q{q}", env.torch.float32)
+                dd.set_methods(m)
+                gpus = [k % max(1, ndev) for k in range(world)] if peer else [device]
+                dd.set_gpus(gpus)
+                dd.set_axis_cost(st.Dim3(*cost))
+                dd.set_partition_objective(obj)
+                dd.set_plan_file("")
+                dd.set_x_halo_align(bool(args.x_halo_align))
+                dd.set_interior_align(args.interior_align)
+                topt = st.TransportOptions()
+                topt.inbox = topt_base.inbox
+                topt.completion = o.get("completion", topt_base.completion)
+                topt.fuse_flags = topt_base.fuse_flags
+                cp = o.get("copy")
+                topt.colo_copy = topt_base.colo_copy if cp is None else (
+                    topt.Copy.Engine if cp == "engine" else topt.Copy.Store)
+                topt.peer_copy = topt.Copy.Engine if o.get("peer") == "engine" else topt.Copy.Store
+                topt.wait_timeout = 10.0  # a failing entry gives up within seconds, not minutes
+                if stall is not None:  # rehearses a rank stuck before RCCL communicator creation
+                    topt.stall_rccl_init_rank = int(stall)
+                dd.set_transport_options(topt)
+                dd.realize()
+                pd = dd.placement_dim()
+                rec["grid"] = list(g)
+                rec["decomposition"] = f"{pd.x}x{pd.y}x{pd.z}"
+                rec["asked"] = st.methods_to_string(m)
+                rec["realized"] = used_methods(st, dd)
+                if dd.rccl_status():
+                    rec["rccl_status"] = dd.rccl_status()
+                    if dd.rccl_status() != "ok":
+                        rec["error"] = f"RCCL communicator: {dd.rccl_status()} (halos ran host-staged)"
+                if peer:
+                    rec["devices_used"] = len(set(gpus))
+                    rec["device_count"] = ndev
+                rec["bytes_by_method"] = {st.methods_to_string(f): int(dd.exchange_bytes_for_method(f))
+                                          for f in (M.Kernel, M.PeerCopy, M.Colocated, M.Rccl, M.Staged)
+                                          if dd.exchange_bytes_for_method(f) > 0}
+                penv = Env(env.torch, env.dist, env.cpu, 1, env.red_dev) if peer else env
+                iters = probe_iters(penv, dd, args.exchange_iters)
+                colo = dd.exchange_bytes_for_method(M.Colocated) > 0 and topt.completion != C.StreamOp
+                rec.update(time_exchanges(penv, dd, iters, int(dd.exchange_bytes_for_method(M.All)),
+                                          log=colo and not args.cpu))
         except Exception as e:  # noqa: BLE001 -- one transport failing must not end the run
             ok = 0.0
             rec["error"] = f"{type(e).__name__}: {str(e)[:300]}"
         del dd
-        if agreed_max(1.0 - ok) > 0 and "error" not in rec:
+        if peer:
+            env.barrier()  # the other ranks wait here while rank 0 drives every GPU
+        if env.agreed_max(1.0 - ok) > 0 and "error" not in rec:
             rec["error"] = "failed on another rank"
         out[name] = rec
-        if int(os.environ.get("RANK", "0")) == 0:
+        if rank == 0:
             print(f"[bench] transport {name}: {rec}", file=sys.stderr, flush=True)
     return out
 
@@ -270,12 +360,14 @@ def rank_setup(gpus: int, launch_timeout: float, argv: list[str]):
     return None
 
 
-def main():
+def build_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--per-gpu", type=int, default=512)
+    ap.add_argument("--cpu", action="store_true",
+                    help="host backend, no GPU (BASELINE config 1's CPU path; the CPU tests of this script)")
     ap.add_argument("--exchange-iters", type=int, default=20)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--methods", default="all")
@@ -303,6 +395,10 @@ def main():
     ap.add_argument("--wrap", type=int, default=1,
                     help="fused pairs read the periodic image along axes the decomposition leaves whole (no self-copy "
                          "of those halos); 0 = copy every halo")
+    ap.add_argument("--with-exchange", choices=["auto", "on", "off"], default="auto",
+                    help="after the headline, time the same steps with every halo copied (BASELINE config 2 as "
+                         "defined: intra-GPU pack/unpack + compute, the reference's exchange() every iteration) -> "
+                         "extra.gcells_with_exchange (auto: on unless --wrap 0 already copies every halo)")
     ap.add_argument("--x-halo-align", type=int, default=0,
                     help="x halos inside the interior's first / last 64-B sector (LocalDomain::set_x_halo_align): "
                          "one sector per row end for x-face copies; every row spans one more sector")
@@ -324,6 +420,10 @@ def main():
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU, and then "
                          "overlapped or whole-region pairs, whichever runs faster in the warm-up)")
+    ap.add_argument("--transport", choices=["auto", "fixed"], default="auto",
+                    help="N > 1: auto = the warm-up times whole steps (max over ranks) with Colocated over uncached / "
+                         "fine-grained / coarse-grained inboxes and with Rccl, and keeps the fastest for the timed loop "
+                         "(extra.transport_tuned); fixed = --methods / --inbox as given")
     ap.add_argument("--colo-copy", choices=["auto", "store", "engine"], default="store",
                     help="co-located (HIP IPC) halos: the pack kernel stores into the peer's inbox (store, default), or "
                          "a DMA engine copies the packed message (engine); auto: both tried in the warm-up. Engine "
@@ -340,67 +440,25 @@ def main():
                     help="multi-process: verify the transports on a probe domain first and fall back along "
                          "Colocated -> Rccl -> Staged until every halo arrives correctly")
     ap.add_argument("--tune-steps", type=int, default=8,
-                    help="steps per timed round of the overlap choice (auto, remote halos only; 0 = no choice)")
+                    help="steps per timed round of the transport / overlap choice (N > 1; 0 = no choice)")
     ap.add_argument("--transport-sweep", choices=["auto", "on", "off"], default="auto",
-                    help="after the headline: exchange-only GB/s of every transport set on the same decomposition "
-                         "and of the reference-rule cube (auto: only with N > 1)")
-    ap.add_argument("--sweep-budget", type=float, default=30.0,
+                    help="after the headline: exchange-only GB/s of every transport set on the same decomposition, the "
+                         "reference-rule cube, config 4's 8-quantity radius-3 exchange and the single-process "
+                         "PeerCopy run (auto: only with N > 1)")
+    ap.add_argument("--sweep-budget", type=float, default=60.0,
                     help="seconds after which the transport sweep starts no further entry")
+    ap.add_argument("--sweep-deadline", type=float, default=240.0,
+                    help="seconds after which a still-running sweep is abandoned: every rank exits 0 behind the "
+                         "headline line it already printed (a transport hanging on real links cannot take it)")
     ap.add_argument("--launch-timeout", type=float, default=3000,
                     help="--gpus N>1 without a launcher: seconds before the spawned ranks are stopped (0 = none)")
-    args = ap.parse_args()
-    rc = rank_setup(args.gpus, args.launch_timeout, sys.argv[1:])
-    if rc is not None:
-        return rc
-    _limit_queues_when_sharing()
+    return ap.parse_args(argv)
 
-    import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
-    device = local_rank % max(1, ndev)
-    torch.cuda.set_device(device)
-    # one rank per GPU: RCCL for the harness barrier/max-reduce. More ranks than GPUs (a rehearsal on a 1-GPU box,
-    # ranks sharing the device through HIP IPC) cannot use RCCL, so the harness collectives go over gloo.
-    shared = world > ndev
-    if world > 1:
-        if shared:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-    red_dev = "cpu" if shared else "cuda"
-
-    import stencil2_amd as st
-
-    pg = st.init_process_group()
-    n = world
-    L = st.models.weak_scaled_size(args.per_gpu, n)
-    axis_cost = tuple(int(v) for v in args.axis_cost.split(","))
-    objective = st.PartitionObjective.MaxLink if args.partition == "maxlink" else st.PartitionObjective.Interface
-    grid = weak_grid(st, args.per_gpu, n, args.grid, axis_cost, objective)
-    methods = st.MethodFlags.All
-    if args.methods != "all":
-        methods = st.MethodFlags.None_
-        for m in args.methods.split(","):
-            methods = methods | getattr(st.MethodFlags, {"staged": "Staged", "rccl": "Rccl", "colo": "Colocated",
-                                                          "peer": "PeerCopy", "kernel": "Kernel"}[m])
-
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    # Transport self-test (multi-process only, DistributedDomain::set_self_test, run inside realize): a
-    # coordinate-encoded field on a small probe domain with the model's radius, placement and transports is exchanged
-    # and checked cell by cell on every rank; any wrong halo or error drops Colocated, then Rccl (host-staged), so a
-    # scaling run never times silently corrupted halos. An RCCL communicator that fails to form falls back to the
-    # host-staged path on every rank as well.
+def make_transport(st, args, inbox=None):
     topt = st.TransportOptions()
-    topt.inbox = {"uncached": topt.Inbox.Uncached, "fine": topt.Inbox.Fine, "coarse": topt.Inbox.Coarse}[args.inbox]
+    topt.inbox = {"uncached": topt.Inbox.Uncached, "fine": topt.Inbox.Fine,
+                  "coarse": topt.Inbox.Coarse}[inbox or args.inbox]
     topt.colo_copy = topt.Copy.Engine if args.colo_copy == "engine" else topt.Copy.Store
     topt.completion = {"kernel": topt.Completion.Kernel, "streamop": topt.Completion.StreamOp,
                        "ipcevent": topt.Completion.IpcEvent}[args.completion]
@@ -408,6 +466,80 @@ def main():
     topt.x_face_sectors = bool(args.x_face_lines)
     if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # rehearses the fallback (scripts): IPC probe reports failure
         topt.fail_ipc_probe = True
+    if os.environ.get("STENCIL_RCCL_STALL_RANK") is not None:  # rehearses a rank stuck in RCCL creation
+        topt.stall_rccl_init_rank = int(os.environ["STENCIL_RCCL_STALL_RANK"])
+    return topt
+
+
+def parse_methods(st, spec: str):
+    if spec == "all":
+        return st.MethodFlags.All
+    m = st.MethodFlags.None_
+    for k in spec.split(","):
+        m = m | getattr(st.MethodFlags, {"staged": "Staged", "rccl": "Rccl", "colo": "Colocated",
+                                         "peer": "PeerCopy", "kernel": "Kernel"}[k])
+    return m
+
+
+def emit(line: dict):
+    """Rank 0's JSON line. Printed twice: right after the headline loop (so nothing later -- the transport sweep on
+    real links -- can cost it), then again with extra.transports filled in."""
+    print(json.dumps(line), flush=True)
+
+
+def arm_deadline(seconds: float, rank: int):
+    """Every rank exits 0 if the sweep is still running `seconds` from now: the headline line is already out, and a
+    hung transport entry must end the job, not run it into the driver's limit."""
+    import threading
+
+    def fire():
+        print(f"[bench] rank {rank}: transport sweep still running after {seconds:.0f} s; abandoning it (the headline "
+              f"line was printed before the sweep)", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(0)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def main(argv=None):
+    args = build_args(argv)
+    rc = rank_setup(args.gpus, args.launch_timeout, sys.argv[1:] if argv is None else list(argv))
+    if rc is not None:
+        return rc
+    if not args.cpu:
+        _limit_queues_when_sharing()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = 0 if args.cpu else torch.cuda.device_count()
+    device = local_rank % max(1, ndev)
+    if not args.cpu:
+        torch.cuda.set_device(device)
+    # one rank per GPU: RCCL for the harness barrier/max-reduce. More ranks than GPUs (a rehearsal on a 1-GPU box,
+    # ranks sharing the device through HIP IPC) cannot use RCCL, so the harness collectives go over gloo (as --cpu).
+    shared = args.cpu or world > ndev
+    if world > 1:
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+    env = Env(torch, dist, args.cpu, world, "cpu" if shared else "cuda")
+
+    import stencil2_amd as st
+
+    pg = st.init_process_group()
+    n = world
+    axis_cost = tuple(int(v) for v in args.axis_cost.split(","))
+    objective = st.PartitionObjective.MaxLink if args.partition == "maxlink" else st.PartitionObjective.Interface
+    grid = weak_grid(st, args.per_gpu, n, args.grid, axis_cost, objective)
+    methods = parse_methods(st, args.methods)
 
     tune = st.StencilTune()
     tune.nontemporal = bool(args.nt)
@@ -423,38 +555,102 @@ def main():
     tune.x2sched = args.x2sched
     tune.x2xfast = args.x2xfast
     overlap = not args.no_overlap and args.overlap != "off"
-    model = st.Jacobi3D(grid, gpus=[device], methods=methods, overlap=overlap,
-                        auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
-                        axis_cost=axis_cost, partition=objective, wrap_self=bool(args.wrap), transport=topt,
-                        self_test=bool(args.self_test) and world > 1, x_halo_align=bool(args.x_halo_align),
-                        interior_align=args.interior_align)
-    model.init()
+
+    # Transport self-test (multi-process only, DistributedDomain::set_self_test, run inside realize): a
+    # coordinate-encoded field on a small probe domain with the model's radius, placement and transports is exchanged
+    # and checked cell by cell on every rank; any wrong halo or error drops Colocated, then Rccl (host-staged), so a
+    # scaling run never times silently corrupted halos. An RCCL communicator that fails to form (or never forms:
+    # bounded non-blocking creation) falls back to the host-staged path on every rank as well.
+    def build(topt, meth, wrap_self=None):
+        model = st.Jacobi3D(grid, gpus=[device], methods=meth, overlap=overlap, auto_overlap=args.overlap == "auto",
+                            tune=tune, temporal=args.temporal, group=pg, axis_cost=axis_cost, partition=objective,
+                            wrap_self=bool(args.wrap) if wrap_self is None else wrap_self, transport=topt,
+                            self_test=bool(args.self_test) and world > 1, x_halo_align=bool(args.x_halo_align),
+                            interior_align=args.interior_align, backend=st.Backend.Host if args.cpu else None)
+        model.init()
+        model.prepare()  # hipGraph capture + instantiation (no steps run) outside the timed region
+        model.run(args.warmup)
+        model.synchronize()
+        env.barrier()
+        return model
+
+    def timed_run(model, k):
+        env.barrier()
+        t = time.perf_counter()
+        model.run(k)
+        model.synchronize()
+        return env.agreed_max(time.perf_counter() - t) / k * 1e3
+
+    def release(model):
+        del model
+        import gc
+        gc.collect()
+        env.barrier()
+
+    # Transport chosen by measurement (N > 1): whole steps, max over ranks, best of two rounds, for Colocated over the
+    # three inbox memories and for Rccl (the reference ladder's next rung). A default picked where "xGMI" was local
+    # HBM must not decide the first multi-GPU record (reference: per-rung runs,
+    # scripts/summit/weak_256n.sh:26-30, ladder src/stencil.cu:163-194).
+    topt = make_transport(st, args)
+    transport_tuned = None
+    model = None
+    if world > 1 and args.transport == "auto" and args.tune_steps > 0:
+        M = st.MethodFlags
+        cands = [("colo_uncached", methods, "uncached"), ("colo_fine", methods, "fine"),
+                 ("colo_coarse", methods, "coarse"),
+                 ("rccl", M(int(methods) & ~int(M.Colocated)), args.inbox)]
+        k = max(2, args.tune_steps // 2 * 2)
+        best = None
+        transport_tuned = {}
+        for name, meth, inbox in cands:
+            rec = {}
+            cand = None
+            try:
+                t_ = make_transport(st, args, inbox)
+                cand = build(t_, meth)
+                rec["realized"] = used_methods(st, cand.domain)
+                if cand.domain.rccl_status():
+                    rec["rccl_status"] = cand.domain.rccl_status()
+                ms = min(timed_run(cand, k), timed_run(cand, k))
+                rec["ms"] = round(ms, 4)
+            except Exception as e:  # noqa: BLE001 -- a candidate failing on this rank: the others learn it below
+                rec["error"] = f"{type(e).__name__}: {str(e)[:200]}"
+                ms = float("inf")
+            if env.agreed_max(0.0 if "error" not in rec else 1.0) > 0:
+                ms = float("inf")
+                rec.setdefault("error", "failed on another rank")
+            transport_tuned[name] = rec
+            if rank == 0:
+                print(f"[bench] transport choice {name}: {rec}", file=sys.stderr, flush=True)
+            if cand is not None and (best is None or ms < best[0]):
+                if best is not None:
+                    release(best[1])
+                best = (ms, cand, name, t_, meth)
+            elif cand is not None:
+                release(cand)
+        if best is None or best[0] == float("inf"):
+            if best is not None:
+                release(best[1])
+            transport_tuned["chosen"] = "fixed (every candidate failed)"
+        else:
+            _, model, chosen, topt, methods = best
+            transport_tuned["chosen"] = chosen
+    if model is None:
+        model = build(topt, methods)
     methods = model.domain.methods()
     preflight = model.domain.self_test_report() or "skipped"
     colo = model.domain.exchange_bytes_for_method(st.MethodFlags.Colocated) > 0
-    model.prepare()  # hipGraph capture + instantiation (no steps run) outside the timed region
-    model.run(args.warmup)
-    model.synchronize()
-    barrier()
+
     # overlapped vs whole-region pairs (remote halos only): both run, the faster one (max over ranks, best of two
     # rounds) is kept for the timed loop -- part of the warm-up, every rank takes the same decision
     overlap_tuned = None
     if args.overlap == "auto" and args.tune_steps > 0 and model.can_toggle_overlap():
-        def timed_run(k):
-            barrier()
-            t = time.perf_counter()
-            model.run(k)
-            model.synchronize()
-            dt = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=red_dev)
-            if world > 1:
-                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            return float(dt.item()) / k * 1e3
         best = {}
         k = max(2, args.tune_steps // 2 * 2)
         r0 = args.x2reserve
         # (mode, CUs left to the transports, co-located copy): mode 1 = slabs beside the sweep, 2 = slabs after
-        # it, 0 = whole-region pairs, 3 = pipelined whole-region pairs; copy "s" = pack kernel stores into the peer inbox, "e" = DMA engine copy (the
-        # transports then need fewer CUs: also tried with a quarter of the reserve)
+        # it, 0 = whole-region pairs, 3 = pipelined whole-region pairs; copy "s" = pack kernel stores into the peer
+        # inbox, "e" = DMA engine copy (the transports then need fewer CUs: also tried with a quarter of the reserve)
         copies = ["s", "e"] if colo and args.colo_copy == "auto" else ["e" if args.colo_copy == "engine" else "s"]
         cands = []
         for cp in copies:
@@ -481,12 +677,12 @@ def main():
             # a 2-step probe first: a candidate far slower than the best so far (ranks sharing one GPU: DMA-engine
             # copies beside overlapped sweeps ran at ~0.8 s per step, profiles/r3/check2) is not given full rounds
             ref = min(best.values(), default=float("inf"))
-            t = timed_run(2)
+            t = timed_run(model, 2)
             if t > 4 * ref:
                 skip.add(c)
                 best[c] = min(best.get(c, float("inf")), t)
             else:
-                best[c] = min(best.get(c, float("inf")), t, timed_run(k))
+                best[c] = min(best.get(c, float("inf")), t, timed_run(model, k))
             if rank == 0:
                 print(f"[bench] overlap choice {c}: {best[c]:.4f} ms/step{' (skipped)' if c in skip else ''}",
                       file=sys.stderr, flush=True)
@@ -494,117 +690,109 @@ def main():
         apply(choice)
         model.run(2)
         model.synchronize()
-        barrier()
+        env.barrier()
         overlap_tuned = {"mode": choice[0], "reserve": choice[1], "colo_copy": "engine" if choice[2] == "e" else "store",
                          **{f"m{c[0]}_r{c[1]}_{c[2]}_ms": round(best[c], 4) for c in cands}}
+
+    # ---- the timed loop: exactly --steps steps, bracketed by a barrier + device synchronize on both sides ----
+    env.barrier()
     t0 = time.perf_counter()
     model.run(args.steps)  # every step is enqueued; whole blocks of steps replay as one hipGraph where possible
     model.synchronize()
-    torch.cuda.synchronize()
+    env.sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = env.agreed_max(elapsed)
     cells = grid[0] * grid[1] * grid[2]
     gcells = cells * args.steps / elapsed / 1e9
 
     # exchange-only loop on the same decomposition (halo-exchange GB/s, bench_exchange definition)
     dd = model.domain
     dd.set_comm_max_blocks(0)  # the exchange alone may use the whole GPU (the overlapped steps confine it to 8 CUs)
-    xbytes = dd.exchange_bytes_for_method(st.MethodFlags.All)
-    for _ in range(3):  # untimed: the first full exchanges after wrapped pairs touch cold halo lines
-        dd.exchange()
-        dd.swap()
-    colo_log = colo and topt.completion != topt.Completion.StreamOp
-    if colo_log:  # device timestamps of the fused co-located kernels (wait vs copy), no host cost
-        dd.set_transport_log(args.exchange_iters)
-    barrier()
-    t1 = time.perf_counter()
-    for _ in range(args.exchange_iters):
-        dd.exchange()
-        dd.swap()
-    torch.cuda.synchronize()
-    xel = time.perf_counter() - t1
-    colo_phases = colo_breakdown(dd.transport_log(0)) if colo_log else None
-    if colo_log:
-        dd.set_transport_log(0)
-    tx = torch.tensor([xel], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        dist.all_reduce(tx, op=dist.ReduceOp.MAX)
-    xel = float(tx.item())
-    xgbs = xbytes * args.exchange_iters / xel / 1e9
-    # the same exchanges stream-ordered back to back (exchange_async on one stream, a single synchronize at the end):
-    # the transports' own rate without the host round trip of every blocking exchange()
-    xs = torch.cuda.Stream()
-    for _ in range(3):  # untimed: the first launches on a new stream create its hardware queue (~ms)
-        dd.exchange_async(xs.cuda_stream, 0)
-        dd.swap()
-    xs.synchronize()
-    dd.sync_exchange()
-    barrier()
-    t2 = time.perf_counter()
-    for _ in range(args.exchange_iters):
-        dd.exchange_async(xs.cuda_stream, 0)
-        dd.swap()
-    xs.synchronize()
-    dd.sync_exchange()
-    xel2 = time.perf_counter() - t2
-    tx2 = torch.tensor([xel2], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        dist.all_reduce(tx2, op=dist.ReduceOp.MAX)
-    xgbs_stream = xbytes * args.exchange_iters / float(tx2.item()) / 1e9
+    xbytes = int(dd.exchange_bytes_for_method(st.MethodFlags.All))
+    colo_log = colo and topt.completion != topt.Completion.StreamOp and not args.cpu
+    xrec = time_exchanges(env, dd, args.exchange_iters, xbytes, log=colo_log)
 
-    pdim = model.domain.placement_dim()
+    pdim = dd.placement_dim()
+    wrap_axes = "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none"
     model_cfg = {
         "decomposition": f"{pdim.x}x{pdim.y}x{pdim.z}", "methods": st.methods_to_string(methods), "preflight": preflight,
         "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
+        "transport_tuned": transport_tuned,
         "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
         "x_face_lines": bool(args.x_face_lines),
         "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
         "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x2row": args.x2row, "x2sched": args.x2sched,
         "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": model.temporal_blocking() and 2 or 1,
-        "wrap_axes": "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none",
-        "transport": {"inbox": args.inbox,
-                      "colo_copy": str(model.domain.transport_options().colo_copy).split(".")[-1].lower(),
+        "wrap_axes": wrap_axes, "backend": "host" if args.cpu else "device",
+        "transport": {"inbox": str(dd.transport_options().inbox).split(".")[-1].lower(),
+                      "colo_copy": str(dd.transport_options().colo_copy).split(".")[-1].lower(),
                       "completion": args.completion, "fuse_flags": bool(args.fuse_flags)},
     }
     del dd
-    del model
-    transports = None
-    if args.transport_sweep == "on" or (args.transport_sweep == "auto" and world > 1):
-        transports = transport_sweep(st, torch, dist, args, world, device, red_dev, axis_cost, objective, topt)
+    release(model)
+    model = None
 
+    # BASELINE config 2 as the reference times it (bin/jacobi3d.cu:265-346: exchange() every iteration): the same
+    # steps with every halo copied -- the intra-GPU pack/unpack (same-GPU copy-plan kernel) plus the compute kernels
+    with_x = None
+    if args.with_exchange == "on" or (args.with_exchange == "auto" and wrap_axes != "none"):
+        m2 = build(topt, methods, wrap_self=False)
+        if model_cfg["overlap_tuned"] is not None and m2.can_toggle_overlap():
+            m2.set_overlap_mode(overlap_tuned["mode"])
+            m2.set_comm_reserve(overlap_tuned["reserve"])
+            m2.run(2)
+            m2.synchronize()
+        env.barrier()
+        t = time.perf_counter()
+        m2.run(args.steps)
+        m2.synchronize()
+        env.sync()
+        el = env.agreed_max(time.perf_counter() - t)
+        with_x = {"gcells": round(cells * args.steps / el / 1e9, 3), "ms_per_step": round(el / args.steps * 1e3, 4),
+                  "wrap_axes": "".join(c for i, c in enumerate("xyz") if m2.wrap_axes() >> i & 1) or "none",
+                  "halo_bytes_per_exchange": int(m2.domain.exchange_bytes_for_method(st.MethodFlags.All))}
+        release(m2)
+
+    out = {
+        "metric": "Jacobi3D Gcells/s (512^3/GPU weak scaling; halo-exchange GB/s in extra)",
+        "value": round(gcells, 3),
+        "unit": "Gcells/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (reference Jacobi3D initial condition: 0.5 + hot/cold spheres)",
+        "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": max(grid),
+                   "grid": list(grid), "grid_rule": args.grid, "partition": args.partition, "per_gpu": args.per_gpu,
+                   "radius": 1, "parallelism": f"domain-decomp{n}",
+                   **model_cfg,
+                   "build": st.build_info()["git_sha"]},
+        "extra": {"halo_exchange_GBps": xrec["GBps"], "halo_exchange_stream_GBps": xrec.get("stream_GBps"),
+                  "halo_bytes_per_exchange": xbytes, "exchange_ms": xrec["exchange_ms"],
+                  "gcells_per_gpu": round(gcells / n, 3), "colo_kernels_us": xrec.get("colo_kernels_us"),
+                  "gcells_with_exchange": with_x["gcells"] if with_x else None, "with_exchange": with_x,
+                  "transports": "pending" if (args.transport_sweep == "on" or
+                                              (args.transport_sweep == "auto" and world > 1)) else None},
+    }
     if rank == 0:
-        out = {
-            "metric": "Jacobi3D Gcells/s (512^3/GPU weak scaling; halo-exchange GB/s in extra)",
-            "value": round(gcells, 3),
-            "unit": "Gcells/s",
-            "n_gpus": n,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (reference Jacobi3D initial condition: 0.5 + hot/cold spheres)",
-            "config": {"model": "jacobi3d", "global_batch": cells, "seq_len": max(grid),
-                       "grid": list(grid), "grid_rule": args.grid, "partition": args.partition, "per_gpu": args.per_gpu, "radius": 1,
-                       "parallelism": f"domain-decomp{n}",
-                       **model_cfg,
-                       "build": st.build_info()["git_sha"]},
-            "extra": {"halo_exchange_GBps": round(xgbs, 3), "halo_exchange_stream_GBps": round(xgbs_stream, 3),
-                      "halo_bytes_per_exchange": int(xbytes),
-                      "exchange_ms": round(xel / args.exchange_iters * 1e3, 4),
-                      "gcells_per_gpu": round(gcells / n, 3), "colo_kernels_us": colo_phases,
-                      "transports": transports},
-        }
-        print(json.dumps(out), flush=True)
+        emit(out)  # line 1: the headline, before anything that could hang
+
+    if out["extra"]["transports"] == "pending":
+        timer = arm_deadline(args.sweep_deadline, rank)
+        out["extra"]["transports"] = transport_sweep(st, env, args, world, rank, device, ndev, axis_cost, objective,
+                                                     topt, methods)
+        timer.cancel()
+        if rank == 0:
+            emit(out)  # line 2: the same headline with the sweep
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

@@ -119,6 +119,10 @@ struct TransportOptions {
   bool failIpcProbe = false;
   // test hook: RCCL communicator creation reports failure on this rank (rehearses the RCCL -> staged fallback)
   bool failRcclInit = false;
+  // test hook: this rank never enters RCCL communicator creation and reports a timeout after waitTimeout (a rank
+  // stuck before ncclCommInitRank); its peers' non-blocking creation runs into the same deadline and aborts, and the
+  // failure is agreed on like any other (-> host-staged)
+  int stallRcclInitRank = -1;
   // test hook: PeerCopy engine pipes between sub-domains on the SAME device also go through hipMemcpyPeerAsync
   // (src device == dst device is legal), so the cross-GPU peer-copy call runs on a one-GPU box
   bool peerApiSameDevice = false;
@@ -221,6 +225,9 @@ public:
   // (src/stencil.cu:163-194). methods() afterwards is the verified set; self_test_report() says what happened.
   void set_self_test(bool on) { selfTest_ = on; }
   const std::string &self_test_report() const { return selfTestReport_; }
+  // RCCL communicator creation in realize(): "" (no RCCL channel planned), "ok", or why it failed (the channels then
+  // run host-staged)
+  const std::string &rccl_status() const { return rcclStatus_; }
   // one probe: wrong halo cells summed over all ranks (0 = the transports of `m` deliver every halo correctly)
   int64_t probe_transports(MethodFlags m);
   // typed transport configuration (before realize)
@@ -366,12 +373,15 @@ private:
   TransportOptions topt_;
   bool selfTest_ = false;
   std::string selfTestReport_;
+  std::string rcclStatus_;
   int probeFailures_ = 0; // TransportOptions::failProbeRank bookkeeping
   // set when an exchange failed fatally (device wait timed out, RCCL error/timeout): every later exchange refuses to
   // run instead of handing a torn-down transport to the GPU
   std::string poisoned_;
   void poison(const std::string &why);
   void init_rccl(const std::function<bool(int, int)> &sharedDev); // realize(): communicator or staged fallback
+  bool drain_ipc_acks(double timeout_s);
+  bool x_face_lines(const LocalDomain &s, const LocalDomain &d) const; // translate s -> d copies x faces as lines // Completion::IpcEvent: consume the last two exchanges' Acks
   std::string planPrefix_ = "plan";
   int numaNode_ = -1; // NUMA node the calling thread was bound to in realize() (-1: none)
 

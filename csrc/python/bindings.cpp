@@ -509,6 +509,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ipc_probe", &TransportOptions::ipcProbe)
       .def_readwrite("fail_ipc_probe", &TransportOptions::failIpcProbe)
       .def_readwrite("fail_rccl_init", &TransportOptions::failRcclInit)
+      .def_readwrite("stall_rccl_init_rank", &TransportOptions::stallRcclInitRank)
       .def_readwrite("fail_probe_rank", &TransportOptions::failProbeRank)
       .def_readwrite("peer_api_same_device", &TransportOptions::peerApiSameDevice)
       .def_readwrite("jitter_us", &TransportOptions::jitterUs)
@@ -618,6 +619,7 @@ PYBIND11_MODULE(_C, m) {
       .def("numa_node", &DistributedDomain::numa_node)
       .def("set_self_test", &DistributedDomain::set_self_test)
       .def("self_test_report", &DistributedDomain::self_test_report)
+      .def("rccl_status", &DistributedDomain::rccl_status)
       .def("probe_transports", &DistributedDomain::probe_transports, py::call_guard<py::gil_scoped_release>())
       .def_readwrite("exchange_stats", &DistributedDomain::exchangeStats_)
       .def("realize", &DistributedDomain::realize, py::call_guard<py::gil_scoped_release>())

@@ -78,6 +78,14 @@ void DistributedDomain::set_transport_options(const TransportOptions &o) {
   if (topt_.waitTimeout <= 0) topt_.waitTimeout = env_wait_timeout(60.0);
 }
 
+// whole-line x faces for the translate s -> d: where asked for explicitly, else only on a device whose same-GPU x
+// faces reached the auto threshold and only for its same-GPU translates (the threshold was measured there; a
+// PeerCopy store across xGMI is left as w-cell pieces)
+bool DistributedDomain::x_face_lines(const LocalDomain &s, const LocalDomain &d) const {
+  if (topt_.xFaceSectors) return true;
+  return s.gpu() == d.gpu() && impl_->xLineDevs.count(s.gpu()) > 0;
+}
+
 void DistributedDomain::poison(const std::string &why) {
   if (poisoned_.empty()) poisoned_ = why;
 }
@@ -92,6 +100,8 @@ DistributedDomain::~DistributedDomain() {
         (void)HIP_TRY(hipSetDevice(d.dev));
         (void)HIP_TRY(hipStreamSynchronize(d.comm));
       }
+      // the Acks no later record consumes: the next IpcEvent domain on this group reuses the channel tags
+      if (!drain_ipc_acks(topt_.waitTimeout)) LOG_WARN("IPC-event acks not drained within the wait timeout");
     } catch (...) {
     }
   }
@@ -103,7 +113,10 @@ DistributedDomain::~DistributedDomain() {
     if (c.dbuf) (void)hipFree(c.dbuf);
     if (c.hbuf) (void)hipHostFree(c.hbuf);
     if (c.ipcEvent) (void)hipEventDestroy(c.ipcEvent);
-    for (auto &r : c.ipcRetired) (void)hipEventDestroy(r.first);
+    for (auto &r : c.ipcRetired) {
+      if (r.fence) (void)hipEventDestroy(r.fence);
+      (void)hipEventDestroy(r.event);
+    }
     if (c.remoteFlag) (void)hipIpcCloseMemHandle(c.remoteFlag);
     if (c.remoteData) (void)hipIpcCloseMemHandle(c.remoteData);
   }
@@ -219,17 +232,9 @@ void DistributedDomain::init_rccl(const std::function<bool(int, int)> &sharedDev
     ok = 0;
   }
   if (ok) {
-    // a communicator that never forms (a rank died between the bcast and here) blocks in RCCL itself: say so
-    // with the plan after the wait timeout instead of hanging silently
-    std::mutex mu;
-    std::condition_variable cv;
-    bool initDone = false;
-    std::thread watch([&] {
-      std::unique_lock<std::mutex> lk(mu);
-      if (!cv.wait_for(lk, std::chrono::duration<double>(topt_.waitTimeout), [&] { return initDone; }))
-        LOG_ERROR("RCCL communicator creation still running after " << topt_.waitTimeout << " s; plan:\n"
-                                                                      << plan_summary());
-    });
+    // non-blocking creation polled against the wait timeout: a member that never joins (a rank died or stalled
+    // between the bcast and here) costs every other member the timeout and an abort of its communicators, after which
+    // the failure is agreed on below like any other -- never a hang inside RCCL
     std::vector<int> ranks, devices, slots;
     for (int k = 0; k < nLocal; ++k) {
       const int nr = ncclRankOf[size_t(myRank) * size_t(maxN) + size_t(k)];
@@ -239,18 +244,19 @@ void DistributedDomain::init_rccl(const std::function<bool(int, int)> &sharedDev
       slots.push_back(k);
     }
     std::vector<rccl::Comm> comms;
-    why = rccl::init_ranks(&comms, total, boot.id, ranks, devices);
+    const double t0 = now_s();
+    why = rccl::init_ranks(&comms, total, boot.id, ranks, devices, topt_.waitTimeout,
+                           topt_.stallRcclInitRank == myRank);
     for (size_t j = 0; j < slots.size(); ++j) I.devs[size_t(slots[j])].nccl = comms[j];
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      initDone = true;
-    }
-    cv.notify_all();
-    watch.join();
     ok = why.empty();
+    if (!ok)
+      LOG_ERROR("RCCL communicator creation failed after " << now_s() - t0 << " s (" << why << "); plan:\n"
+                                                           << plan_summary());
   }
   if (!ok) LOG_WARN("rank " << myRank << ": RCCL unavailable (" << why << ")");
-  if (pg.allreduce_min_i64(ok) == 1) {
+  const bool allOk = pg.allreduce_min_i64(ok) == 1;
+  rcclStatus_ = allOk ? "ok" : (ok ? "failed on another rank" : why);
+  if (allOk) {
     // translate remote (rank, device) into RCCL ranks
     for (auto &c : I.chans) {
       if (c.method != MethodFlags::Rccl) continue;
@@ -701,7 +707,7 @@ void DistributedDomain::realize() {
     for (const auto &t : localTranslates) {
       const LocalDomain &s = domains_[std::get<0>(t)], &d = domains_[std::get<1>(t)];
       DevCtx &ctx = I.devs[I.devIndex[s.gpu()]];
-      const bool lines = I.xLineDevs.count(s.gpu()) > 0;
+      const bool lines = x_face_lines(s, d);
       for (int p = 0; p < 2; ++p) build_translate(s, d, std::get<2>(t), p == 0, ctx.translate.host[p], lines);
       if (d.gpu() != s.gpu()) I.devs[I.devIndex[d.gpu()]].peerWriters.insert(s.gpu());
     }

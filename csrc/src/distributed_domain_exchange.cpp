@@ -175,6 +175,54 @@ void DistributedDomain::set_transport_options_live(const TransportOptions &o) {
   topt_.fakeRemoteAxes = o.fakeRemoteAxes;
 }
 
+void retire_ipc_events(Channel &c, uint64_t epoch, hipStream_t s) {
+  for (auto &r : c.ipcRetired)
+    if (!r.fence && epoch >= r.fenceEpoch) {
+      HIP_CHECK(hipEventCreateWithFlags(&r.fence, hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(r.fence, s));
+    }
+  while (!c.ipcRetired.empty() && c.ipcRetired.front().fence) {
+    const hipError_t q = hipEventQuery(c.ipcRetired.front().fence);
+    if (q == hipErrorNotReady) {
+      (void)hipGetLastError();
+      break;
+    }
+    HIP_CHECK(q);
+    (void)hipEventDestroy(c.ipcRetired.front().fence);
+    (void)hipEventDestroy(c.ipcRetired.front().event);
+    c.ipcRetired.pop_front();
+  }
+}
+
+// Completion::IpcEvent: the receivers' Acks of the last two exchanges are consumed by no later record. Take them, so
+// that neither a switch back to IpcEvent nor another IpcEvent domain on the same group (same channel tags) finds a
+// stale Ack queued. timeout_s > 0: poll, give up after that long (teardown); else blocking receives.
+bool DistributedDomain::drain_ipc_acks(double timeout_s) {
+  Impl &I = *impl_;
+  if (!realized_ || backend_ != Backend::Device || topt_.completion != TransportOptions::Completion::IpcEvent)
+    return true;
+  const double t0 = now_s();
+  for (auto &ctx : I.devs)
+    for (int ci : ctx.coloSend) {
+      Channel &ch = I.chans[size_t(ci)];
+      for (uint64_t e = I.epoch >= 1 ? I.epoch - 1 : 0; e <= I.epoch; ++e) {
+        if (e == 0 || e < I.ipcEventFirstEpoch) continue;
+        uint64_t acked = 0;
+        const uint32_t tag = retag(ch.tag, comm::MsgKind::Ack);
+        if (timeout_s > 0) {
+          while (!pg_->try_recv(ch.remoteRank, tag, &acked, sizeof(acked))) {
+            if (now_s() - t0 > timeout_s) return false;
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+          }
+        } else {
+          pg_->recv(ch.remoteRank, tag, &acked, sizeof(acked));
+        }
+        STENCIL_REQUIRE(acked == e, "IPC-event ack out of order: got epoch " << acked << ", want " << e);
+      }
+    }
+  return true;
+}
+
 void DistributedDomain::set_completion(TransportOptions::Completion c) {
   if (c == topt_.completion) return;
   STENCIL_REQUIRE(!realized_ || c != TransportOptions::Completion::IpcEvent || impl_->ipcEvents ||
@@ -182,20 +230,7 @@ void DistributedDomain::set_completion(TransportOptions::Completion c) {
                   "Completion::IpcEvent needs its interprocess events: realize() with that completion");
   if (realized_) sync_exchange(); // flag words are monotonic epochs: either method continues where the other left off
   Impl &I = *impl_;
-  if (realized_ && topt_.completion == TransportOptions::Completion::IpcEvent && backend_ == Backend::Device) {
-    // leaving IpcEvent: take the acknowledgements of the last two exchanges that no later record will consume, so a
-    // later switch back finds no stale Ack queued
-    for (auto &ctx : I.devs)
-      for (int ci : ctx.coloSend) {
-        Channel &ch = I.chans[size_t(ci)];
-        for (uint64_t e = I.epoch >= 1 ? I.epoch - 1 : 0; e <= I.epoch; ++e) {
-          if (e == 0 || e < I.ipcEventFirstEpoch) continue;
-          uint64_t acked = 0;
-          pg_->recv(ch.remoteRank, retag(ch.tag, comm::MsgKind::Ack), &acked, sizeof(acked));
-          STENCIL_REQUIRE(acked == e, "IPC-event ack out of order: got epoch " << acked << ", want " << e);
-        }
-      }
-  }
+  drain_ipc_acks(0); // leaving IpcEvent: no stale Ack for a later switch back
   topt_.completion = c;
   // every rank switches between the same two exchanges: acknowledgements exist from the next epoch on
   if (c == TransportOptions::Completion::IpcEvent) I.ipcEventFirstEpoch = I.epoch + 1;
@@ -278,7 +313,7 @@ void DistributedDomain::prepare_skip_wrapped(int axes) {
     if (((axes & 1) && dir.x != 0) || ((axes & 2) && dir.y != 0) || ((axes & 4) && dir.z != 0)) continue;
     const LocalDomain &sd = domains_[std::get<0>(t)], &dd = domains_[std::get<1>(t)];
     DevCtx &ctx = I.devs[I.devIndex[sd.gpu()]];
-    for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p], I.xLineDevs.count(sd.gpu()) > 0);
+    for (int p = 0; p < 2; ++p) build_translate(sd, dd, dir, p == 0, ctx.translateSkip.host[p], x_face_lines(sd, dd));
   }
   for (auto &ctx : I.devs) ctx.translateSkip.upload(ctx.dev);
   // PeerCopy pipes: the same subset, packed compactly
@@ -594,7 +629,7 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       } else {
         fa.wait = credits;
         fa.waitTarget = I.epoch - 2;
-        if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords;
+        if (ctx.xlog && !capturing) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords;
         ctx.coloPack.run_device_sync(cv, S(ctx), commBlocks_, fa);
       }
       for (int ci : ctx.coloSend) {
@@ -608,16 +643,13 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
         IpcNotify msg;
         msg.epoch = I.epoch;
         if (c.ipcUses >= kIpcEventUses) { // a fresh event before HIP's per-event record limit
-          c.ipcRetired.emplace_back(c.ipcEvent, I.epoch);
+          c.ipcRetired.push_back({c.ipcEvent, I.epoch + 1, nullptr});
           HIP_CHECK(hipEventCreateWithFlags(&c.ipcEvent, hipEventDisableTiming | hipEventInterprocess));
           HIP_CHECK(hipIpcGetEventHandle(&msg.handle, c.ipcEvent));
           msg.fresh = 1;
           c.ipcUses = 0;
         }
-        while (!c.ipcRetired.empty() && I.epoch - c.ipcRetired.front().second >= kIpcRetireEpochs) {
-          (void)hipEventDestroy(c.ipcRetired.front().first);
-          c.ipcRetired.pop_front();
-        }
+        retire_ipc_events(c, I.epoch, S(ctx));
         HIP_CHECK(hipEventRecord(c.ipcEvent, S(ctx)));
         ++c.ipcUses;
         pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::Notify), &msg, sizeof(msg));
@@ -639,7 +671,7 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       fa.code = 1;
       fa.timeout_s = topt_.waitTimeout;
       fa.sharedGpu = ctx.sharedGpu;
-      if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords;
+      if (ctx.xlog && !capturing) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords;
       ctx.coloPack.run_device_sync(cv, S(ctx), commBlocks_, fa);
       continue;
     }
@@ -672,7 +704,10 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       for (int ci : ctx.rcclRecv)
         RCCL_CHECK(rccl::recv(I.chans[ci].dbuf, size_t(I.chans[ci].bytes), I.chans[ci].ncclPeer, ctx.nccl, S(ctx)));
     }
-    RCCL_CHECK(rccl::group_end());
+    std::vector<rccl::Comm> comms;
+    for (auto &ctx : I.devs)
+      if (ctx.nccl) comms.push_back(ctx.nccl);
+    RCCL_CHECK(rccl::group_end(comms, topt_.waitTimeout));
     for (auto &ctx : I.devs) {
       if (ctx.rcclRecv.empty()) continue;
       HIP_CHECK(hipSetDevice(ctx.dev));
@@ -732,13 +767,10 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
         STENCIL_REQUIRE(msg.epoch == I.epoch,
                         "IPC-event notify out of order: got epoch " << msg.epoch << ", want " << I.epoch);
         if (msg.fresh) { // the sender replaced its event: open the new one, keep the old until no wait needs it
-          c.ipcRetired.emplace_back(c.ipcEvent, I.epoch);
+          c.ipcRetired.push_back({c.ipcEvent, I.epoch, nullptr});
           HIP_CHECK(hipIpcOpenEventHandle(&c.ipcEvent, msg.handle));
         }
-        while (!c.ipcRetired.empty() && I.epoch - c.ipcRetired.front().second >= kIpcRetireEpochs) {
-          (void)hipEventDestroy(c.ipcRetired.front().first);
-          c.ipcRetired.pop_front();
-        }
+        retire_ipc_events(c, I.epoch, S(ctx));
         HIP_CHECK(hipStreamWaitEvent(S(ctx), c.ipcEvent, 0));
         const uint64_t e = I.epoch;
         pg.send(c.remoteRank, retag(c.tag, comm::MsgKind::Ack), &e, sizeof(e));
@@ -751,7 +783,7 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       fa.code = 2;
       fa.timeout_s = topt_.waitTimeout;
       fa.sharedGpu = ctx.sharedGpu;
-      if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords + 4;
+      if (ctx.xlog && !capturing) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords + 4;
       ctx.coloUnpack.run_device_sync(cv, S(ctx), commBlocks_, fa);
       continue;
     }
@@ -769,7 +801,7 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
       fa.code = 2;
       fa.timeout_s = topt_.waitTimeout;
       fa.sharedGpu = ctx.sharedGpu;
-      if (ctx.xlog) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords + 4;
+      if (ctx.xlog && !capturing) fa.stamps = ctx.xlog + ((I.epoch - 1) % uint64_t(I.xlogCap)) * kTransportLogWords + 4;
       ctx.coloUnpack.run_device_sync(cv, S(ctx), commBlocks_, fa);
       continue;
     }

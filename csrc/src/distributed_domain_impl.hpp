@@ -105,7 +105,18 @@ struct Channel {
   // the records / waits it has served, and replaced events kept until no wait can still reference them
   hipEvent_t ipcEvent = nullptr;
   int ipcUses = 0;
-  std::deque<std::pair<hipEvent_t, uint64_t>> ipcRetired; // (event, epoch it was replaced at)
+  // replaced events, destroyed by DEVICE progress: once the exchange of epoch `fenceEpoch` has been
+  // enqueued, an ordinary event `fence` is recorded on the comm stream behind it; the old event is destroyed when
+  // `fence` has completed (hipEventQuery), or at teardown after the streams are synchronized. Sender: fenceEpoch =
+  // replacement + 1, i.e. behind the pack kernel whose credit wait proves the receiver finished the unpack that
+  // followed its last wait on the old event. Receiver: fenceEpoch = replacement (every wait on the old event is
+  // already enqueued on this stream).
+  struct RetiredEvent {
+    hipEvent_t event = nullptr;
+    uint64_t fenceEpoch = 0;
+    hipEvent_t fence = nullptr;
+  };
+  std::deque<RetiredEvent> ipcRetired;
 };
 
 // HIP (ROCm 7.2) refuses hipStreamWaitEvent on an opened interprocess event after 32 records of it ("invalid
@@ -117,8 +128,8 @@ struct IpcNotify {
   uint64_t fresh = 0; // 1: `handle` is the channel's new event from this epoch on
   hipIpcEventHandle_t handle{};
 };
-// a replaced event is destroyed once this many more exchanges have passed (at most two are ever in flight)
-constexpr uint64_t kIpcRetireEpochs = 8;
+// fence and destroy the replaced events of channel c whose fence epoch has been reached (see Channel::ipcRetired)
+void retire_ipc_events(Channel &c, uint64_t epoch, hipStream_t s);
 
 // PeerCopy over a DMA engine (TransportOptions::peerCopy == Engine): every message from one local sub-domain to
 // another (on a peer GPU of this process) is packed into sbuf on the source GPU, copied by hipMemcpyPeerAsync into

@@ -1,0 +1,69 @@
+"""bench.py's control flow on the host backend (--cpu, BASELINE config 1's CPU path): the headline JSON line is
+printed BEFORE the transport sweep and again with the sweep (so a transport hanging on real links cannot cost the
+headline), a sweep that never returns is abandoned by the deadline with exit 0 behind the headline, and at N > 1 the
+warm-up times every transport candidate and keeps the fastest."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+ARGS = ["--cpu", "--per-gpu", "16", "--steps", "4", "--warmup", "1", "--exchange-iters", "3", "--tune-steps", "2"]
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "STENCIL_BENCH_DRY")}
+    env["STENCIL_PLAN_FILE"] = "0"
+    env["OMP_NUM_THREADS"] = "1"
+    env.update(kw)
+    return env
+
+
+def _lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_headline_printed_before_and_after_sweep():
+    r = subprocess.run([sys.executable, BENCH, *ARGS, "--transport-sweep", "on"], env=_env(), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _lines(r.stdout)
+    assert len(lines) == 2
+    first, second = lines
+    assert first["extra"]["transports"] == "pending"
+    assert isinstance(second["extra"]["transports"], dict) and "staged" in second["extra"]["transports"]
+    assert first["value"] == second["value"] and first["ms_per_step"] == second["ms_per_step"]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in first
+    # the sweep's first line was flushed before the sweep started
+    assert r.stdout.index('"pending"') < r.stdout.rindex('"transports": {')
+
+
+def test_hung_sweep_is_abandoned_behind_the_headline():
+    r = subprocess.run([sys.executable, BENCH, *ARGS, "--transport-sweep", "on", "--sweep-deadline", "3"],
+                       env=_env(STENCIL_BENCH_SWEEP_HANG="1"), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _lines(r.stdout)
+    assert len(lines) == 1 and lines[0]["extra"]["transports"] == "pending"
+    assert "abandoning it" in r.stderr
+
+
+def test_two_ranks_transport_chosen_by_measurement():
+    r = subprocess.run([sys.executable, BENCH, *ARGS, "--gpus", "2"], env=_env(), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _lines(r.stdout)
+    assert len(lines) == 2  # N > 1: the sweep runs by default
+    tt = lines[-1]["config"]["transport_tuned"]
+    assert set(tt) == {"colo_uncached", "colo_fine", "colo_coarse", "rccl", "chosen"}
+    timed = {k: v["ms"] for k, v in tt.items() if k != "chosen"}
+    assert tt["chosen"] == min(timed, key=timed.get)
+    tr = lines[-1]["extra"]["transports"]
+    assert {"staged", "ref_rule", "astaroth_q8", "peer_store"} <= set(tr)
+    assert tr["peer_store"]["devices_used"] >= 1
+    assert tr["astaroth_q8"]["halo_bytes"] > tr["ref_rule"]["halo_bytes"]
+    assert lines[-1]["n_gpus"] == 2 and lines[-1]["config"]["decomposition"] == "1x1x2"
