@@ -293,6 +293,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("default_group", &comm::default_group, py::call_guard<py::gil_scoped_release>());
   m.def("set_default_group", &comm::set_default_group);
   m.def("find_free_port", &comm::find_free_port);
+  // a one-wave kernel that busy-waits `seconds` on `stream` (tests: hold a stream while host work runs ahead of it)
+  m.def(
+      "spin_device", [](double seconds, uintptr_t stream) { spin_device(seconds, reinterpret_cast<hipStream_t>(stream)); },
+      py::arg("seconds"), py::arg("stream") = 0);
   m.def("set_copy_block_items", &set_copy_block_items, py::arg("narrow"), py::arg("wide"));
   m.def("set_copy_small_rows", &set_copy_small_rows, py::arg("max_items"), py::arg("per_entry"));
   m.def("ipc_event_stress", &ipc_event_stress, py::arg("group"), py::arg("device"), py::arg("n"), py::arg("after"),

@@ -321,6 +321,46 @@ def scenario_streamloop(size):
     return bad
 
 
+def scenario_ipcseq(size):
+    """ADVICE r4: two Completion::IpcEvent domains built one after the other on ONE process group (same channel tags:
+    the first one's undrained Acks would reach the second), and in the second one more than 40 stream-ordered
+    exchanges enqueued behind a long spin of the comm stream, so the host runs far ahead of the device while the
+    sender replaces its event (every 24 records) -- replaced events must outlive the queued records / waits."""
+    g = st.init_process_group()
+    r = st.Radius.constant(0)
+    r.set_face(2)
+    bad = 0
+    from stencil2_amd import _C
+    for k in range(2):
+        t = transport_from_env()
+        t.completion = st.TransportOptions.Completion.IpcEvent
+        dd = st.DistributedDomain(*size, group=g)
+        dd.set_transport_options(t)
+        dd.set_radius(r)
+        dd.set_gpus([0])
+        dd.set_methods(st.MethodFlags.Colocated | st.MethodFlags.Kernel)
+        q = dd.add_data("c", torch.int64)
+        dd.realize()
+        for it in range(3):
+            fill_coords(dd, q, offset=100 * k + it)
+            dd.exchange()
+            bad += check_exchange(dd, q, r, offset=100 * k + it)
+            dd.swap()
+        if k == 1:
+            fill_coords(dd, q, offset=7)
+            _C.spin_device(1.0, dd.comm_stream(0))
+            n = int(os.environ.get("MP_ITERS", "48"))
+            for it in range(n):  # an even number: the field is back in the buffer fill_coords wrote
+                dd.exchange_async(0, 0)
+                dd.swap()
+            dd.sync_exchange()
+            bad += check_exchange(dd, q, r, offset=7)
+        print(f"rank {g.rank()} ipcseq domain {k} bad {bad}", flush=True)
+        del dd
+    print(f"rank {g.rank()} ipcseq bad {bad}", flush=True)
+    return bad
+
+
 def main():
     # a stalled rank dumps every thread's Python stack (its C++ frames show as the native call it is in) so a hang
     # names its rank, scenario and phase; repeated, in case the first dump lands before the stall
@@ -343,6 +383,8 @@ def main():
         bad = scenario_streamloop(tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "ipcstress":
         bad = scenario_ipcstress()
+    elif sc == "ipcseq":
+        bad = scenario_ipcseq(tuple(int(v) for v in sys.argv[2].split(",")))
     elif sc == "ipcevent":
         bad = scenario_ipcevent()
     elif sc == "jacobi":

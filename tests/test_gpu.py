@@ -667,6 +667,16 @@ def test_colocated_caller_stream_two_ranks(completion, iters):
         assert "streamloop bad 0" in out, out[-2000:]
 
 
+def test_ipc_event_domains_in_sequence_and_host_run_ahead():
+    """Acks drained at teardown (a second IpcEvent domain on the same group starts clean) and replaced
+    interprocess events retired by device progress (48 stream-ordered exchanges behind a 1-s spin of the stream)"""
+    outs = run_ranks(2, WORKER, ["ipcseq", "64,48,80"],
+                     env_extra={"MP_DEVICE": "1", "STENCIL_WAIT_TIMEOUT": "20"}, timeout=100)
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "ipcseq bad 0" in out, out[-2000:]
+
+
 def test_colocated_completion_switching_two_ranks():
     """set_completion between exchanges: interprocess events (realized with them) -> spin kernels -> events again
     (30 exchanges: past the event replacement) -> stream ops -> events -> kernels; coordinate oracle throughout"""
