@@ -50,6 +50,12 @@ struct StencilTune {
   // z lookahead (1/2/3). 12 waves get 3 waves/SIMD and up to 168 VGPRs (no spills at any lookahead, fp32 or fp64);
   // one MI355X, 512^3, bench.py: 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s
   int x2nw = 12, x2pf = 1; // one plane of lookahead: best for the whole-row kernel once its edge waves skip u1/u2
+  int x3pf = 1;            // fused triples (stencil7x3): planes of z lookahead (1/2)
+  // fused triples: staggered levels (u1 / u2 / u3 of a step one plane apart and independent, so their row updates
+  // interleave) instead of the chained u1 -> u2 -> u3 of one z position per step
+  bool x3stagger = false;
+  int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
+  bool x3permute = false; // fused triples: waves -> rows permuted (SIMD-balanced under either wave->SIMD deal): -3 %
   // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells
   // long; x-neighbours and the wrap by DPP lane rotates, stencil7x2_row_kernel), or 512-cell columns (x a whole
   // number of 512-cell columns: two 16-B chunks per lane, only the column ends from outside the wave,
@@ -157,6 +163,12 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
 bool stencil7x2_supported(const LocalDomain &dom, int64_t qi);
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune = StencilTune());
+// Three fused steps: dst = S(S(S(src))) on the whole compute region of a fp32 sub-domain of 512-cell rows whose
+// every axis wraps in-kernel (tune.wrap == 7: one GPU, no halo read at all), bitwise equal to three single steps.
+// Returns false (nothing launched) when this layout / region / tune is not supported.
+bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune);
+bool stencil7x3_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
+                      hipStream_t stream, const StencilTune &tune);
 // S o S on several small regions (the exterior slabs of an overlapped fused pair), one thread per cell
 void stencil7x2_apply_regions(const LocalDomain &dom, int64_t qi, const std::vector<Rect3> &regions, StencilKind kind,
                               const Spheres &sph, hipStream_t stream, int wrap = 0);

@@ -88,6 +88,10 @@ public:
   // graph (one launch instead of kGraphSteps: the GPU-side gap between graph launches is ~9 us on MI355X).
   void run(int iters);
   static constexpr int kGraphSteps = 16; // even: the block starts and ends on the same buffer parity
+  // fused triples: 6 sweeps of 3 steps per block (an even number of sweeps keeps the buffer parity)
+  static constexpr int kGraphStepsTriple = 18;
+  int graph_steps() const { return triples_ ? kGraphStepsTriple : kGraphSteps; }
+  int steps_per_sweep() const { return triples_ ? 3 : (pairs_ ? 2 : 1); }
   void synchronize();           // wait for all enqueued work (and check exchange errors)
   void prepare();               // instantiate run()'s hipGraph blocks for both buffer parities (no work is run)
   DistributedDomain &domain() { return *dd_; }
@@ -119,6 +123,8 @@ public:
   bool local_interior_steps() const { return localSteps_; } // overlapped single steps on get_local_interior
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }
+  // three steps per sweep (stencil7x3_row_kernel): temporal >= 3, one device, every axis wrapped in-kernel
+  bool temporal_triples() const { return triples_; }
   int wrap_axes() const { return pairTune_.wrap; } // axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
   int step_wrap_axes() const { return stepTune_.wrap; } // same for single steps (stencil7_apply)
 
@@ -135,6 +141,7 @@ private:
   bool graphs_ = false;
   bool forward_ = false;
   bool pairs_ = false; // temporal blocking active
+  bool triples_ = false; // ... by three steps per sweep (run() then uses pairs / single steps only for remainders)
   bool overlapToggle_ = false;
   bool slabsAfter_ = false; // overlap mode 2 (see set_overlap_mode)
   bool pipeOk_ = false;      // overlap mode 3 possible (see init)

@@ -727,6 +727,10 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("alternate_z", &StencilTune::alternateZ)
       .def_readwrite("nw", &StencilTune::nw)
       .def_readwrite("x2pf", &StencilTune::x2pf)
+      .def_readwrite("x3pf", &StencilTune::x3pf)
+      .def_readwrite("x3stagger", &StencilTune::x3stagger)
+      .def_readwrite("x3sched", &StencilTune::x3sched)
+      .def_readwrite("x3permute", &StencilTune::x3permute)
       .def_readwrite("x2nw", &StencilTune::x2nw)
       .def_readwrite("x2row", &StencilTune::x2row)
       .def_readwrite("x2sched", &StencilTune::x2sched)
@@ -795,6 +799,7 @@ PYBIND11_MODULE(_C, m) {
       .def("local_interior_steps", &StencilModel::local_interior_steps)
       .def("forwarding", &StencilModel::forwarding)
       .def("temporal_blocking", &StencilModel::temporal_blocking)
+      .def("temporal_triples", &StencilModel::temporal_triples)
       .def("wrap_axes", &StencilModel::wrap_axes)
       .def("step_wrap_axes", &StencilModel::step_wrap_axes)
       .def("compute_stream", [](StencilModel &mdl, size_t di) { return reinterpret_cast<uintptr_t>(mdl.compute_stream(di)); })

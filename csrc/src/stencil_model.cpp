@@ -230,6 +230,19 @@ void StencilModel::init() {
   }
   // overlapped pairs with the slabs after the interior sweep (set_overlap_mode(2)) from the start
   slabsAfter_ = pairs_ && overlap_ && cfg_.overlapMode == 2;
+  // fused triples: one device, every axis wrapped in-kernel (nothing is exchanged), whole region, the spheres at
+  // least 3 cells from the periodic faces (the intermediate steps evaluate them at unwrapped halo coordinates)
+  triples_ = pairs_ && cfg_.temporal >= 3 && !overlap_ && doms0.size() == 1 && pairTune_.wrap == 7;
+  if (triples_ && sph_.enabled) {
+    const Dim3 L = cfg_.size;
+    for (const Dim3 &c : {sph_.hot, sph_.cold}) {
+      const int64_t cc[3] = {c.x, c.y, c.z}, ll[3] = {L.x, L.y, L.z};
+      for (int a = 0; a < 3; ++a)
+        if (cc[a] - sph_.radius < 2 || cc[a] + sph_.radius > ll[a] - 3) triples_ = false;
+    }
+  }
+  for (int64_t q = 0; triples_ && q < doms0[0].num_data(); ++q)
+    triples_ = stencil7x3_supported(doms0[0], q, doms0[0].get_compute_region(), pairTune_);
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
@@ -300,19 +313,27 @@ void StencilModel::step() {
 void StencilModel::run(int iters) {
   TraceRange tr("StencilModel::run");
   auto &doms = dd_->domains();
-  const int per = pairs_ ? 2 : 1; // steps per enqueued sweep
-  const int sweeps = kGraphSteps / per;  // sweeps per graph block (an even number: the block keeps the parity)
-  while (graphs_ && iters >= kGraphSteps) {
+  const int per = steps_per_sweep(), gsteps = graph_steps();
+  const int sweeps = gsteps / per; // sweeps per graph block (an even number: the block keeps the parity)
+  while (graphs_ && iters >= gsteps) {
     const int p = doms[0].parity();
     hipStream_t s = compute_[0].get();
     if (!graphBlock_[p]) capture_block();
     for (int k = 0; k < sweeps; ++k) dd_->swap();
     HIP_CHECK(hipGraphLaunch(graphBlock_[p], s));
-    steps_ += kGraphSteps;
-    iters -= kGraphSteps;
+    steps_ += gsteps;
+    iters -= gsteps;
   }
   const bool device = !compute_.empty();
   const bool singleStream = device && !overlap_ && doms.size() == 1;
+  while (triples_ && iters >= 3) {
+    enqueue_step(3);
+    dd_->swap();
+    if (device && !singleStream)
+      for (size_t di = 0; di < doms.size(); ++di) dd_->record_ready(di, compute_[di]);
+    steps_ += 3;
+    iters -= 3;
+  }
   while (pairs_ && iters >= 2) {
     enqueue_step(2);
     dd_->swap();
@@ -328,7 +349,7 @@ void StencilModel::capture_block() {
   // records kGraphSteps steps starting at the current buffer parity into graphBlock_[parity]; nothing runs, and
   // the swaps done while recording are undone (an even number of sweeps returns to the same parity anyway)
   auto &doms = dd_->domains();
-  const int per = pairs_ ? 2 : 1, sweeps = kGraphSteps / per;
+  const int per = steps_per_sweep(), sweeps = graph_steps() / per;
   const int p = doms[0].parity();
   hipStream_t s = compute_[0].get();
   hipGraph_t g = nullptr;
@@ -412,6 +433,19 @@ void StencilModel::enqueue_step(int k) {
       exteriorDone_[di].record(s);
       exteriorDone_[di].wait_on(compute_[di]);
     }
+    return;
+  }
+  if (k == 3) {
+    // fused triples: every halo is read in-kernel at its periodic image, so the exchange has nothing left to copy
+    // (it still orders the step like the pairs' one); then S o S o S of the whole region
+    const bool single = device && doms.size() == 1;
+    dd_->exchange_async(single ? compute_[0].get() : nullptr, pairTune_.wrap);
+    hipStream_t s = device ? compute_[0].get() : nullptr;
+    if (!single) dd_->wait_exchange(0, s);
+    StencilTune ti = pairTune_;
+    for (int64_t q = 0; q < doms[0].num_data(); ++q)
+      STENCIL_REQUIRE(stencil7x3_apply(doms[0], q, doms[0].get_compute_region(), cfg_.kind, sph_, s, ti),
+                      "fused triple not supported for quantity " << q);
     return;
   }
   if (k == 2) {

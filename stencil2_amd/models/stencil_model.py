@@ -128,6 +128,10 @@ class StencilModel:
         """True when run() advances in fused pairs of steps (stencil7x2, one depth-2 exchange per pair)."""
         return self._m.temporal_blocking()
 
+    def temporal_triples(self) -> bool:
+        """True when run() advances in fused triples of steps (stencil7x3, temporal=3 on one fully periodic GPU)."""
+        return self._m.temporal_triples()
+
     def wrap_axes(self) -> int:
         """Axes (mask 1=x, 2=y, 4=z) the fused pairs read periodically in-kernel instead of from copied halos."""
         return self._m.wrap_axes()

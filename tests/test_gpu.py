@@ -223,6 +223,40 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
+@pytest.mark.parametrize("stagger", [False, True])
+@pytest.mark.parametrize("kind,size,pf", [("jacobi", (512, 120, 116), 1), ("jacobi", (512, 128, 120), 2),
+                                           ("jacobi", (512, 512, 112), 1), ("astaroth", (512, 36, 28), 1),
+                                           ("astaroth", (512, 13, 17), 2), ("astaroth", (512, 3, 16), 1)])
+def test_temporal3_matches_three_single_steps(st, kind, size, pf, stagger):
+    """Fused triples (stencil7x3_row_kernel, temporal=3, one GPU, every axis wrapped in-kernel): S(S(S(u))) bitwise
+    equal to three single steps of the torch oracle; run(n) covers whole hipGraph blocks (18 steps), triples and the
+    pair / single-step remainders; y extents that are not a multiple of the block's 6 output rows and a 3-row grid
+    (every block row wraps onto itself twice)."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    t = st.StencilTune()
+    t.x3pf = pf
+    t.x3stagger = stagger
+    m = cls(size, gpus=[0], temporal=3, tune=t, **kw)
+    m.init()
+    assert m.temporal_triples() and m.wrap_axes() == 7
+    m.prepare()
+    u = torch.rand((size[2], size[1], size[0]), device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+    for q in range(kw.get("quantities", 1)):
+        m.interior(0, q).copy_(u)
+    torch.cuda.synchronize()
+    for n in (3, 7, 2, 20, 1):
+        m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        m.synchronize()
+        for q in range(kw.get("quantities", 1)):
+            got = m.interior(0, q)
+            bad = int((got != u).sum())
+            assert bad == 0, f"run({n}) q{q}: {bad} cells differ, max {(got - u).abs().max().item()}"
+
+
 @pytest.mark.parametrize("kind,size,gpus,pf,row", [
     *[(k, sz, g, pf, 1) for k, sz, g in [("jacobi", (512, 120, 116), [0]), ("jacobi", (512, 300, 112), [0, 0]),
                                          ("astaroth", (512, 36, 28), [0]), ("astaroth", (512, 520, 40), [0, 0, 0, 0])]
