@@ -233,6 +233,7 @@ def transport_sweep(st, env, args, world, rank, device, ndev, axis_cost, objecti
                 dd.set_plan_file("")
                 dd.set_x_halo_align(bool(args.x_halo_align))
                 dd.set_interior_align(args.interior_align)
+                dd.set_shared_halo_line(args.shared_halo_line == 1)
                 topt = st.TransportOptions()
                 topt.inbox = topt_base.inbox
                 topt.completion = o.get("completion", topt_base.completion)
@@ -393,9 +394,11 @@ def build_args(argv=None):
     ap.add_argument("--zchunk", type=int, default=0, help="z planes per block (0 = auto)")
     ap.add_argument("--x2sched", type=int, default=1,
                     help="fused-pair work split: 1 = balanced segments over the resident blocks, 0 = fixed z-chunks")
-    ap.add_argument("--temporal", type=int, default=2,
-                    help="steps fused per sweep: 2 = temporal blocking (one depth-2 halo exchange + one fused "
-                         "S(S(u)) sweep per two steps, bitwise equal to single steps), 1 = one exchange + sweep per step")
+    ap.add_argument("--temporal", type=int, default=3,
+                    help="steps fused per sweep: 3 = fused triples S(S(S(u))) where every axis wraps in-kernel (one GPU, "
+                         "512-cell fp32 rows: the driver's command 1334-1349 vs 1270-1296 Gcells/s with pairs, "
+                         "profiles/r5/g; elsewhere pairs), 2 = temporal blocking (one depth-2 halo exchange + one fused "
+                         "S(S(u)) sweep per two steps), 1 = one exchange + sweep per step; all bitwise equal to single steps")
     ap.add_argument("--x2xfast", type=int, default=0, help="fused-pair column order: 1 x-major, 0 y-major")
     ap.add_argument("--wrap", type=int, default=1,
                     help="fused pairs read the periodic image along axes the decomposition leaves whole (no self-copy "
@@ -407,6 +410,11 @@ def build_args(argv=None):
     ap.add_argument("--x-halo-align", type=int, default=0,
                     help="x halos inside the interior's first / last 64-B sector (LocalDomain::set_x_halo_align): "
                          "one sector per row end for x-face copies; every row spans one more sector")
+    ap.add_argument("--shared-halo-line", type=int, default=-1,
+                    help="17-line row pitch at 512^3: row r's +x and row r+1's -x halo share one 128-B line, written once "
+                         "per row by the x-face self copies (LocalDomain::set_shared_halo_line). -1 (auto): on for the "
+                         "with-exchange model, whose sweeps read the x-halo lines (967 -> 1027 Gcells/s, "
+                         "profiles/r5/f), off for the headline (wrapped sweeps: no change; exchange-only -1 %%)")
     ap.add_argument("--x-face-lines", type=int, default=0,
                     help="same-GPU x-face copies as whole 128-B lines (TransportOptions.x_face_sectors)")
     ap.add_argument("--interior-align", type=int, default=128, choices=[64, 128],
@@ -570,12 +578,13 @@ def main(argv=None):
     # and checked cell by cell on every rank; any wrong halo or error drops Colocated, then Rccl (host-staged), so a
     # scaling run never times silently corrupted halos. An RCCL communicator that fails to form (or never forms:
     # bounded non-blocking creation) falls back to the host-staged path on every rank as well.
-    def build(topt, meth, wrap_self=None):
+    def build(topt, meth, wrap_self=None, shared=None):
         model = st.Jacobi3D(grid, gpus=[device], methods=meth, overlap=overlap, auto_overlap=args.overlap == "auto",
                             tune=tune, temporal=args.temporal, group=pg, axis_cost=axis_cost, partition=objective,
                             wrap_self=bool(args.wrap) if wrap_self is None else wrap_self, transport=topt,
                             self_test=bool(args.self_test) and world > 1, x_halo_align=bool(args.x_halo_align),
-                            interior_align=args.interior_align, backend=st.Backend.Host if args.cpu else None)
+                            interior_align=args.interior_align, backend=st.Backend.Host if args.cpu else None,
+                            shared_halo_line=bool(args.shared_halo_line == 1 if shared is None else shared))
         model.init()
         model.prepare()  # hipGraph capture + instantiation (no steps run) outside the timed region
         model.run(args.warmup)
@@ -730,7 +739,7 @@ def main(argv=None):
         "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
         "transport_tuned": transport_tuned,
         "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
-        "x_face_lines": bool(args.x_face_lines),
+        "x_face_lines": bool(args.x_face_lines), "shared_halo_line": args.shared_halo_line == 1,
         "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
         "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x3pf": args.x3pf, "x3stagger": args.x3stagger, "x3sched": args.x3sched, "x3permute": args.x3permute, "x2row": args.x2row, "x2sched": args.x2sched,
         "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": 3 if model.temporal_triples() else (2 if model.temporal_blocking() else 1),
@@ -747,7 +756,7 @@ def main(argv=None):
     # steps with every halo copied -- the intra-GPU pack/unpack (same-GPU copy-plan kernel) plus the compute kernels
     with_x = None
     if args.with_exchange == "on" or (args.with_exchange == "auto" and wrap_axes != "none"):
-        m2 = build(topt, methods, wrap_self=False)
+        m2 = build(topt, methods, wrap_self=False, shared=args.shared_halo_line != 0)
         if model_cfg["overlap_tuned"] is not None and m2.can_toggle_overlap():
             m2.set_overlap_mode(overlap_tuned["mode"])
             m2.set_comm_reserve(overlap_tuned["reserve"])
@@ -761,6 +770,7 @@ def main(argv=None):
         el = env.agreed_max(time.perf_counter() - t)
         with_x = {"gcells": round(cells * args.steps / el / 1e9, 3), "ms_per_step": round(el / args.steps * 1e3, 4),
                   "wrap_axes": "".join(c for i, c in enumerate("xyz") if m2.wrap_axes() >> i & 1) or "none",
+                  "shared_halo_line": bool(m2.domain.domain(0).shared_halo_line()),
                   "halo_bytes_per_exchange": int(m2.domain.exchange_bytes_for_method(st.MethodFlags.All))}
         release(m2)
 

@@ -13,6 +13,7 @@ using namespace stencil;
 struct MethodArgs {
   bool staged = false, rccl = false, colo = false, peer = false, kernel = false, trivial = false;
   int interiorAlign = 128; // bytes; the row-start alignment of every interior (LocalDomain::set_interior_align)
+  bool sharedHaloLine = false; // LocalDomain::set_shared_halo_line
   bool xFaceLines = false; // TransportOptions::xFaceSectors: same-GPU x faces copied as whole lines
   int xFaceLinesAutoMiB = 128; // TransportOptions::xFaceLinesAutoBytes in MiB (0 = never by themselves)
   void add(ArgParser &p) {
@@ -23,6 +24,7 @@ struct MethodArgs {
         .flag(&kernel, "--kernel", "same-GPU kernel transport")
         .flag(&trivial, "--trivial,--naive", "trivial placement")
         .option(&interiorAlign, "--interior-align", "interior row alignment in bytes (64 or 128)")
+        .flag(&sharedHaloLine, "--shared-halo-line", "row r's +x and row r+1's -x halo in one 128-B line")
         .flag(&xFaceLines, "--x-face-lines", "same-GPU x faces copied as whole 128-B lines")
         .option(&xFaceLinesAutoMiB, "--x-face-lines-auto", "MiB of x-face lines from which whole lines switch on (0 never)");
   }

@@ -13,13 +13,17 @@ using namespace stencil;
 int main(int argc, char **argv) {
   int64_t x = 512, y = 512, z = 512;
   int iters = 5, nq = 8, temporal = 1;
-  bool noOverlap = false, weak = false, fp64 = false, noWrap = false;
+  bool noOverlap = false, weak = false, fp64 = false, noWrap = false, forceOverlap = false;
+  int reserve = -1;
   app::MethodArgs ma;
   ArgParser p("Astaroth proxy (reference bin/astaroth_sim.cu)");
   p.option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z").option(&iters, "-n,--iters", "iterations")
       .option(&nq, "--q", "quantities")
       .option(&temporal, "--temporal", "steps fused per sweep (1 or 2)")
       .flag(&noOverlap, "--no-overlap", "no overlap")
+      .flag(&forceOverlap, "--overlap", "overlap the interior sweep with the exchange even when every halo is a "
+                                        "same-GPU copy (one GPU, --no-wrap: the reference's iteration)")
+      .option(&reserve, "--reserve", "CUs the overlapped sweep leaves to the exchange kernels (default 8)")
       .flag(&noWrap, "--no-wrap", "exchange every periodic self-halo each sweep (the reference's per-iteration "
                                   "exchange, bin/astaroth_sim.cu:223-274) instead of reading the periodic image")
       .flag(&weak, "--weak", "treat x,y,z as per-GPU sizes").flag(&fp64, "--fp64", "fp64 quantities");
@@ -42,8 +46,11 @@ int main(int argc, char **argv) {
   cfg.methods = ma.flags();
   cfg.placement = ma.placement();
   cfg.interiorAlign = ma.interiorAlign;
+  cfg.sharedHaloLine = ma.sharedHaloLine;
   cfg.transport = ma.transport(cfg.transport);
   cfg.overlap = !noOverlap;
+  cfg.autoOverlap = !forceOverlap;
+  if (reserve >= 0) cfg.tune.x2reserve = reserve;
   cfg.wrapSelf = !noWrap;
   StencilModel m(cfg, pg);
   m.init();

@@ -22,6 +22,7 @@ static std::pair<Statistics, uint64_t> bench(comm::ProcGroup &pg, int iters, int
   dd.set_placement(pl);
   dd.set_x_halo_align(xHaloAlign);
   dd.set_interior_align(ma.interiorAlign);
+  dd.set_shared_halo_line(ma.sharedHaloLine);
   dd.set_transport_options(ma.transport());
   for (int i = 0; i < nq; ++i) dd.add_data<float>("d" + std::to_string(i));
   dd.realize();

@@ -31,6 +31,7 @@ int main(int argc, char **argv) {
   dd.set_methods(ma.flags());
   dd.set_placement(ma.placement());
   dd.set_interior_align(ma.interiorAlign);
+  dd.set_shared_halo_line(ma.sharedHaloLine);
   dd.set_transport_options(ma.transport());
   for (int i = 0; i < nq; ++i) {
     if (fp64)

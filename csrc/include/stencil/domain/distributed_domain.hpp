@@ -215,6 +215,9 @@ public:
   // halo-aligned x layout of every local domain (LocalDomain::set_x_halo_align)
   void set_x_halo_align(bool on) { xHaloAlign_ = on; }
   bool x_halo_align() const { return xHaloAlign_; }
+  // shared halo lines of every local domain (LocalDomain::set_shared_halo_line)
+  void set_shared_halo_line(bool on) { sharedHaloLine_ = on; }
+  bool shared_halo_line() const { return sharedHaloLine_; }
   // LocalDomain::set_interior_align of every local domain (128 B default, or 64)
   void set_interior_align(int64_t bytes) { interiorAlign_ = bytes; }
   int64_t interior_align() const { return interiorAlign_; }
@@ -313,6 +316,10 @@ public:
   // sweep costs the pair ~80 us unconfined (its blocks land on CUs the sweep's blocks then wait for) and ~25 us
   // confined to 8 CUs beside a sweep that leaves 8 free.
   void set_comm_max_blocks(int n) { commBlocks_ = n; }
+  // the same confinement for the same-device translate (the Kernel method's copy plan): an overlapped single step whose
+  // every halo is a same-GPU copy (one GPU, config 4) runs the translate on n CUs beside an interior sweep that leaves
+  // n CUs free (0 = the whole GPU, the default)
+  void set_translate_max_blocks(int n) { translateBlocks_ = n; }
   // Producer gate for the next exchange_async on the comm stream (pipelined pairs): instead of waiting for the
   // producer's whole kernel (record_ready), the fused co-located pack kernel polls *counter >= target, a word the
   // still-running stencil sweep raises once the boundary planes the exchange reads are written
@@ -363,11 +370,13 @@ private:
   Dim3 axisCost_{1, 1, 1};
   PartitionObjective objective_ = PartitionObjective::Interface;
   int commBlocks_ = 0;
+  int translateBlocks_ = 0;
   Backend backend_ = Backend::Device;
   bool backendSet_ = false;
   bool realized_ = false;
   bool pad_ = true;
   bool xHaloAlign_ = false;
+  bool sharedHaloLine_ = false;
   int64_t interiorAlign_ = 128;
   int rowPadLines_ = 0;
   TransportOptions topt_;

@@ -78,6 +78,14 @@ public:
   void set_row_pad_lines(int n) { rowPadLines_ = n; }
   int row_pad_lines() const { return rowPadLines_; }
   bool x_halo_align() const { return xHaloAlign_; }
+  // shared halo lines: the row pitch is the raw row rounded up to whole interior-alignment units
+  // (512^3 fp32 radius 2: 17 lines of 128 B instead of 18), so row r's +x halo and row r+1's -x halo sit in ONE line
+  // -- the line between row r's last and row r+1's first interior line. A row's raw cells then reach into the next
+  // row's front padding (never into its raw cells); x-face self copies write each shared line from one item (both
+  // halos: make_copy_plan pairs them), i.e. one written line per row instead of two. Needs the padded layout, the
+  // interior on an alignment unit and x halos that fit one unit together; ignored with the halo-aligned x layout.
+  void set_shared_halo_line(bool on) { sharedLine_ = on; }
+  bool shared_halo_line() const { return sharedLine_ && sharedActive_; }
   void realize();
   bool realized() const { return realized_; }
 
@@ -105,6 +113,10 @@ public:
   // elements in front of raw x = 0 that a kernel may read (ignoring the values) without leaving the allocation:
   // the row padding, plus the guard before the first row (halo-aligned layout)
   int64_t front_slack(int64_t qi) const { return padX_.at(size_t(qi)) + guard_ / elem_size(qi); }
+  // raw x (exclusive, from a row's raw x = 0) up to which a kernel may READ in any row without leaving the allocation
+  // (values beyond the row's raw cells are ignored): the end of the row's own pitch block, and with shared halo
+  // lines the end of the next row's front padding (the last row of a buffer has an allocated tail for it)
+  int64_t row_limit(int64_t qi) const { return pitchX_.at(size_t(qi)) - (shared_halo_line() ? 0 : padX_.at(size_t(qi))); }
   // bytes of one curr (or next) buffer of quantity qi
   int64_t buffer_bytes(int64_t qi) const;
 
@@ -164,6 +176,7 @@ private:
   Backend backend_;
   bool pad_ = true;
   bool xHaloAlign_ = false;
+  bool sharedLine_ = false, sharedActive_ = false;
   int64_t interiorAlign_ = 128;
   int rowPadLines_ = 0;
   int64_t guard_ = 0; // bytes before the first row of every buffer (halo-aligned layout)
@@ -173,6 +186,7 @@ private:
   std::vector<DType> dtype_;
   std::vector<std::string> names_;
   std::vector<int64_t> pitchX_, padX_;
+  std::vector<int64_t> tailX_; // elements allocated after the last pitch block (shared halo lines)
   std::vector<void *> base_[2]; // allocations
   std::vector<void *> curr_, next_;
   void free_all();

@@ -67,6 +67,7 @@ struct StencilModelConfig {
   // halo-aligned x layout (DistributedDomain::set_x_halo_align): x halos share the interior's first / last 64-B
   // sector (x-face copies touch one sector per row end instead of two; every row spans one more sector)
   bool xHaloAlign = false;
+  bool sharedHaloLine = false; // DistributedDomain::set_shared_halo_line
   int64_t interiorAlign = 128; // DistributedDomain::set_interior_align (128 B default, or 64)
   int rowPadLines = 0;          // DistributedDomain::set_row_pad_lines (measurement knob)
   TransportOptions transport; // DistributedDomain::set_transport_options
@@ -141,7 +142,8 @@ private:
   bool graphs_ = false;
   bool forward_ = false;
   bool pairs_ = false; // temporal blocking active
-  bool triples_ = false; // ... by three steps per sweep (run() then uses pairs / single steps only for remainders)
+  bool triples_ = false;
+  bool confinedSelf_ = false; // overlapped single steps with only same-GPU halos: translate on x2reserve CUs // ... by three steps per sweep (run() then uses pairs / single steps only for remainders)
   bool overlapToggle_ = false;
   bool slabsAfter_ = false; // overlap mode 2 (see set_overlap_mode)
   bool pipeOk_ = false;      // overlap mode 3 possible (see init)

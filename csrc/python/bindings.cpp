@@ -437,6 +437,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_radius", py::overload_cast<const Radius &>(&LocalDomain::set_radius))
       .def("set_padding", &LocalDomain::set_padding)
       .def("set_x_halo_align", &LocalDomain::set_x_halo_align)
+      .def("set_shared_halo_line", &LocalDomain::set_shared_halo_line)
+      .def("shared_halo_line", &LocalDomain::shared_halo_line)
+      .def("row_limit", &LocalDomain::row_limit)
       .def("x_halo_align", &LocalDomain::x_halo_align)
       .def("set_interior_align", &LocalDomain::set_interior_align)
       .def("set_row_pad_lines", &LocalDomain::set_row_pad_lines)
@@ -596,6 +599,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_plan_file", &DistributedDomain::set_plan_file)
       .def("set_padding", &DistributedDomain::set_padding)
       .def("set_x_halo_align", &DistributedDomain::set_x_halo_align)
+      .def("set_shared_halo_line", &DistributedDomain::set_shared_halo_line)
+      .def("shared_halo_line", &DistributedDomain::shared_halo_line)
       .def("x_halo_align", &DistributedDomain::x_halo_align)
       .def("set_interior_align", &DistributedDomain::set_interior_align)
       .def("set_row_pad_lines", &DistributedDomain::set_row_pad_lines)
@@ -759,6 +764,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("temporal", &StencilModelConfig::temporal)
       .def_readwrite("wrap_self", &StencilModelConfig::wrapSelf)
       .def_readwrite("x_halo_align", &StencilModelConfig::xHaloAlign)
+      .def_readwrite("shared_halo_line", &StencilModelConfig::sharedHaloLine)
       .def_readwrite("interior_align", &StencilModelConfig::interiorAlign)
       .def_readwrite("row_pad_lines", &StencilModelConfig::rowPadLines)
       .def_readwrite("wrap_axes_mask", &StencilModelConfig::wrapAxesMask)

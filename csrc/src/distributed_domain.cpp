@@ -388,6 +388,7 @@ void DistributedDomain::realize() {
     d.set_radius(radius_);
     d.set_padding(pad_);
     d.set_x_halo_align(xHaloAlign_);
+    d.set_shared_halo_line(sharedHaloLine_);
     d.set_interior_align(interiorAlign_);
     d.set_row_pad_lines(rowPadLines_);
     for (size_t q = 0; q < elemSize_.size(); ++q) d.add_data(elemSize_[q], names_[q], dtypes_[q]);

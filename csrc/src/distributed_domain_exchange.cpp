@@ -554,7 +554,7 @@ void DistributedDomain::exchange_async(hipStream_t stream, int skipAxes) {
     TraceRange t("kernel/peer translate");
     const SegList &tl = skipAxes != 0 ? ctx.translateSkip : ctx.translate;
     ctx.translateEmpty = tl.host[parity].empty();
-    if (!ctx.translateEmpty) tl.run_device(parity, S(ctx));
+    if (!ctx.translateEmpty) tl.run_device(parity, S(ctx), translateBlocks_);
     if (!over) ctx.translated.record(S(ctx)); // events only matter across streams
   }
 

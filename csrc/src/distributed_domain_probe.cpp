@@ -53,6 +53,7 @@ int64_t DistributedDomain::probe_transports(MethodFlags m) {
     p.set_transport_options(topt_);
     p.set_plan_file("");
     p.set_x_halo_align(xHaloAlign_);
+    p.set_shared_halo_line(sharedHaloLine_);
     p.set_interior_align(interiorAlign_);
     p.add_data(4, "probe", DType::I32);
     try {

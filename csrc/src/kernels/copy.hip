@@ -212,21 +212,35 @@ static std::vector<CopySeg> pair_narrow_segs(const std::vector<CopySeg> &in) {
   auto narrow = [](const CopySeg &s) {
     return s.units && s.row_units <= kNarrowMaxUnits && !s.src2 && !(s.flags & kSegWide);
   };
-  for (size_t i = 0; i < in.size(); ++i) {
-    if (used[i]) continue;
-    CopySeg a = in[i];
-    if (narrow(a))
+  auto compatible = [&](const CopySeg &a, const CopySeg &b) {
+    return narrow(b) && b.vec == a.vec && b.row_units == a.row_units && b.ny == a.ny && b.units == a.units &&
+           b.src_ystride == a.src_ystride && b.src_zstride == a.src_zstride && b.dst_ystride == a.dst_ystride &&
+           b.dst_zstride == a.dst_zstride;
+  };
+  // first choice: a partner whose rows write the same 128-B line (shared halo lines: row y's +x halo and row y+1's
+  // -x halo), so the line is written once, by one item
+  auto sameLine = [](const CopySeg &a, const CopySeg &b) {
+    return uintptr_t(a.dst) / 128 == uintptr_t(b.dst) / 128 && uintptr_t(a.dst) + a.row_units * a.vec <= uintptr_t(b.dst) + 128;
+  };
+  std::vector<long> partner(in.size(), -1);
+  for (int pass = 0; pass < 2; ++pass)
+    for (size_t i = 0; i < in.size(); ++i) {
+      if (used[i] || !narrow(in[i])) continue;
       for (size_t j = i + 1; j < in.size(); ++j) {
-        const CopySeg &b = in[j];
-        if (used[j] || !narrow(b) || b.vec != a.vec || b.row_units != a.row_units || b.ny != a.ny ||
-            b.units != a.units || b.src_ystride != a.src_ystride || b.src_zstride != a.src_zstride ||
-            b.dst_ystride != a.dst_ystride || b.dst_zstride != a.dst_zstride)
-          continue;
-        a.src2 = b.src;
-        a.dst2 = b.dst;
-        used[j] = true;
+        if (used[j] || !compatible(in[i], in[j]) || (pass == 0 && !sameLine(in[i], in[j]))) continue;
+        partner[i] = long(j);
+        used[i] = used[j] = true;
         break;
       }
+    }
+  // emitted in the input order (the dispatch order of the work table matters for speed, profiles/r4/ad)
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (used[i] && partner[i] < 0) continue; // the second half of a pair
+    CopySeg a = in[i];
+    if (partner[i] >= 0) {
+      a.src2 = in[size_t(partner[i])].src;
+      a.dst2 = in[size_t(partner[i])].dst;
+    }
     out.push_back(a);
   }
   return out;

@@ -914,7 +914,7 @@ static void apply_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, con
   const bool alignedLayout = (reinterpret_cast<uintptr_t>(a.src + a.x0) % 16 == 0) &&
                              (reinterpret_cast<uintptr_t>(a.dst + a.x0) % 16 == 0) && ((a.px * int64_t(sizeof(T))) % 16 == 0);
   // vector loads and the right-edge neighbour stay inside the padded row (LocalDomain keeps >= V+1 tail elements)
-  const bool fits = a.x0 + int64_t(a.nchunks) * V < a.px - dom.pad_x(qi);
+  const bool fits = a.x0 + int64_t(a.nchunks) * V < dom.row_limit(qi);
   dom.set_device();
   STENCIL_REQUIRE(!fwd || (alignedLayout && fits), "halo forwarding needs the aligned vector layout");
   if (tune.wrap != 0) {
@@ -987,7 +987,7 @@ int stencil7_wrappable_axes(const LocalDomain &dom, int64_t qi) {
   const bool aligned = (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + lox * es) % 16 == 0) &&
                        (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + lox * es) % 16 == 0) &&
                        (p.x * es) % 16 == 0;
-  if (!aligned || lox + (nx + V - 1) / V * V >= p.x - dom.pad_x(qi)) return 0;
+  if (!aligned || lox + (nx + V - 1) / V * V >= dom.row_limit(qi)) return 0;
   // x: whole chunks (the last chunk's right edge is the face); y / z: one conditional shift per access
   return (nx % V == 0 ? 1 : 0) | 2 | 4;
 }
@@ -1147,7 +1147,7 @@ bool HaloForwarder::supported(const LocalDomain &dom, int64_t qi) {
   const bool aligned = (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + x0 * es) % 16 == 0) &&
                        (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + x0 * es) % 16 == 0) &&
                        (p.x * es) % 16 == 0;
-  return aligned && x0 + nchunks * V < p.x - dom.pad_x(qi);
+  return aligned && x0 + nchunks * V < dom.row_limit(qi);
 }
 
 HaloForwarder::HaloForwarder(const LocalDomain &src, int64_t qi, const std::vector<ForwardTarget> &targets) {

@@ -1117,23 +1117,22 @@ bool stencil7x2_supported(const LocalDomain &dom, int64_t qi) {
                        (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + lox * es) % 16 == 0) &&
                        (p.x * es) % 16 == 0;
   // the edge lanes read x-2 and x+V+1 of their chunk: stay inside the padded row
-  return aligned && lox - 2 + dom.front_slack(qi) >= 0 && lox + nchunks * V + 1 < p.x - dom.pad_x(qi);
+  return aligned && lox - 2 + dom.front_slack(qi) >= 0 && lox + nchunks * V + 1 < dom.row_limit(qi);
 }
 
 int stencil7x2_wrappable_axes(const LocalDomain &dom, int64_t qi, int x2row) {
   if (!stencil7x2_supported(dom, qi)) return 0;
   const int64_t es = dom.elem_size(qi), V = 16 / es;
-  const int64_t lox = dom.radius().x(-1), nx = dom.size().x, px = dom.pitch(qi).x, pad = dom.pad_x(qi),
-                slack = dom.front_slack(qi);
+  const int64_t lox = dom.radius().x(-1), nx = dom.size().x, lim = dom.row_limit(qi), slack = dom.front_slack(qi);
   // ragged fp32 rows of 257-832 cells: the whole-row kernel wraps x by broadcasting the row-end cells (a ragged last
   // chunk reads at most 3 cells past the row end, inside the padded row; rows of 769-832 end in per-lane tail cells)
-  const bool rowX = x2row != 0 && es == 4 && nx > 256 && nx <= 832 && lox + (nx + V - 1) / V * V < px - pad;
+  const bool rowX = x2row != 0 && es == 4 && nx > 256 && nx <= 832 && lox + (nx + V - 1) / V * V < lim;
   if (rowX && nx % V != 0) return 1 | (dom.size().y >= 2 ? 2 : 0) | (dom.size().z >= 2 ? 4 : 0);
   // x: whole chunks only (the chunk grid starts at the 16-B aligned lox), at least two, and the last chunk not on
   // lane 0 of its column (a wrap lane shifts both of its edge pairs: its other edge must be the unused one, never a
   // column boundary); the unused edge pair of a wrap lane (x-2 .. x+V+1 shifted by +-nx) must stay in the row
   const bool x = nx % V == 0 && nx >= 2 * V && (nx / V) % 64 != 1 && lox - V - 2 + slack >= 0 &&
-                 lox + nx + V + 1 < px - pad;
+                 lox + nx + V + 1 < lim;
   // y / z: one conditional shift maps the 2 cells beyond a face onto the grid
   return (x ? 1 : 0) | (dom.size().y >= 2 ? 2 : 0) | (dom.size().z >= 2 ? 4 : 0);
 }

@@ -2,6 +2,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -15,8 +16,8 @@ LocalDomain::LocalDomain(const Dim3 &sz, const Dim3 &origin, int dev, Backend ba
 
 LocalDomain::LocalDomain(LocalDomain &&o) noexcept
     : sz_(o.sz_), origin_(o.origin_), radius_(o.radius_), dev_(o.dev_), backend_(o.backend_), pad_(o.pad_),
-      xHaloAlign_(o.xHaloAlign_), interiorAlign_(o.interiorAlign_), rowPadLines_(o.rowPadLines_), guard_(o.guard_), realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
-      names_(std::move(o.names_)), pitchX_(std::move(o.pitchX_)), padX_(std::move(o.padX_)),
+      xHaloAlign_(o.xHaloAlign_), sharedLine_(o.sharedLine_), sharedActive_(o.sharedActive_), interiorAlign_(o.interiorAlign_), rowPadLines_(o.rowPadLines_), guard_(o.guard_), realized_(o.realized_), parity_(o.parity_), elemSize_(std::move(o.elemSize_)), dtype_(std::move(o.dtype_)),
+      names_(std::move(o.names_)), pitchX_(std::move(o.pitchX_)), padX_(std::move(o.padX_)), tailX_(std::move(o.tailX_)),
       curr_(std::move(o.curr_)), next_(std::move(o.next_)) {
   base_[0] = std::move(o.base_[0]);
   base_[1] = std::move(o.base_[1]);
@@ -72,12 +73,30 @@ void LocalDomain::realize() {
   const int64_t nq = num_data();
   pitchX_.assign(size_t(nq), raw.x);
   padX_.assign(size_t(nq), 0);
+  tailX_.assign(size_t(nq), 0);
   int64_t total = 0;
   const int64_t rxm = radius_.x(-1), rxp = radius_.x(1);
   const bool haloAligned = xHaloAlign_ && pad_;
   guard_ = haloAligned ? 128 : 0;
+  // shared halo lines: every quantity's interior on an alignment unit and both x halos within one unit
+  sharedActive_ = sharedLine_ && pad_ && !haloAligned;
+  for (int64_t q = 0; q < nq && sharedActive_; ++q) {
+    const int64_t es = elemSize_[q];
+    sharedActive_ = interiorAlign_ % es == 0 && (rxm + rxp) * es <= interiorAlign_ && (128 % es == 0);
+  }
   for (int64_t q = 0; q < nq; ++q) {
     const int64_t es = elemSize_[q];
+    if (sharedActive_) {
+      const int64_t perLine = interiorAlign_ / es, rowAlign = 128 / es;
+      padX_[q] = (perLine - (rxm % perLine)) % perLine;
+      // row r's raw end (padX + raw.x) stays within row r+1's front padding: raw.x <= pitch; the interior start
+      // (padX + rxm) is on a unit in every row since the pitch is a multiple of the unit
+      pitchX_[q] = round_up(std::max(raw.x, int64_t(1)), std::max(perLine, rowAlign));
+      const int64_t tail = (16 % es == 0) ? 16 / es + 1 : 1;
+      tailX_[q] = padX_[q] + tail + rowAlign; // the last row's halo + vector over-reads stay allocated
+      total += 2 * (buffer_bytes(q) + tailX_[q] * es);
+      continue;
+    }
     if (pad_ && interiorAlign_ % es == 0) {
       const int64_t perLine = interiorAlign_ / es; // elements per interior alignment unit (64 or 128 B)
       if (haloAligned && 16 % es == 0 && rxm * es <= kMaxAlignedHaloBytes && rxp * es <= kMaxAlignedHaloBytes) {
@@ -106,7 +125,7 @@ void LocalDomain::realize() {
   curr_.assign(size_t(nq), nullptr);
   next_.assign(size_t(nq), nullptr);
   for (int64_t q = 0; q < nq; ++q) {
-    const int64_t bytes = buffer_bytes(q) + guard_;
+    const int64_t bytes = buffer_bytes(q) + guard_ + tailX_[q] * elemSize_[q];
     for (int b = 0; b < 2; ++b) {
       void *p = nullptr;
       if (backend_ == Backend::Device) {
@@ -206,7 +225,7 @@ void LocalDomain::region_from_host(const Dim3 &pos, const Dim3 &ext, int64_t qi,
 }
 
 void LocalDomain::fill_bytes(int64_t qi, uint8_t v, bool curr, bool next) {
-  const int64_t bytes = buffer_bytes(qi);
+  const int64_t bytes = buffer_bytes(qi) + tailX_.at(size_t(qi)) * elem_size(qi);
   for (int which = 0; which < 2; ++which) {
     if ((which == 0 && !curr) || (which == 1 && !next)) continue;
     char *p = static_cast<char *>(which == 0 ? curr_data(qi) : next_data(qi)) - padX_[qi] * elem_size(qi);

@@ -73,7 +73,9 @@ static bool widen_x_face(const LocalDomain &src, const LocalDomain &dst, const D
   if (dir.y != 0 || dir.z != 0 || dir.x == 0) return false;
   const int64_t es = src.elem_size(q);
   const int64_t unit = std::min(src.interior_align(), dst.interior_align());
-  if (es != dst.elem_size(q) || unit % es != 0 || src.x_halo_align() || dst.x_halo_align()) return false;
+  // shared halo lines: the unit behind / in front of a row holds the neighbour row's halo too -- never widen into it
+  if (es != dst.elem_size(q) || unit % es != 0 || src.x_halo_align() || dst.x_halo_align() || dst.shared_halo_line())
+    return false;
   const int64_t S = unit / es, w = ext->x;
   if (w > S || src.size().x % S || dst.size().x % S || src.size().x < S) return false;
   const int64_t srxm = src.radius().x(-1), drxm = dst.radius().x(-1);
@@ -102,6 +104,17 @@ void build_translate_segs_q(const LocalDomain &src, const LocalDomain &dst, cons
     sp = wsp;
     dp = wdp;
     ext = wext;
+  }
+  if (!wide && dst.shared_halo_line() && dir.x != 0 && dir.y == 0 && dir.z == 0 && ext.y > 1) {
+    // shared halo lines: row y's +x halo (written by the dir = -x translate) and row y+1's -x halo (dir = +x) are one
+    // line. Split off the row without a partner in this face (the last row of the +x halo column, the first of the
+    // -x one) so the remaining rows of the two faces have the same shape and make_copy_plan pairs them row by row:
+    // one item then writes both halos of a line (one written line per row instead of two)
+    const int64_t lone = dir.x < 0 ? ext.y - 1 : 0, first = dir.x < 0 ? 0 : 1;
+    const Dim3 e1(ext.x, ext.y - 1, ext.z), e2(ext.x, 1, ext.z);
+    out.push_back(make_copy_seg(src.box(q, curr, sp + Dim3(0, first, 0)), dst.box(q, curr, dp + Dim3(0, first, 0)), e1, es));
+    out.push_back(make_copy_seg(src.box(q, curr, sp + Dim3(0, lone, 0)), dst.box(q, curr, dp + Dim3(0, lone, 0)), e2, es));
+    return;
   }
   CopySeg sg = make_copy_seg(src.box(q, curr, sp), dst.box(q, curr, dp), ext, es);
   if (wide && sg.vec == 16) sg.flags |= kSegWide;

@@ -34,6 +34,7 @@ StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::
   if (cfg.setBackend) dd_->set_backend(cfg.backend);
   dd_->set_transport_options(cfg.transport);
   dd_->set_x_halo_align(cfg.xHaloAlign);
+  dd_->set_shared_halo_line(cfg.sharedHaloLine);
   dd_->set_interior_align(cfg.interiorAlign);
   dd_->set_row_pad_lines(cfg.rowPadLines);
   dd_->set_self_test(cfg.selfTest);
@@ -228,6 +229,12 @@ void StencilModel::init() {
     stepTune_.wrap = w;
     if (w != 0) dd_->prepare_skip_wrapped(w);
   }
+  // forced overlap of single steps whose every halo is a same-GPU copy (one GPU with --no-wrap: BASELINE config 4 as
+  // the reference runs it, bin/astaroth_sim.cu:223-274): the copy-plan translate runs confined to x2reserve CUs on
+  // the comm stream while the interior sweep leaves those CUs free, then the exterior slabs
+  confinedSelf_ = !pairs_ && !forward_ && overlap_ && !localSteps_ && stepDevice && cfg_.tune.x2reserve > 0 &&
+                  dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All);
+  if (confinedSelf_) dd_->set_translate_max_blocks(cfg_.tune.x2reserve);
   // overlapped pairs with the slabs after the interior sweep (set_overlap_mode(2)) from the start
   slabsAfter_ = pairs_ && overlap_ && cfg_.overlapMode == 2;
   // fused triples: one device, every axis wrapped in-kernel (nothing is exchanged), whole region, the spheres at
@@ -501,9 +508,11 @@ void StencilModel::enqueue_step(int k) {
   if (overlap_) {
     // exchange first: its pack/send kernels (high-priority comm stream) get CUs before the interior sweep fills them
     dd_->exchange_async();
+    StencilTune ti = cfg_.tune;
+    if (confinedSelf_) ti.reserveCUs = cfg_.tune.x2reserve;
     for (size_t di = 0; di < doms.size(); ++di)
       for (int64_t q = 0; q < doms[di].num_data(); ++q)
-        stencil7_apply(doms[di], q, interiors_[di], cfg_.kind, sph_, device ? compute_[di].get() : nullptr, cfg_.tune);
+        stencil7_apply(doms[di], q, interiors_[di], cfg_.kind, sph_, device ? compute_[di].get() : nullptr, ti);
     // The exterior slabs only need the halos, not the interior result: run them on the comm stream right behind
     // the exchange; the compute stream then joins the comm stream.
     for (size_t di = 0; di < doms.size(); ++di) {
@@ -554,6 +563,7 @@ void StencilModel::set_comm_reserve(int cus) {
   pairTune_.x2reserve = cus;
   stepTune_.x2reserve = cus;
   if (overlap_) dd_->set_comm_max_blocks(cus);
+  if (confinedSelf_) dd_->set_translate_max_blocks(cus);
 }
 
 void StencilModel::synchronize() {

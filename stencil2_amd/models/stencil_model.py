@@ -25,7 +25,7 @@ class StencilModel:
                  tune: _C.StencilTune | None = None, group=None, axis_cost=None, wrap_self: bool = True,
                  transport: _C.TransportOptions | None = None, wrap_axes_mask: int = 7, local_interior: bool = True,
                  overlap_mode: int = 1, self_test: bool = False, partition=None, x_halo_align: bool = False,
-                 interior_align: int = 128, row_pad_lines: int = 0):
+                 interior_align: int = 128, row_pad_lines: int = 0, shared_halo_line: bool = False):
         cfg = _C.StencilModelConfig()
         cfg.size = _C.Dim3(*size)
         cfg.kind = kind
@@ -50,6 +50,7 @@ class StencilModel:
         cfg.x_halo_align = x_halo_align  # x halos inside the interior's first / last 64-B sector
         cfg.interior_align = interior_align  # byte alignment of every row's first interior cell (128 or 64)
         cfg.row_pad_lines = row_pad_lines  # extra 128-B lines per row pitch (measurement knob)
+        cfg.shared_halo_line = shared_halo_line  # row r's +x and row r+1's -x halo in one 128-B line
         if transport is not None:  # DistributedDomain.set_transport_options (inbox memory, DMA copies, completion)
             cfg.transport = transport
         if backend is not None:

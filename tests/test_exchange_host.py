@@ -253,3 +253,53 @@ def test_exchange_x_halo_aligned_layout(st, name, dtype, gpus):
     fill_coords(dd, q)
     dd.exchange()
     assert check_exchange(dd, q, radius) == 0
+
+
+@pytest.mark.parametrize("name", ["r1", "r2", "+x2", "-x1", "+x2-x1", "fec", "mixed"])
+@pytest.mark.parametrize("gpus", [[0], [0, 0]])
+@pytest.mark.parametrize("dtype", [torch.int64, torch.float32])
+def test_exchange_shared_halo_lines(st, name, gpus, dtype):
+    """Shared halo lines (LocalDomain.set_shared_halo_line): the row pitch is the raw row rounded
+    up to whole 128-B lines, so row r's +x halo and row r+1's -x halo share a line and a row's raw cells reach into
+    the next row's front padding. Every halo still lands on its own cell (coordinate oracle, 3 exchanges with swaps),
+    the interiors stay line-aligned, and the pitch is one line shorter than the default layout's."""
+    radius = radius_patterns(st)[name]
+    size = (64, 11, 9)
+    dd = st.DistributedDomain(*size, group=st.make_single_group())
+    dd.set_backend(st.Backend.Host)
+    dd.set_radius(radius)
+    dd.set_gpus(gpus)
+    dd.set_shared_halo_line(True)
+    q = dd.add_data("q", dtype)
+    dd.realize()
+    ref, _ = make_dd(st, size, radius, gpus, dtype=dtype)
+    for di in range(dd.num_domains()):
+        d, r = dd.domain(di), ref.domain(di)
+        assert d.shared_halo_line()
+        es = torch.empty((), dtype=dtype).element_size()
+        assert d.pitch(0).x * es % 128 == 0 and (d.pad_x(0) + d.radius().x(-1)) * es % 128 == 0
+        assert d.raw_size().x <= d.pitch(0).x < d.raw_size().x + 128 // es
+        assert d.pitch(0).x <= r.pitch(0).x - (128 // es if d.radius().x(-1) and d.radius().x(1) else 0)
+        assert d.row_limit(0) == d.pitch(0).x
+    for it in range(3):
+        fill_coords(dd, q, offset=it)
+        dd.exchange()
+        assert check_exchange(dd, q, radius, offset=it) == 0
+        dd.swap()
+
+
+def test_shared_halo_line_translate_pairs_one_line(st):
+    """Depth-2 face self-exchange on a shared-halo-line domain: the x-face translates are split into the rows that
+    pair up line by line (row y's +x halo with row y+1's -x halo) and the one row per plane that has no partner in
+    its face; every halo cell still arrives."""
+    dd = st.DistributedDomain(64, 8, 4, group=st.make_single_group())
+    dd.set_backend(st.Backend.Host)
+    r = st.Radius.constant(0)
+    r.set_face(2)
+    dd.set_radius(r)
+    dd.set_shared_halo_line(True)
+    q = dd.add_data("q", torch.float32)
+    dd.realize()
+    fill_coords(dd, q)
+    dd.exchange()
+    assert check_exchange(dd, q, r) == 0

@@ -61,6 +61,83 @@ def test_device_exchange(st, method, gpus, rname):
         dd.swap()
 
 
+@pytest.mark.parametrize("method,gpus", [("Kernel", [0]), ("Kernel", [0, 0]), ("PeerCopy", [0, 0]),
+                                         ("PeerCopyEngine", [0, 0]), ("Rccl", [0, 0]), ("Staged", [0, 0])])
+@pytest.mark.parametrize("rname", ["r1", "r3", "asym", "fec"])
+def test_device_exchange_shared_halo_lines(st, method, gpus, rname):
+    """Shared halo lines (row r's +x and row r+1's -x halo in one 128-B line) on the device backend: every transport
+    against the coordinate oracle, fp32 and int64 rows long enough for whole lines."""
+    radius = _radii(st)[rname]
+    tr = st.TransportOptions()
+    if method == "PeerCopyEngine":
+        tr.peer_copy = st.TransportOptions.Copy.Engine
+        method = "PeerCopy"
+    for dtype in (torch.float32, torch.int64):
+        dd = st.DistributedDomain(96, 13, 11, group=st.make_single_group())
+        dd.set_backend(st.Backend.Device)
+        dd.set_transport_options(tr)
+        dd.set_radius(radius)
+        dd.set_gpus(gpus)
+        dd.set_methods(getattr(st.MethodFlags, method))
+        dd.set_shared_halo_line(True)
+        q = dd.add_data("c", dtype)
+        dd.realize()
+        assert all(dd.domain(i).shared_halo_line() for i in range(dd.num_domains()))
+        for it in range(2):
+            fill_coords(dd, q, offset=it)
+            dd.exchange()
+            assert check_exchange(dd, q, radius, offset=it) == 0
+            dd.swap()
+
+
+@pytest.mark.parametrize("kind,size,temporal", [("jacobi", (512, 120, 116), 2), ("jacobi", (512, 120, 116), 1),
+                                                ("astaroth", (512, 36, 28), 2), ("astaroth", (256, 24, 20), 1)])
+def test_shared_halo_lines_models_match_oracle(st, kind, size, temporal):
+    """Fused pairs / single steps on the shared-halo-line layout with every halo copied (wrap_self=False, config 2
+    as defined) and with in-kernel wrap: bitwise equal to the torch oracle."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    for wrap in (False, True):
+        m = cls(size, gpus=[0], temporal=temporal, wrap_self=wrap, shared_halo_line=True, **kw)
+        m.init()
+        assert m.domain.domain(0).shared_halo_line()
+        u = torch.rand((size[2], size[1], size[0]), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+        for q in range(kw.get("quantities", 1)):
+            m.interior(0, q).copy_(u)
+        torch.cuda.synchronize()
+        m.run(5)
+        for _ in range(5):
+            u = ref(u)
+        m.synchronize()
+        for q in range(kw.get("quantities", 1)):
+            assert torch.equal(m.interior(0, q), u), f"wrap_self={wrap} q{q}"
+
+
+@pytest.mark.parametrize("reserve", [8, 0, 32])
+def test_astaroth_forced_overlap_one_gpu(st, reserve):
+    """Config 4 as the reference iterates (bin/astaroth_sim.cu:223-274) on one GPU: interior sweep overlapped with
+    the same-GPU radius-3 exchange (the translate confined to `reserve` CUs the sweep leaves free; 0 = unconfined),
+    exterior slabs after; every halo copied (wrap_self=False). Bitwise equal to the oracle."""
+    from stencil2_amd.ops import astaroth_step_reference
+    t = st.StencilTune()
+    t.x2reserve = reserve
+    size = (64, 40, 36)
+    m = st.AstarothSim(size, quantities=2, gpus=[0], overlap=True, auto_overlap=False, wrap_self=False, tune=t)
+    m.init()
+    assert m.overlapping()
+    u = torch.rand((size[2], size[1], size[0]), device="cuda", generator=torch.Generator(device="cuda").manual_seed(9))
+    for q in range(2):
+        m.interior(0, q).copy_(u)
+    torch.cuda.synchronize()
+    m.run(4)
+    for _ in range(4):
+        u = astaroth_step_reference(u)
+    m.synchronize()
+    for q in range(2):
+        assert torch.equal(m.interior(0, q), u)
+
+
 def test_device_exchange_float_views(st):
     radius = st.Radius.constant(2)
     dd, q = _dd(st, (64, 32, 16), radius, [0], st.MethodFlags.All, dtype=torch.float32)
