@@ -95,7 +95,7 @@ def test_bench_alltoallv_and_measure_buf_exchange():
 
 
 def test_bench_py_json_contract():
-    """bench.py on one GPU prints one JSON line with the driver's fields (exact 512^3 grid, temporal pairs)."""
+    """bench.py on one GPU prints one JSON line with the driver's fields (exact 512^3 grid, fused triples)."""
     import json
     import sys
     env = dict(os.environ)
@@ -112,4 +112,4 @@ def test_bench_py_json_contract():
               "vs_baseline", "dtype", "data", "config"):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2 and d["value"] > 0
-    assert d["config"]["grid"] == [512, 512, 512] and d["config"]["temporal"] == 2
+    assert d["config"]["grid"] == [512, 512, 512] and d["config"]["temporal"] == 3
