@@ -382,11 +382,7 @@ def build_args(argv=None):
     ap.add_argument("--nw", type=int, default=8, help="waves per block of the stencil kernel")
     ap.add_argument("--x2nw", type=int, default=12, help="waves per block of the fused two-step kernel (8/12/16)")
     ap.add_argument("--x2pf", type=int, default=1, help="planes of z lookahead of the fused two-step kernel (1/2/3)")
-    ap.add_argument("--x3pf", type=int, default=1, help="planes of z lookahead of the fused three-step kernel (1/2)")
     ap.add_argument("--x3sched", type=int, default=1, help="fused three-step schedule (0: the pairs', 1: lockstep)")
-    ap.add_argument("--x3permute", type=int, default=0, help="fused three-step kernel: SIMD-balanced wave->row map")
-    ap.add_argument("--x3stagger", type=int, default=0,
-                    help="fused three-step kernel: staggered levels (independent row updates per z step)")
     ap.add_argument("--x2row", type=int, default=1,
                     help="fused pairs: one wave per whole 512-cell row when x wraps in-kernel (fp32); 0 = columns")
     ap.add_argument("--x2reserve", type=int, default=8,
@@ -562,10 +558,7 @@ def main(argv=None):
     tune.variant = args.variant
     tune.x2nw = args.x2nw
     tune.x2pf = args.x2pf
-    tune.x3pf = args.x3pf
-    tune.x3stagger = bool(args.x3stagger)
     tune.x3sched = args.x3sched
-    tune.x3permute = bool(args.x3permute)
     tune.x2row = args.x2row
     tune.zchunk = args.zchunk
     tune.x2reserve = args.x2reserve
@@ -741,7 +734,7 @@ def main(argv=None):
         "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
         "x_face_lines": bool(args.x_face_lines), "shared_halo_line": args.shared_halo_line == 1,
         "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
-        "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x3pf": args.x3pf, "x3stagger": args.x3stagger, "x3sched": args.x3sched, "x3permute": args.x3permute, "x2row": args.x2row, "x2sched": args.x2sched,
+        "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x3sched": args.x3sched, "x2row": args.x2row, "x2sched": args.x2sched,
         "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": 3 if model.temporal_triples() else (2 if model.temporal_blocking() else 1),
         "wrap_axes": wrap_axes, "backend": "host" if args.cpu else "device",
         "transport": {"inbox": str(dd.transport_options().inbox).split(".")[-1].lower(),

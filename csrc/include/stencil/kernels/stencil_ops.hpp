@@ -50,12 +50,7 @@ struct StencilTune {
   // z lookahead (1/2/3). 12 waves get 3 waves/SIMD and up to 168 VGPRs (no spills at any lookahead, fp32 or fp64);
   // one MI355X, 512^3, bench.py: 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s
   int x2nw = 12, x2pf = 1; // one plane of lookahead: best for the whole-row kernel once its edge waves skip u1/u2
-  int x3pf = 1;            // fused triples (stencil7x3): planes of z lookahead (1/2)
-  // fused triples: staggered levels (u1 / u2 / u3 of a step one plane apart and independent, so their row updates
-  // interleave) instead of the chained u1 -> u2 -> u3 of one z position per step
-  bool x3stagger = false;
   int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
-  bool x3permute = false; // fused triples: waves -> rows permuted (SIMD-balanced under either wave->SIMD deal): -3 %
   // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells
   // long; x-neighbours and the wrap by DPP lane rotates, stencil7x2_row_kernel), or 512-cell columns (x a whole
   // number of 512-cell columns: two 16-B chunks per lane, only the column ends from outside the wave,

@@ -732,10 +732,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("alternate_z", &StencilTune::alternateZ)
       .def_readwrite("nw", &StencilTune::nw)
       .def_readwrite("x2pf", &StencilTune::x2pf)
-      .def_readwrite("x3pf", &StencilTune::x3pf)
-      .def_readwrite("x3stagger", &StencilTune::x3stagger)
       .def_readwrite("x3sched", &StencilTune::x3sched)
-      .def_readwrite("x3permute", &StencilTune::x3permute)
       .def_readwrite("x2nw", &StencilTune::x2nw)
       .def_readwrite("x2row", &StencilTune::x2row)
       .def_readwrite("x2sched", &StencilTune::x2sched)

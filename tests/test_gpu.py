@@ -300,11 +300,11 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
-@pytest.mark.parametrize("stagger", [False, True])
-@pytest.mark.parametrize("kind,size,pf", [("jacobi", (512, 120, 116), 1), ("jacobi", (512, 128, 120), 2),
-                                           ("jacobi", (512, 512, 112), 1), ("astaroth", (512, 36, 28), 1),
-                                           ("astaroth", (512, 13, 17), 2), ("astaroth", (512, 3, 16), 1)])
-def test_temporal3_matches_three_single_steps(st, kind, size, pf, stagger):
+@pytest.mark.parametrize("sched", [0, 1])
+@pytest.mark.parametrize("kind,size", [("jacobi", (512, 120, 116)), ("jacobi", (512, 128, 120)),
+                                       ("jacobi", (512, 512, 112)), ("astaroth", (512, 36, 28)),
+                                       ("astaroth", (512, 13, 17)), ("astaroth", (512, 3, 16))])
+def test_temporal3_matches_three_single_steps(st, kind, size, sched):
     """Fused triples (stencil7x3_row_kernel, temporal=3, one GPU, every axis wrapped in-kernel): S(S(S(u))) bitwise
     equal to three single steps of the torch oracle; run(n) covers whole hipGraph blocks (18 steps), triples and the
     pair / single-step remainders; y extents that are not a multiple of the block's 6 output rows and a 3-row grid
@@ -313,8 +313,7 @@ def test_temporal3_matches_three_single_steps(st, kind, size, pf, stagger):
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
     t = st.StencilTune()
-    t.x3pf = pf
-    t.x3stagger = stagger
+    t.x3sched = sched
     m = cls(size, gpus=[0], temporal=3, tune=t, **kw)
     m.init()
     assert m.temporal_triples() and m.wrap_axes() == 7
