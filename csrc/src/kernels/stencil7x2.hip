@@ -403,6 +403,9 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   // Ragged three-chunk rows keep the per-cell test: with the bounds they ran 10 % slower (645x645x323 867-891 vs
   // 972 Gcells/s, same box; the 512-cell kernel with bounds 1047-1052 vs 1142-1157; profiles/r3/s3/ab_sphere.txt)
   const int w = TL ? __builtin_amdgcn_readfirstlane(int(threadIdx.y)) : int(threadIdx.y);
+  // raw buffer over the source field: row offsets from raw [0,0,0] are non-negative and the field is below 4 GiB
+  // (apply_x2row_t checks)
+  const __amdgpu_buffer_rsrc_t srcRsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.src), 0, -1, 0x00020000);
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
   // z-march direction alternates between neighbouring segments (their shared boundary planes meet in cache); in the
   // part-major lockstep order it alternates by part, so y-adjacent blocks march together
@@ -560,11 +563,16 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
     NV C[NC][H];
     NV Ub[H], Uc[H], Ua[H];
     T Ct[NC] = {}, Ubt = 0, Uct = 0, Uat = 0; // tail cells (TL)
+    // buffer loads: plane offset in an SGPR, row offset a per-segment VGPR. Recomputing a 64-bit VGPR address every
+    // step wrote registers of the slot's previous load, and the compiler then waited for every outstanding memory
+    // op (s_waitcnt vmcnt(0), the previous step's stores included) before issuing the step's loads
     auto load_row = [&](int zz, int k) {
-      const char *b = planep(zz) + rowoff;
+      const uint32_t po = uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
 #pragma unroll
-      for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + choff(h));
-      if constexpr (TL) Ct[k] = *reinterpret_cast<const T *>(b + toff);
+      for (int h = 0; h < H; ++h)
+        C[k][h] = __builtin_bit_cast(NV, __builtin_amdgcn_raw_buffer_load_b128(srcRsrc, rowoff + uint32_t(choff(h)), po, 0));
+      if constexpr (TL)
+        Ct[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(srcRsrc, rowoff + uint32_t(toff), po, 0));
     };
     {
       const int zw = z0 - 2 * dz;
@@ -1211,6 +1219,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   const int nx = a.hix - a.lox;
   const bool fitsH = TL ? (nx > 256 * H && nx <= 256 * H + 64) : (RAG ? (nx > 256 * (H - 1) && nx <= 256 * H) : nx == 512);
   if (!(tune.wrap & 1) || !fitsH || (a.lox - rxm) % 4 != 0) return false;
+  if (dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096) return false; // 32-bit buffer-load offsets
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
   a.wrapm = tune.wrap;
@@ -1327,7 +1336,8 @@ bool stencil7x2_row_kernel_used(const LocalDomain &dom, int64_t qi, const Rect3 
     return false;
   const Rect3 rr(region.lo - dom.accessor_origin(), region.hi - dom.accessor_origin());
   const int64_t nx = rr.hi.x - rr.lo.x;
-  return (nx == 512 || (nx > 256 && nx <= 832)) && (rr.lo.x - dom.radius().x(-1)) % 4 == 0;
+  return (nx == 512 || (nx > 256 && nx <= 832)) && (rr.lo.x - dom.radius().x(-1)) % 4 == 0 &&
+         dom.buffer_bytes(qi) < (int64_t(1) << 32) - 4096;
 }
 
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,

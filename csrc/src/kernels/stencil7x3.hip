@@ -87,6 +87,9 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
   const int xb = a.lox + lane * V; // chunk h at xb + h * HS
   const int zwn = a.wn[2], zwlo = a.wlo[2], zwhi = a.wlo[2] + a.wn[2];
+  // raw buffer over the source field (offsets from raw [0,0,0] are non-negative and below 4 GiB: checked by the host)
+  const __amdgpu_buffer_rsrc_t srcRsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.src), 0, -1, 0x00020000);
   auto zcl = [&](int zz) {
     zz += zz < zwlo ? zwn : 0;
     zz -= zz >= zwhi ? zwn : 0;
@@ -119,9 +122,7 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
         yw = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
         const uint32_t rowoff = uint32_t((yw * int64_t(a.px) + xb) * int64_t(sizeof(T)));
         const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
-        auto planep = [&](int zz) -> const char * {
-          return reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy);
-        };
+
         // spheres (Jacobi): the planes P of this row that cross the hot / cold sphere form two intervals
         // |P - c.z| <= h (h * h < r1sq - dy^2), computed once per segment; per-cell tests only on those planes
         struct RowSph {
@@ -213,10 +214,16 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
           NV C[NC][H];
           NV U1a[H], U1b[H], U1c[H]; // u1 at planes z+2dz (new), z, z+dz
           NV U2a[H], U2b[H], U2c[H]; // u2 at planes z+dz (new), z-dz, z
+          // buffer loads: the plane offset in an SGPR (soffset), the row offset a per-segment constant VGPR. With
+          // 64-bit VGPR addresses recomputed every step, the address write landed on registers of the slot's
+          // previous load and the compiler waited for every outstanding memory op (s_waitcnt vmcnt(0)) before each
+          // step's loads, the previous step's stores included
           auto load_row = [&](int zz, int k) {
-            const char *b = planep(zz) + rowoff;
+            const uint32_t po = uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
 #pragma unroll
-            for (int h = 0; h < H; ++h) C[k][h] = *reinterpret_cast<const NV *>(b + h * HS * int(sizeof(T)));
+            for (int h = 0; h < H; ++h)
+              C[k][h] = __builtin_bit_cast(
+                  NV, __builtin_amdgcn_raw_buffer_load_b128(srcRsrc, rowoff + uint32_t(h * HS * int(sizeof(T))), po, 0));
           };
           // step t = -4 starts with src planes z+dz .. z+(NC-1)dz, z = z0 - 4dz, and the src row of its u1 plane
           // (z+2dz: slot 1) published
@@ -286,16 +293,17 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
             // registers (the fast results stay live across the redo: 168 VGPRs + 21 spilled for Jacobi), so not used
             (void)levels(std::true_type{});
             if constexpr (LV >= 3) {
-              if (outRow) {
-                char *dp = reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff;
+              // unconditional: a row past the region's y end (the last row group) stores into a per-device sink, so
+              // every path has the same vector-memory ops and the next step's load wait counts past these stores
+              char *dp = outRow ? reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff
+                                : a.sink + lane * V * int(sizeof(T));
 #pragma unroll
-                for (int h = 0; h < H; ++h) {
-                  NV *q = reinterpret_cast<NV *>(dp + h * HS * int(sizeof(T)));
-                  if (a.nt)
-                    __builtin_nontemporal_store(o[h], q);
-                  else
-                    *q = o[h];
-                }
+              for (int h = 0; h < H; ++h) {
+                NV *q = reinterpret_cast<NV *>(dp + h * HS * int(sizeof(T)));
+                if (a.nt)
+                  __builtin_nontemporal_store(o[h], q);
+                else
+                  *q = o[h];
               }
             }
             const int nbuf = buf ^ 1;
@@ -369,6 +377,23 @@ static int64_t x3_resident_blocks(const void *kernel, int threads) {
   return r;
 }
 
+// per-device sink for the stores of rows past a region's y end (2 chunks x 64 lanes x 16 B); allocated by
+// stencil7x3_supported (model init), never inside a stream capture
+static std::map<int, char *> gX3Sinks;
+static std::mutex gX3SinkMu;
+static char *x3_sink(int dev, bool create) {
+  std::lock_guard<std::mutex> lk(gX3SinkMu);
+  char *&p = gX3Sinks[dev];
+  if (!p && create) {
+    int cur = 0;
+    HIP_CHECK(hipGetDevice(&cur));
+    HIP_CHECK(hipSetDevice(dev));
+    HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&p), 4096));
+    HIP_CHECK(hipSetDevice(cur));
+  }
+  return p;
+}
+
 bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune) {
   if (dom.backend() != Backend::Device || tune.wrap != 7) return false;
   if (!(dom.dtype(qi) == DType::F32 || (dom.dtype(qi) == DType::Bytes && dom.elem_size(qi) == 4))) return false;
@@ -377,6 +402,8 @@ bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   if (!(region.lo == cr.lo && region.hi == cr.hi)) return false; // every axis wraps at the region's faces
   const Dim3 n = dom.size();
   if (n.x != 512 || n.y < 3 || n.z < 16) return false;
+  if (dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096) return false; // 32-bit buffer-load offsets
+  (void)x3_sink(dom.gpu(), true);
   const int64_t lox = dom.radius().x(-1);
   return (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + lox * 4) % 16 == 0) &&
          (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + lox * 4) % 16 == 0) &&
@@ -427,6 +454,8 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     blocks = uint32_t(ls.blocks);
   }
   dom.set_device();
+  a.sink = x3_sink(dom.gpu(), false);
+  STENCIL_REQUIRE(a.sink, "stencil7x3: no store sink on device " << dom.gpu() << " (stencil7x3_supported first)");
   hipLaunchKernelGGL((stencil7x3_row_kernel<NW, PF, KIND>), dim3(blocks), dim3(64, NW), 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }

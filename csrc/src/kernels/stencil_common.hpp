@@ -72,6 +72,8 @@ template <typename T> struct StencilArgs {
   // boundary-plane publication (StencilTune::publish): output planes z < pubLo or z >= pubHi (raw) count into *pub
   unsigned long long *pub;
   int pubLo, pubHi;
+  // fused triples: rows past the region's y end store here instead of being skipped (same memory ops on every path)
+  char *sink;
 };
 
 // periodic image of raw coordinate c along axis ax (identity unless the axis wraps)
