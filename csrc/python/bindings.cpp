@@ -733,6 +733,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("nw", &StencilTune::nw)
       .def_readwrite("x2pf", &StencilTune::x2pf)
       .def_readwrite("x3sched", &StencilTune::x3sched)
+      .def_readwrite("x3layout", &StencilTune::x3layout)
+      .def_readwrite("x3var", &StencilTune::x3var)
+      .def_readwrite("x2early", &StencilTune::x2early)
       .def_readwrite("x2nw", &StencilTune::x2nw)
       .def_readwrite("x2row", &StencilTune::x2row)
       .def_readwrite("x2sched", &StencilTune::x2sched)

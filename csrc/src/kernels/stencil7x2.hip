@@ -602,6 +602,17 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
         const T cAt = TL ? cst[buf][wA][TL ? lane : 0] : T(0), cBt = TL ? cst[buf][wB][TL ? lane : 0] : T(0);
         apply_row(C[s1], cA, cB, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], row_sph(P), Ua, Ct[s1], cAt, cBt,
                   DOWN ? Ct[s0] : Ct[s2], DOWN ? Ct[s2] : Ct[s0], Uat);
+        if (a.early) { // block-uniform: publish into the other buffer now (its readers finished last step)
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            cs[buf ^ 1][w][h][lane] = C[s2][h];
+            us[buf ^ 1][w][h][lane] = Ua[h];
+          }
+          if constexpr (TL) {
+            cst[buf ^ 1][w][lane] = Ct[s2];
+            ust[buf ^ 1][w][lane] = Uat;
+          }
+        }
       } else {
 #pragma unroll
         for (int h = 0; h < H; ++h) Ua[h] = C[s1][h]; // never read: the edge waves' u1 feeds no output row
@@ -642,14 +653,16 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
         }
       }
       const int nbuf = buf ^ 1;
+      if (!(a.early && needU1)) {
 #pragma unroll
-      for (int h = 0; h < H; ++h) {
-        cs[nbuf][w][h][lane] = C[s2][h];
-        if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
-      }
-      if constexpr (TL) {
-        cst[nbuf][w][lane] = Ct[s2];
-        if (needU1) ust[nbuf][w][lane] = Uat;
+        for (int h = 0; h < H; ++h) {
+          cs[nbuf][w][h][lane] = C[s2][h];
+          if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
+        }
+        if constexpr (TL) {
+          cst[nbuf][w][lane] = Ct[s2];
+          if (needU1) ust[nbuf][w][lane] = Uat;
+        }
       }
       // boundary-plane publication (block-uniform): every wave's stores of plane z complete before the barrier,
       // then one thread writes the XCD's L2 back (system-scope release) and counts the block's cells of the plane
@@ -880,6 +893,11 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
           UaE[0] = fix(rs, xcol - 1, UaE[0]);
           UaE[1] = fix(rs, xcol + CW, UaE[1]);
         }
+        if (a.early) { // block-uniform: publish into the other buffer now (its readers finished last step)
+          publish_src(buf ^ 1, s2);
+#pragma unroll
+          for (int h = 0; h < H; ++h) us[buf ^ 1][w][h][lane] = Ua[h];
+        }
       }
       if (t >= 0 && needU2) {
         NV uA[H], uB[H], o[H];
@@ -902,10 +920,12 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
         }
       }
       const int nbuf = buf ^ 1;
-      publish_src(nbuf, s2);
+      if (!(a.early && needU1)) {
+        publish_src(nbuf, s2);
 #pragma unroll
-      for (int h = 0; h < H; ++h)
-        if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
+        for (int h = 0; h < H; ++h)
+          if (needU1) us[nbuf][w][h][lane] = Ua[h]; // the edge waves' u1 is never read
+      }
       __syncthreads();
       buf = nbuf;
 #pragma unroll
@@ -1223,6 +1243,7 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
   a.wrapm = tune.wrap;
+  a.early = tune.x2early ? 1 : 0;
   a.x0 = a.lox;
   a.nchunks = 128;
   a.remap = tune.xcdRemap ? 1 : 0;
@@ -1282,6 +1303,7 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
   a.wrapm = tune.wrap;
   a.xfast = tune.x2xfast;
   a.remap = tune.xcdRemap ? 1 : 0;
+  a.early = tune.x2early ? 1 : 0;
   a.x0 = a.lox; // 16-B aligned (checked by the caller)
   a.nchunks = (a.hix - a.x0) / V;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;

@@ -63,12 +63,20 @@ __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<float> &a, uint32
   return r;
 }
 
-template <int NW, int PF, int KIND>
+template <int NW, int PF, int KIND, bool CONTIG, int VAR>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x3_row_kernel(StencilArgs<float> a) {
   using T = float;
   using NV = nf4;
-  constexpr int V = 4, H = 2, HS = 64 * V;
+  constexpr int V = 4, H = 2;
+  // CONTIG: a lane holds 8 adjacent cells (chunk h = cells 8 lane + 4h ..): the row's x-neighbours and the periodic
+  // wrap are one rotate each way and no lane-0 / lane-63 selects. Otherwise chunk h = cells 256 h + 4 lane .. (every
+  // memory op a contiguous 1 KiB; each rotate needs a select between the two chunks at lanes 0 / 63)
+  constexpr int CS = CONTIG ? V : 64 * V; // cells between a lane's chunks
+  constexpr int LS = CONTIG ? H * V : V;  // cells between adjacent lanes
+  // VAR bit 0: publish u1 / u2 rows right after their update (LDS writes spread over the step instead of all before
+  // the barrier); bit 1: no scheduling fences between the levels; bit 2: publish the src row right after the u1 update (its load was waited for there)
+  constexpr bool EARLYW = (VAR & 1) != 0, NOSB = (VAR & 2) != 0, EARLYC = (VAR & 4) != 0;
   constexpr int YO = NW - 6; // output rows per block
   constexpr int NC = 3 + PF; // src planes in registers
   static_assert(NW == 12, "12 waves: 3 per SIMD (168 VGPRs), 3 x 48 KiB of LDS");
@@ -80,12 +88,12 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
   const uint32_t nb = gridDim.x;
   const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
   const int lane = threadIdx.x;
-  const int w = int(threadIdx.y); // the wave's block row
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.y)); // the wave's block row (wave-uniform: SGPR)
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
   const X3Seg sg = x3_segments(a, lb, nb, uint32_t(a.gy), nzt);
   const bool lane0 = lane == 0, lane63 = lane == 63;
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
-  const int xb = a.lox + lane * V; // chunk h at xb + h * HS
+  const int xb = a.lox + lane * LS; // chunk h at xb + h * CS
   const int zwn = a.wn[2], zwlo = a.wlo[2], zwhi = a.wlo[2] + a.wn[2];
   // raw buffer over the source field (offsets from raw [0,0,0] are non-negative and below 4 GiB: checked by the host)
   const __amdgpu_buffer_rsrc_t srcRsrc =
@@ -164,7 +172,7 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
             for (int h = 0; h < H; ++h)
 #pragma unroll
               for (int k = 0; k < V; ++k) {
-                const int x = xb + h * HS + k;
+                const int x = xb + h * CS + k;
                 const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
                 const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
                 o[h][k] = hot ? T(1) : (cold ? T(0) : o[h][k]);
@@ -178,6 +186,32 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
                               const NV(&zm)[H], NV(&o)[H]) -> T {
           constexpr bool EXACT = decltype(exactTag)::value;
           static_assert(H == 2, "two chunks per lane");
+          if constexpr (CONTIG) {
+            // cells c0..c7 of the lane; left of c0 = c7 of lane - 1 (lane 0: lane 63, the wrap), right of c7 = c0 of
+            // lane + 1
+            const T L = rot_prev(cm[1][V - 1]), Rr = rot_next(cm[0][0]);
+            const NV vmx0 = {L, cm[0][0], cm[0][1], cm[0][2]}, vpx0 = {cm[0][1], cm[0][2], cm[0][3], cm[1][0]};
+            const NV vmx1 = {cm[0][3], cm[1][0], cm[1][1], cm[1][2]}, vpx1 = {cm[1][1], cm[1][2], cm[1][3], Rr};
+            const NV sm0 = sum6v<T, KIND>(vpx0, vmx0, dn[0], up[0], zp[0], zm[0]);
+            const NV sm1 = sum6v<T, KIND>(vpx1, vmx1, dn[1], up[1], zp[1], zm[1]);
+            if constexpr (EXACT) {
+              // one tiny-sum test for the lane's 8 quotients
+              using NV8 = float __attribute__((ext_vector_type(8)));
+              const NV8 q = div6v<T, NV8, 2 * V>(__builtin_shufflevector(sm0, sm1, 0, 1, 2, 3, 4, 5, 6, 7));
+              o[0] = __builtin_shufflevector(q, q, 0, 1, 2, 3);
+              o[1] = __builtin_shufflevector(q, q, 4, 5, 6, 7);
+              return T(1);
+            } else {
+              T m = T(1);
+              const NV c = NV(1.0f / 6.0f), six = NV(6.0f);
+              const NV q0 = sm0 * c, q1 = sm1 * c;
+              o[0] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q0, six, sm0), c, q0);
+              o[1] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, six, sm1), c, q1);
+#pragma unroll
+              for (int k = 0; k < V; ++k) m = __builtin_fminf(m, __builtin_fminf(__builtin_fabsf(sm0[k]), __builtin_fabsf(sm1[k])));
+              return m;
+            }
+          }
           // named scalars, not arrays: a select between two array elements became a dynamically indexed private
           // array (scratch stores + loads on every row update, 449 vs 304 us per triple)
           const T r30 = rot_prev(cm[0][V - 1]), r31 = rot_prev(cm[1][V - 1]);
@@ -223,7 +257,7 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
 #pragma unroll
             for (int h = 0; h < H; ++h)
               C[k][h] = __builtin_bit_cast(
-                  NV, __builtin_amdgcn_raw_buffer_load_b128(srcRsrc, rowoff + uint32_t(h * HS * int(sizeof(T))), po, 0));
+                  NV, __builtin_amdgcn_raw_buffer_load_b128(srcRsrc, rowoff + uint32_t(h * CS * int(sizeof(T))), po, 0));
           };
           // step t = -4 starts with src planes z+dz .. z+(NC-1)dz, z = z0 - 4dz, and the src row of its u1 plane
           // (z+2dz: slot 1) published
@@ -261,10 +295,16 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
                 }
                 m = __builtin_fminf(m, row_update(exactTag, C[s1], A, B, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], U1a));
                 sphere_row(row_sph(z + 2 * dz), U1a);
+                if constexpr (EARLYC)
+#pragma unroll
+                  for (int h = 0; h < H; ++h) cs[buf ^ 1][w][h][lane] = C[s2][h];
+                if constexpr (EARLYW) // publish u1 now (the other buffer: its readers finished last step)
+#pragma unroll
+                  for (int h = 0; h < H; ++h) us[buf ^ 1][w][h][lane] = U1a[h];
               }
               // keep each level's LDS reads next to its update: hoisting all three levels' neighbour rows (48 VGPRs)
               // to the top of the step spills
-              __builtin_amdgcn_sched_barrier(0);
+              if constexpr (!NOSB) __builtin_amdgcn_sched_barrier(0);
               if constexpr (LV >= 2) {
                 NV A[H], B[H];
 #pragma unroll
@@ -274,8 +314,11 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
                 }
                 m = __builtin_fminf(m, row_update(exactTag, U1c, A, B, DOWN ? U1b : U1a, DOWN ? U1a : U1b, U2a));
                 sphere_row(row_sph(z + dz), U2a);
+                if constexpr (EARLYW)
+#pragma unroll
+                  for (int h = 0; h < H; ++h) vs[buf ^ 1][w][h][lane] = U2a[h];
               }
-              __builtin_amdgcn_sched_barrier(0);
+              if constexpr (!NOSB) __builtin_amdgcn_sched_barrier(0);
               if constexpr (LV >= 3) {
                 NV A[H], B[H];
 #pragma unroll
@@ -296,10 +339,10 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
               // unconditional: a row past the region's y end (the last row group) stores into a per-device sink, so
               // every path has the same vector-memory ops and the next step's load wait counts past these stores
               char *dp = outRow ? reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff
-                                : a.sink + lane * V * int(sizeof(T));
+                                : a.sink + lane * LS * int(sizeof(T));
 #pragma unroll
               for (int h = 0; h < H; ++h) {
-                NV *q = reinterpret_cast<NV *>(dp + h * HS * int(sizeof(T)));
+                NV *q = reinterpret_cast<NV *>(dp + h * CS * int(sizeof(T)));
                 if (a.nt)
                   __builtin_nontemporal_store(o[h], q);
                 else
@@ -309,9 +352,9 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
             const int nbuf = buf ^ 1;
 #pragma unroll
             for (int h = 0; h < H; ++h) {
-              cs[nbuf][w][h][lane] = C[s2][h];
-              if constexpr (R >= 1) us[nbuf][w][h][lane] = U1a[h];
-              if constexpr (R >= 2) vs[nbuf][w][h][lane] = U2a[h];
+              if constexpr (!EARLYC || LV < 1) cs[nbuf][w][h][lane] = C[s2][h];
+              if constexpr (R >= 1 && !EARLYW) us[nbuf][w][h][lane] = U1a[h];
+              if constexpr (R >= 2 && !EARLYW) vs[nbuf][w][h][lane] = U2a[h];
             }
             __syncthreads();
             buf = nbuf;
@@ -410,7 +453,7 @@ bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &regio
          (dom.pitch(qi).x * 4) % 16 == 0;
 }
 
-template <int KIND, int PF>
+template <int KIND, int PF, bool CONTIG, int VAR>
 static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
                        const StencilTune &tune) {
   constexpr int NW = 12, YO = NW - 6;
@@ -423,7 +466,7 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = 1;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = (const void *)stencil7x3_row_kernel<NW, PF, KIND>;
+  const void *kern = (const void *)stencil7x3_row_kernel<NW, PF, KIND, CONTIG, VAR>;
   const int64_t cols = a.gy;
   const int64_t slots = x3_resident_blocks(kern, 64 * NW);
   a.seg = 1;
@@ -456,17 +499,34 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   dom.set_device();
   a.sink = x3_sink(dom.gpu(), false);
   STENCIL_REQUIRE(a.sink, "stencil7x3: no store sink on device " << dom.gpu() << " (stencil7x3_supported first)");
-  hipLaunchKernelGGL((stencil7x3_row_kernel<NW, PF, KIND>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  hipLaunchKernelGGL((stencil7x3_row_kernel<NW, PF, KIND, CONTIG, VAR>), dim3(blocks), dim3(64, NW), 0, stream, a);
   HIP_CHECK(hipGetLastError());
 }
 
 bool stencil7x3_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune) {
   if (!stencil7x3_supported(dom, qi, region, tune)) return false;
-  if (kind == StencilKind::Jacobi)
-    apply_x3_t<0, 1>(dom, qi, region, sph, stream, tune);
+  const bool contig = tune.x3layout == 1;
+  const bool jac = kind == StencilKind::Jacobi;
+  auto go = [&](auto kindTag, auto varTag) {
+    constexpr int K = decltype(kindTag)::value, VR = decltype(varTag)::value;
+    contig ? apply_x3_t<K, 1, true, VR>(dom, qi, region, sph, stream, tune)
+           : apply_x3_t<K, 1, false, VR>(dom, qi, region, sph, stream, tune);
+  };
+  auto byvar = [&](auto kindTag) {
+    switch (tune.x3var) {
+    case 1: go(kindTag, std::integral_constant<int, 1>{}); break;
+    case 2: go(kindTag, std::integral_constant<int, 2>{}); break;
+    case 3: go(kindTag, std::integral_constant<int, 3>{}); break;
+    case 5: go(kindTag, std::integral_constant<int, 5>{}); break;
+    case 7: go(kindTag, std::integral_constant<int, 7>{}); break;
+    default: go(kindTag, std::integral_constant<int, 0>{}); break;
+    }
+  };
+  if (jac)
+    byvar(std::integral_constant<int, 0>{});
   else
-    apply_x3_t<1, 1>(dom, qi, region, sph, stream, tune);
+    byvar(std::integral_constant<int, 1>{});
   return true;
 }
 

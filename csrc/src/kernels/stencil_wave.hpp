@@ -100,23 +100,25 @@ template <typename F, int... I> __device__ __forceinline__ bool run_phases(F &f,
   return (f(std::integral_constant<int, I>{}) && ...);
 }
 
+// wave rotates write every lane, so no old value: mov_dpp leaves it undefined (update_dpp(0, ...) cost a v_mov 0 per
+// rotate) and lets the DPP combiner fold the rotate into its consumer
 __device__ __forceinline__ float rot_prev(float v) { // lane i <- lane i-1, lane 0 <- lane 63 (wave_ror:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x13C, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x13C, 0xf, 0xf, false));
 }
 __device__ __forceinline__ float rot_next(float v) { // lane i <- lane i+1, lane 63 <- lane 0 (wave_rol:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xf, 0xf, false));
 }
 
 __device__ __forceinline__ double rot_prev(double v) { // fp64: both 32-bit halves rotated
   const int64_t b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(b), 0x13C, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), 0x13C, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(int(b), 0x13C, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), 0x13C, 0xf, 0xf, false);
   return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
 }
 __device__ __forceinline__ double rot_next(double v) {
   const int64_t b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(b), 0x134, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), 0x134, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(int(b), 0x134, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), 0x134, 0xf, 0xf, false);
   return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
 }
 

@@ -300,25 +300,31 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
-@pytest.mark.parametrize("sched", [0, 1])
+@pytest.mark.parametrize("sched,layout,var,scale", [(0, 0, 0, 1.0), (1, 0, 0, 1.0), (1, 1, 0, 1.0), (1, 0, 1, 1.0),
+                                                    (1, 0, 3, 1.0), (1, 0, 5, 1.0), (1, 0, 7, 1.0),
+                                                    (1, 0, 1, 1e-33), (1, 1, 0, 1e-33)])
 @pytest.mark.parametrize("kind,size", [("jacobi", (512, 120, 116)), ("jacobi", (512, 128, 120)),
                                        ("jacobi", (512, 512, 112)), ("astaroth", (512, 36, 28)),
                                        ("astaroth", (512, 13, 17)), ("astaroth", (512, 3, 16))])
-def test_temporal3_matches_three_single_steps(st, kind, size, sched):
+def test_temporal3_matches_three_single_steps(st, kind, size, sched, layout, var, scale):
     """Fused triples (stencil7x3_row_kernel, temporal=3, one GPU, every axis wrapped in-kernel): S(S(S(u))) bitwise
     equal to three single steps of the torch oracle; run(n) covers whole hipGraph blocks (18 steps), triples and the
     pair / single-step remainders; y extents that are not a multiple of the block's 6 output rows and a 3-row grid
-    (every block row wraps onto itself twice)."""
+    (every block row wraps onto itself twice). Both lane layouts (x3layout: 8 adjacent cells per lane, or chunks 256
+    apart); scale 1e-33 puts every sum below 2^-100, where the quotient is the true division."""
     from stencil2_amd.ops import astaroth_step_reference
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
     t = st.StencilTune()
     t.x3sched = sched
+    t.x3layout = layout
+    t.x3var = var
     m = cls(size, gpus=[0], temporal=3, tune=t, **kw)
     m.init()
     assert m.temporal_triples() and m.wrap_axes() == 7
     m.prepare()
     u = torch.rand((size[2], size[1], size[0]), device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+    u = u * scale
     for q in range(kw.get("quantities", 1)):
         m.interior(0, q).copy_(u)
     torch.cuda.synchronize()
@@ -353,10 +359,11 @@ def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf, row):
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
     ms = []
-    for r in (row, 0):
+    for r, early in ((row, False), (0, False), (row, True)):  # x2early: src / u1 rows published right after u1
         t = st.StencilTune()
         t.x2pf = pf
         t.x2row = r
+        t.x2early = early
         ms.append(cls(size, gpus=gpus, temporal=2, tune=t, axis_cost=(4, 2, 3), **kw))  # bench.py's cut: x stays whole
     for m in ms:
         m.init()
@@ -370,7 +377,7 @@ def test_temporal2_whole_row_kernel(st, kind, size, gpus, pf, row):
             u = ref(u)
         for m in ms:
             m.synchronize()
-            assert torch.equal(_gather(m), u), f"x2row={(row, 0)[ms.index(m)]} after run({n})"
+            assert torch.equal(_gather(m), u), f"model {ms.index(m)} (x2row, x2early = {row}/0/{row}+early) after run({n})"
 
 
 @pytest.mark.parametrize("kind,size,gpus,fp64", [("jacobi", (512, 120, 116), [0], False),
@@ -431,9 +438,10 @@ def test_temporal2_col512_kernel(st, kind, size, gpus, wrap, cost, fp64):
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
     ms = []
-    for row in (1, 0):
+    for row, early in ((1, False), (0, False), (1, True)):
         t = st.StencilTune()
         t.x2row = row
+        t.x2early = early
         ms.append(cls(size, gpus=gpus, temporal=2, tune=t, wrap_self=wrap, axis_cost=cost, fp64=fp64, **kw))
     for m in ms:
         m.init()
@@ -446,7 +454,7 @@ def test_temporal2_col512_kernel(st, kind, size, gpus, wrap, cost, fp64):
             u = ref(u)
         for m in ms:
             m.synchronize()
-            assert torch.equal(_gather(m), u), f"x2row={1 - ms.index(m)} after run({n})"
+            assert torch.equal(_gather(m), u), f"model {ms.index(m)} (col2 / column / col2 + x2early) after run({n})"
 
 
 @pytest.mark.parametrize("temporal", [1, 2])
