@@ -52,8 +52,11 @@ struct StencilTune {
   int x2nw = 12, x2pf = 1; // one plane of lookahead: best for the whole-row kernel once its edge waves skip u1/u2
   int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
   int x3layout = 0;       // fused triples: 1 = 8 adjacent cells per lane (one rotate per x side), 0 = chunks 256 apart
-  int x3var = 0;          // fused triples: bit 0 = publish u1/u2 right after their update, bit 1 = no fences between levels
-  bool x2early = false;   // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
+  int x3var = 7;          // fused triples: bit 0 = publish u1/u2 right after their update, bit 1 = no fences between
+                          // levels, bit 2 = publish the src row right after u1 (7: 1431-1443 vs 0: 1381-1392 Gcells/s)
+  int x3pf = 1;           // fused triples: src planes of lookahead in registers (1, 2)
+  bool x2early = true;    // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
+                          // (row kernel 208.6 vs 216.6 us per pair, col2 226.9 vs 234.1)
   // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells
   // long; x-neighbours and the wrap by DPP lane rotates, stencil7x2_row_kernel), or 512-cell columns (x a whole
   // number of 512-cell columns: two 16-B chunks per lane, only the column ends from outside the wave,

@@ -80,7 +80,7 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
   constexpr int YO = NW - 6; // output rows per block
   constexpr int NC = 3 + PF; // src planes in registers
   static_assert(NW == 12, "12 waves: 3 per SIMD (168 VGPRs), 3 x 48 KiB of LDS");
-  static_assert(PF == 1, "the warm-up is one unrolled cycle of the NC = 4 slot rotation");
+  static_assert(PF == 1 || PF == 2, "slot rotations of 4 or 5 planes (4 unrolled warm-up steps, then the cycle)");
   __shared__ NV cs[2][NW][H][64]; // src rows  (plane z+3dz at publish)
   __shared__ NV us[2][NW][H][64]; // u1 rows   (plane z+2dz at publish)
   __shared__ NV vs[2][NW][H][64]; // u2 rows   (plane z+dz at publish)
@@ -372,6 +372,7 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
           using I1 = std::integral_constant<int, 1>;
           using I2 = std::integral_constant<int, 2>;
           using I3 = std::integral_constant<int, 3>;
+          using I4 = std::integral_constant<int, 4 % NC>;
           using L1 = std::integral_constant<int, (R < 1 ? R : 1)>;
           using L2 = std::integral_constant<int, (R < 2 ? R : 2)>;
           using LR = std::integral_constant<int, R>;
@@ -380,7 +381,11 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
           step(I1{}, L1{});
           step(I2{}, L2{});
           step(I3{}, L2{});
-          while (step(I0{}, LR{}) && step(I1{}, LR{}) && step(I2{}, LR{}) && step(I3{}, LR{})) {
+          if constexpr (NC == 5)
+            while (step(I4{}, LR{}) && step(I0{}, LR{}) && step(I1{}, LR{}) && step(I2{}, LR{}) && step(I3{}, LR{})) {
+            }
+          else
+            while (step(I0{}, LR{}) && step(I1{}, LR{}) && step(I2{}, LR{}) && step(I3{}, LR{})) {
           }
         };
         if (down)
@@ -506,27 +511,26 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
 bool stencil7x3_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune) {
   if (!stencil7x3_supported(dom, qi, region, tune)) return false;
-  const bool contig = tune.x3layout == 1;
-  const bool jac = kind == StencilKind::Jacobi;
-  auto go = [&](auto kindTag, auto varTag) {
-    constexpr int K = decltype(kindTag)::value, VR = decltype(varTag)::value;
-    contig ? apply_x3_t<K, 1, true, VR>(dom, qi, region, sph, stream, tune)
-           : apply_x3_t<K, 1, false, VR>(dom, qi, region, sph, stream, tune);
+  // instantiated: x3var 7 (the default) and 0 (r5/s: everything published before the barrier), both layouts, one or
+  // two planes of lookahead; r5/v measured 1 / 3 / 5 between them (profiles/r5/v/summary.txt)
+  STENCIL_REQUIRE(tune.x3var == 0 || tune.x3var == 7, "stencil7x3: x3var " << tune.x3var << " not instantiated (0, 7)");
+  STENCIL_REQUIRE(tune.x3pf == 1 || tune.x3pf == 2, "stencil7x3: x3pf " << tune.x3pf << " (1, 2)");
+  const bool contig = tune.x3layout == 1, v7 = tune.x3var == 7, pf2 = tune.x3pf == 2;
+  auto go = [&](auto kindTag, auto pfTag) {
+    constexpr int K = decltype(kindTag)::value, P = decltype(pfTag)::value;
+    if (contig)
+      v7 ? apply_x3_t<K, P, true, 7>(dom, qi, region, sph, stream, tune)
+         : apply_x3_t<K, P, true, 0>(dom, qi, region, sph, stream, tune);
+    else
+      v7 ? apply_x3_t<K, P, false, 7>(dom, qi, region, sph, stream, tune)
+         : apply_x3_t<K, P, false, 0>(dom, qi, region, sph, stream, tune);
   };
-  auto byvar = [&](auto kindTag) {
-    switch (tune.x3var) {
-    case 1: go(kindTag, std::integral_constant<int, 1>{}); break;
-    case 2: go(kindTag, std::integral_constant<int, 2>{}); break;
-    case 3: go(kindTag, std::integral_constant<int, 3>{}); break;
-    case 5: go(kindTag, std::integral_constant<int, 5>{}); break;
-    case 7: go(kindTag, std::integral_constant<int, 7>{}); break;
-    default: go(kindTag, std::integral_constant<int, 0>{}); break;
-    }
-  };
-  if (jac)
-    byvar(std::integral_constant<int, 0>{});
+  using P1 = std::integral_constant<int, 1>;
+  using P2 = std::integral_constant<int, 2>;
+  if (kind == StencilKind::Jacobi)
+    pf2 ? go(std::integral_constant<int, 0>{}, P2{}) : go(std::integral_constant<int, 0>{}, P1{});
   else
-    byvar(std::integral_constant<int, 1>{});
+    pf2 ? go(std::integral_constant<int, 1>{}, P2{}) : go(std::integral_constant<int, 1>{}, P1{});
   return true;
 }
 

@@ -300,13 +300,13 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
-@pytest.mark.parametrize("sched,layout,var,scale", [(0, 0, 0, 1.0), (1, 0, 0, 1.0), (1, 1, 0, 1.0), (1, 0, 1, 1.0),
-                                                    (1, 0, 3, 1.0), (1, 0, 5, 1.0), (1, 0, 7, 1.0),
-                                                    (1, 0, 1, 1e-33), (1, 1, 0, 1e-33)])
+@pytest.mark.parametrize("sched,layout,var,pf,scale", [(0, 0, 7, 1, 1.0), (1, 0, 7, 1, 1.0), (1, 1, 7, 1, 1.0),
+                                                       (1, 0, 0, 1, 1.0), (1, 0, 7, 2, 1.0), (1, 1, 0, 2, 1.0),
+                                                       (1, 0, 7, 1, 1e-33), (1, 1, 7, 2, 1e-33)])
 @pytest.mark.parametrize("kind,size", [("jacobi", (512, 120, 116)), ("jacobi", (512, 128, 120)),
                                        ("jacobi", (512, 512, 112)), ("astaroth", (512, 36, 28)),
                                        ("astaroth", (512, 13, 17)), ("astaroth", (512, 3, 16))])
-def test_temporal3_matches_three_single_steps(st, kind, size, sched, layout, var, scale):
+def test_temporal3_matches_three_single_steps(st, kind, size, sched, layout, var, pf, scale):
     """Fused triples (stencil7x3_row_kernel, temporal=3, one GPU, every axis wrapped in-kernel): S(S(S(u))) bitwise
     equal to three single steps of the torch oracle; run(n) covers whole hipGraph blocks (18 steps), triples and the
     pair / single-step remainders; y extents that are not a multiple of the block's 6 output rows and a 3-row grid
@@ -319,6 +319,7 @@ def test_temporal3_matches_three_single_steps(st, kind, size, sched, layout, var
     t.x3sched = sched
     t.x3layout = layout
     t.x3var = var
+    t.x3pf = pf
     m = cls(size, gpus=[0], temporal=3, tune=t, **kw)
     m.init()
     assert m.temporal_triples() and m.wrap_axes() == 7
