@@ -666,7 +666,10 @@ def main(argv=None):
     overlap_tuned = None
     if args.overlap == "auto" and args.tune_steps > 0 and model.can_toggle_overlap():
         best = {}
-        k = max(2, args.tune_steps // 2 * 2)
+        # whole-region candidates (mode 0) run fused triples where the model can (temporal 3): probe and time whole
+        # triples and pairs alike (multiples of 6 steps)
+        sweep = 6 if args.temporal >= 3 else 2
+        k = max(sweep, args.tune_steps // sweep * sweep)
         r0 = args.x2reserve
         # (mode, CUs left to the transports, co-located copy): mode 1 = slabs beside the sweep, 2 = slabs after
         # it, 0 = whole-region pairs, 3 = pipelined whole-region pairs; copy "s" = pack kernel stores into the peer
@@ -692,12 +695,12 @@ def main(argv=None):
             if c in skip:
                 continue
             apply(c)
-            model.run(2)
+            model.run(sweep)
             model.synchronize()
-            # a 2-step probe first: a candidate far slower than the best so far (ranks sharing one GPU: DMA-engine
+            # a short probe first: a candidate far slower than the best so far (ranks sharing one GPU: DMA-engine
             # copies beside overlapped sweeps ran at ~0.8 s per step, profiles/r3/check2) is not given full rounds
             ref = min(best.values(), default=float("inf"))
-            t = timed_run(model, 2)
+            t = timed_run(model, sweep)
             if t > 4 * ref:
                 skip.add(c)
                 best[c] = min(best.get(c, float("inf")), t)
@@ -708,10 +711,11 @@ def main(argv=None):
                       file=sys.stderr, flush=True)
         choice = min(cands, key=lambda c: best[c])
         apply(choice)
-        model.run(2)
+        model.run(sweep)
         model.synchronize()
         env.barrier()
         overlap_tuned = {"mode": choice[0], "reserve": choice[1], "colo_copy": "engine" if choice[2] == "e" else "store",
+                         "triples": bool(model.temporal_triples()),
                          **{f"m{c[0]}_r{c[1]}_{c[2]}_ms": round(best[c], 4) for c in cands}}
 
     # ---- the timed loop: exactly --steps steps, bracketed by a barrier + device synchronize on both sides ----

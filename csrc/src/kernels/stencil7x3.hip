@@ -75,8 +75,9 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
   constexpr int CS = CONTIG ? V : 64 * V; // cells between a lane's chunks
   constexpr int LS = CONTIG ? H * V : V;  // cells between adjacent lanes
   // VAR bit 0: publish u1 / u2 rows right after their update (LDS writes spread over the step instead of all before
-  // the barrier); bit 1: no scheduling fences between the levels; bit 2: publish the src row right after the u1 update (its load was waited for there)
-  constexpr bool EARLYW = (VAR & 1) != 0, NOSB = (VAR & 2) != 0, EARLYC = (VAR & 4) != 0;
+  // the barrier); bit 1: no scheduling fences between the levels; bit 2: publish the src row right after the u1 update (its load was waited for there); bit 3: every
+  // level's LDS reads at the top of the step
+  constexpr bool EARLYW = (VAR & 1) != 0, NOSB = (VAR & 2) != 0, EARLYC = (VAR & 4) != 0, HOIST = (VAR & 8) != 0;
   constexpr int YO = NW - 6; // output rows per block
   constexpr int NC = 3 + PF; // src planes in registers
   static_assert(NW == 12, "12 waves: 3 per SIMD (168 VGPRs), 3 x 48 KiB of LDS");
@@ -286,14 +287,24 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
             NV o[H];
             auto levels = [&](auto exactTag) -> T {
               T m = T(1);
-              if constexpr (LV >= 1) {
-                NV A[H], B[H];
+              // every level reads the previous step's rows (buf): no level waits for another's LDS writes, so HOIST
+              // issues all of them right after the barrier (one LDS latency per step instead of three)
+              NV A1[H], B1[H], A2[H], B2[H], A3[H], B3[H];
+              auto rd = [&](NV(&sh)[2][NW][H][64], NV(&A)[H], NV(&B)[H]) {
 #pragma unroll
                 for (int h = 0; h < H; ++h) {
-                  A[h] = cs[buf][wA][h][lane];
-                  B[h] = cs[buf][wB][h][lane];
+                  A[h] = sh[buf][wA][h][lane];
+                  B[h] = sh[buf][wB][h][lane];
                 }
-                m = __builtin_fminf(m, row_update(exactTag, C[s1], A, B, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], U1a));
+              };
+              if constexpr (HOIST) {
+                if constexpr (LV >= 1) rd(cs, A1, B1);
+                if constexpr (LV >= 2) rd(us, A2, B2);
+                if constexpr (LV >= 3) rd(vs, A3, B3);
+              }
+              if constexpr (LV >= 1) {
+                if constexpr (!HOIST) rd(cs, A1, B1);
+                m = __builtin_fminf(m, row_update(exactTag, C[s1], A1, B1, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], U1a));
                 sphere_row(row_sph(z + 2 * dz), U1a);
                 if constexpr (EARLYC)
 #pragma unroll
@@ -302,17 +313,12 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
 #pragma unroll
                   for (int h = 0; h < H; ++h) us[buf ^ 1][w][h][lane] = U1a[h];
               }
-              // keep each level's LDS reads next to its update: hoisting all three levels' neighbour rows (48 VGPRs)
-              // to the top of the step spills
+              // (!NOSB) keep each level's LDS reads next to its update: at 144 VGPRs, hoisting all three levels'
+              // neighbour rows (48 VGPRs) to the top of the step spilled
               if constexpr (!NOSB) __builtin_amdgcn_sched_barrier(0);
               if constexpr (LV >= 2) {
-                NV A[H], B[H];
-#pragma unroll
-                for (int h = 0; h < H; ++h) {
-                  A[h] = us[buf][wA][h][lane];
-                  B[h] = us[buf][wB][h][lane];
-                }
-                m = __builtin_fminf(m, row_update(exactTag, U1c, A, B, DOWN ? U1b : U1a, DOWN ? U1a : U1b, U2a));
+                if constexpr (!HOIST) rd(us, A2, B2);
+                m = __builtin_fminf(m, row_update(exactTag, U1c, A2, B2, DOWN ? U1b : U1a, DOWN ? U1a : U1b, U2a));
                 sphere_row(row_sph(z + dz), U2a);
                 if constexpr (EARLYW)
 #pragma unroll
@@ -320,13 +326,8 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
               }
               if constexpr (!NOSB) __builtin_amdgcn_sched_barrier(0);
               if constexpr (LV >= 3) {
-                NV A[H], B[H];
-#pragma unroll
-                for (int h = 0; h < H; ++h) {
-                  A[h] = vs[buf][wA][h][lane];
-                  B[h] = vs[buf][wB][h][lane];
-                }
-                m = __builtin_fminf(m, row_update(exactTag, U2c, A, B, DOWN ? U2b : U2a, DOWN ? U2a : U2b, o));
+                if constexpr (!HOIST) rd(vs, A3, B3);
+                m = __builtin_fminf(m, row_update(exactTag, U2c, A3, B3, DOWN ? U2b : U2a, DOWN ? U2a : U2b, o));
                 sphere_row(row_sph(z), o);
               }
               return m;
@@ -443,11 +444,16 @@ static char *x3_sink(int dev, bool create) {
 }
 
 bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune) {
-  if (dom.backend() != Backend::Device || tune.wrap != 7) return false;
+  // x wraps in-kernel (whole 512-cell rows, DPP rotates); y / z either wrap in-kernel too (one GPU: nothing is
+  // exchanged) or read 3-deep halos the exchange filled (an axis cut across GPUs / sub-domains)
+  if (dom.backend() != Backend::Device || !(tune.wrap & 1)) return false;
   if (!(dom.dtype(qi) == DType::F32 || (dom.dtype(qi) == DType::Bytes && dom.elem_size(qi) == 4))) return false;
-  if ((stencil7x2_wrappable_axes(dom, qi, 1) & 7) != 7) return false;
+  if (!(stencil7x2_wrappable_axes(dom, qi, 1) & 1)) return false;
+  const Radius &rad = dom.radius();
+  if (!(tune.wrap & 2) && (rad.y(-1) < 3 || rad.y(1) < 3)) return false;
+  if (!(tune.wrap & 4) && (rad.z(-1) < 3 || rad.z(1) < 3)) return false;
   const Rect3 cr = dom.get_compute_region();
-  if (!(region.lo == cr.lo && region.hi == cr.hi)) return false; // every axis wraps at the region's faces
+  if (!(region.lo == cr.lo && region.hi == cr.hi)) return false; // the kernel sweeps whole sub-domains
   const Dim3 n = dom.size();
   if (n.x != 512 || n.y < 3 || n.z < 16) return false;
   if (dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096) return false; // 32-bit buffer-load offsets
@@ -465,7 +471,10 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   StencilArgs<float> a = make_args<float>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
-  a.wrapm = 7;
+  a.wrapm = tune.wrap & 7;
+  // an axis read from its halos: no periodic shift (the kernel's row / plane wrap adds / subtracts wn)
+  if (!(a.wrapm & 2)) a.wn[1] = 0;
+  if (!(a.wrapm & 4)) a.wn[2] = 0;
   a.x0 = a.lox;
   a.remap = tune.xcdRemap ? 1 : 0;
   const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
@@ -513,17 +522,20 @@ bool stencil7x3_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   if (!stencil7x3_supported(dom, qi, region, tune)) return false;
   // instantiated: x3var 7 (the default) and 0 (r5/s: everything published before the barrier), both layouts, one or
   // two planes of lookahead; r5/v measured 1 / 3 / 5 between them (profiles/r5/v/summary.txt)
-  STENCIL_REQUIRE(tune.x3var == 0 || tune.x3var == 7, "stencil7x3: x3var " << tune.x3var << " not instantiated (0, 7)");
+  STENCIL_REQUIRE(tune.x3var == 0 || tune.x3var == 7 || tune.x3var == 15,
+                  "stencil7x3: x3var " << tune.x3var << " not instantiated (0, 7, 15)");
   STENCIL_REQUIRE(tune.x3pf == 1 || tune.x3pf == 2, "stencil7x3: x3pf " << tune.x3pf << " (1, 2)");
-  const bool contig = tune.x3layout == 1, v7 = tune.x3var == 7, pf2 = tune.x3pf == 2;
+  const bool contig = tune.x3layout == 1, pf2 = tune.x3pf == 2;
   auto go = [&](auto kindTag, auto pfTag) {
     constexpr int K = decltype(kindTag)::value, P = decltype(pfTag)::value;
     if (contig)
-      v7 ? apply_x3_t<K, P, true, 7>(dom, qi, region, sph, stream, tune)
-         : apply_x3_t<K, P, true, 0>(dom, qi, region, sph, stream, tune);
+      tune.x3var == 7 ? apply_x3_t<K, P, true, 7>(dom, qi, region, sph, stream, tune)
+                      : apply_x3_t<K, P, true, 0>(dom, qi, region, sph, stream, tune);
+    else if (tune.x3var == 15)
+      apply_x3_t<K, P, false, 15>(dom, qi, region, sph, stream, tune);
     else
-      v7 ? apply_x3_t<K, P, false, 7>(dom, qi, region, sph, stream, tune)
-         : apply_x3_t<K, P, false, 0>(dom, qi, region, sph, stream, tune);
+      tune.x3var == 7 ? apply_x3_t<K, P, false, 7>(dom, qi, region, sph, stream, tune)
+                      : apply_x3_t<K, P, false, 0>(dom, qi, region, sph, stream, tune);
   };
   using P1 = std::integral_constant<int, 1>;
   using P2 = std::integral_constant<int, 2>;

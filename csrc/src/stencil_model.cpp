@@ -17,11 +17,15 @@ StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::
     r.set_face(cfg.radius);
   }
   if (cfg.temporal >= 2) {
-    // S o S of a 7-point stencil reaches 2 cells along an axis and 1 cell diagonally (edges), never corners
+    // S o S of a 7-point stencil reaches 2 cells along an axis and 1 cell diagonally (edges), never corners;
+    // S o S o S 3 along an axis and (1, 2) / (2, 1) on edges (an edge halo spans the face depths of its two axes,
+    // LocalDomain::halo_extent, so a nonzero edge radius is enough). Its (1, 1, 1) corners involve x, which the
+    // triples always wrap in-kernel (stencil7x3_supported), so corners stay out of the exchange
+    const int64_t face = cfg.temporal >= 3 ? 3 : 2;
     for (int i = 0; i < 27; ++i) {
       const Dim3 d = dir_from_index(i);
       const int nz = (d.x != 0) + (d.y != 0) + (d.z != 0);
-      if (nz == 1) r.dir(d) = std::max<int64_t>(r.dir(d), 2);
+      if (nz == 1) r.dir(d) = std::max<int64_t>(r.dir(d), face);
       if (nz == 2) r.dir(d) = std::max<int64_t>(r.dir(d), 1);
     }
   }
@@ -237,9 +241,11 @@ void StencilModel::init() {
   if (confinedSelf_) dd_->set_translate_max_blocks(cfg_.tune.x2reserve);
   // overlapped pairs with the slabs after the interior sweep (set_overlap_mode(2)) from the start
   slabsAfter_ = pairs_ && overlap_ && cfg_.overlapMode == 2;
-  // fused triples: one device, every axis wrapped in-kernel (nothing is exchanged), whole region, the spheres at
+  // fused triples: device sub-domains whose x axis wraps in-kernel (whole 512-cell rows); y / z wrap in-kernel too
+  // (one GPU: nothing is exchanged) or read the 3-deep halos of a depth-3 exchange, one per three steps (multi-GPU).
+  // Whole regions only, so not beside an overlapped exchange (set_overlap switches between the two). The spheres at
   // least 3 cells from the periodic faces (the intermediate steps evaluate them at unwrapped halo coordinates)
-  triples_ = pairs_ && cfg_.temporal >= 3 && !overlap_ && doms0.size() == 1 && pairTune_.wrap == 7;
+  triples_ = pairs_ && cfg_.temporal >= 3 && stepDevice && (pairTune_.wrap & 1);
   if (triples_ && sph_.enabled) {
     const Dim3 L = cfg_.size;
     for (const Dim3 &c : {sph_.hot, sph_.cold}) {
@@ -248,8 +254,11 @@ void StencilModel::init() {
         if (cc[a] - sph_.radius < 2 || cc[a] + sph_.radius > ll[a] - 3) triples_ = false;
     }
   }
-  for (int64_t q = 0; triples_ && q < doms0[0].num_data(); ++q)
-    triples_ = stencil7x3_supported(doms0[0], q, doms0[0].get_compute_region(), pairTune_);
+  for (size_t di = 0; di < doms0.size() && triples_; ++di)
+    for (int64_t q = 0; triples_ && q < doms0[di].num_data(); ++q)
+      triples_ = stencil7x3_supported(doms0[di], q, doms0[di].get_compute_region(), pairTune_);
+  triplesOk_ = triples_;
+  triples_ = triplesOk_ && !overlap_;
   graphs_ = cfg_.useGraph && !overlap_ && dd_->domains().size() == 1 &&
             dd_->domains()[0].backend() == Backend::Device &&
             dd_->exchange_bytes_for_method(MethodFlags::Kernel) == dd_->exchange_bytes_for_method(MethodFlags::All) &&
@@ -443,16 +452,17 @@ void StencilModel::enqueue_step(int k) {
     return;
   }
   if (k == 3) {
-    // fused triples: every halo is read in-kernel at its periodic image, so the exchange has nothing left to copy
-    // (it still orders the step like the pairs' one); then S o S o S of the whole region
+    // fused triples: one depth-3 exchange (one GPU: every halo is read in-kernel at its periodic image, so it has
+    // nothing left to copy and only orders the step), then S o S o S of every sub-domain
     const bool single = device && doms.size() == 1;
     dd_->exchange_async(single ? compute_[0].get() : nullptr, pairTune_.wrap);
-    hipStream_t s = device ? compute_[0].get() : nullptr;
-    if (!single) dd_->wait_exchange(0, s);
-    StencilTune ti = pairTune_;
-    for (int64_t q = 0; q < doms[0].num_data(); ++q)
-      STENCIL_REQUIRE(stencil7x3_apply(doms[0], q, doms[0].get_compute_region(), cfg_.kind, sph_, s, ti),
-                      "fused triple not supported for quantity " << q);
+    for (size_t di = 0; di < doms.size(); ++di) {
+      hipStream_t s = device ? compute_[di].get() : nullptr;
+      if (!single) dd_->wait_exchange(di, s);
+      for (int64_t q = 0; q < doms[di].num_data(); ++q)
+        STENCIL_REQUIRE(stencil7x3_apply(doms[di], q, doms[di].get_compute_region(), cfg_.kind, sph_, s, pairTune_),
+                        "fused triple not supported for quantity " << q);
+    }
     return;
   }
   if (k == 2) {
@@ -543,6 +553,7 @@ void StencilModel::set_overlap(bool on) {
   if (on == overlap_) return;
   synchronize();
   overlap_ = on;
+  triples_ = triplesOk_ && !on; // whole-region sweeps: triples where supported
   dd_->set_comm_max_blocks(on ? cfg_.tune.x2reserve : 0);
 }
 

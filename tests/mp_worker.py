@@ -171,6 +171,8 @@ def scenario_jacobi(backend, methods, size):
                 m.run(k)
                 for _ in range(k):
                     u = ref(u)
+    if os.environ.get("MP_EXPECT_TRIPLES") is not None:  # fused triples in the final (whole-region) mode
+        bad += int(m.temporal_triples() != (os.environ["MP_EXPECT_TRIPLES"] == "1"))
     m.synchronize()
     for di in range(m.domain.num_domains()):
         d = m.domain.domain(di)

@@ -302,7 +302,8 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
 
 @pytest.mark.parametrize("sched,layout,var,pf,scale", [(0, 0, 7, 1, 1.0), (1, 0, 7, 1, 1.0), (1, 1, 7, 1, 1.0),
                                                        (1, 0, 0, 1, 1.0), (1, 0, 7, 2, 1.0), (1, 1, 0, 2, 1.0),
-                                                       (1, 0, 7, 1, 1e-33), (1, 1, 7, 2, 1e-33)])
+                                                       (1, 0, 7, 1, 1e-33), (1, 1, 7, 2, 1e-33),
+                                                       (1, 0, 15, 1, 1.0), (1, 0, 15, 2, 1e-33)])
 @pytest.mark.parametrize("kind,size", [("jacobi", (512, 120, 116)), ("jacobi", (512, 128, 120)),
                                        ("jacobi", (512, 512, 112)), ("astaroth", (512, 36, 28)),
                                        ("astaroth", (512, 13, 17)), ("astaroth", (512, 3, 16))])
@@ -338,6 +339,29 @@ def test_temporal3_matches_three_single_steps(st, kind, size, sched, layout, var
             got = m.interior(0, q)
             bad = int((got != u).sum())
             assert bad == 0, f"run({n}) q{q}: {bad} cells differ, max {(got - u).abs().max().item()}"
+
+
+# cuts follow the interface cost (NodePartition): 4*Y*Z for an x cut against 2*X*Z (y, cost 4,2,3) / 2*X*Y (z, 4,3,2)
+@pytest.mark.parametrize("kind,size,gpus,cost", [("astaroth", (512, 300, 24), [0, 0], (4, 2, 3)),
+                                                 ("astaroth", (512, 16, 300), [0, 0], (4, 3, 2)),
+                                                 ("jacobi", (512, 300, 128), [0, 0], (4, 2, 3)),
+                                                 ("astaroth", (512, 600, 24), [0, 0, 0, 0], (4, 2, 3))])
+def test_temporal3_halo_axes(st, kind, size, gpus, cost):
+    """Fused triples on sub-domains cut along y and/or z (several on one GPU, same-GPU depth-3 exchange): x wraps
+    in-kernel, the cut axes read their 3-deep halos. Bitwise equal to single steps of the torch oracle."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    m = cls(size, gpus=gpus, temporal=3, axis_cost=cost, **kw)
+    m.init()
+    assert m.temporal_triples() and (m.wrap_axes() & 1) and m.wrap_axes() != 7, f"wrap_axes={m.wrap_axes()}"
+    u = _gather(m)
+    for n in (3, 7, 9, 2):
+        m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        m.synchronize()
+        assert torch.equal(_gather(m), u), f"run({n}) wrap_axes={m.wrap_axes()}"
 
 
 @pytest.mark.parametrize("kind,size,gpus,pf,row", [
@@ -857,6 +881,25 @@ def test_colocated_ipc_overlap_toggle_two_ranks():
                                 "MP_TEMPORAL": "2", "MP_EXPECT_OVERLAP": "1", "MP_TOGGLE_OVERLAP": "1"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
+
+
+# cuts follow the interface cost (NodePartition): 4*Y*Z for an x cut against 2*X*Z (y, cost 4,2,3) / 2*X*Y (z, 4,3,2)
+@pytest.mark.parametrize("kind,size,cost,ranks", [("astaroth", "512,264,16", "4,2,3", 2), ("astaroth", "512,16,300", "4,3,2", 2),
+                                                  ("jacobi", "512,300,128", "4,2,3", 2),
+                                                  ("astaroth", "512,600,24", "4,2,3", 4)])
+def test_triples_across_ranks(kind, size, cost, ranks):
+    """Fused triples with remote halos (multi-GPU layout rehearsed by ranks sharing one GPU over HIP IPC): x wrapped
+    in-kernel, the cut axes read the 3-deep halos of one exchange per three steps. The overlapped pairs are the
+    auto default; set_overlap_mode(0) (the bench's whole-region candidate) switches to triples. Bitwise vs the
+    oracle through single steps, pairs and triples."""
+    outs = run_ranks(ranks, WORKER, ["jacobi", size],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": "3", "MP_KIND": kind, "MP_RANDOM": "1", "MP_AXIS_COST": cost,
+                                "MP_TOGGLE_OVERLAP": "1", "MP_TOGGLE_MODES": "0", "MP_TOGGLE_STEPS": "10",
+                                "MP_EXPECT_TRIPLES": "1"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out, out[-2000:]
 
 
 @pytest.mark.parametrize("size,cost", [("512,264,16", "4,2,3"), ("1024,520,12", "4,2,3"), ("645,520,12", "4,2,3"),
