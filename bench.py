@@ -672,7 +672,8 @@ def main(argv=None):
         k = max(sweep, args.tune_steps // sweep * sweep)
         r0 = args.x2reserve
         # (mode, CUs left to the transports, co-located copy): mode 1 = slabs beside the sweep, 2 = slabs after
-        # it, 0 = whole-region pairs, 3 = pipelined whole-region pairs; copy "s" = pack kernel stores into the peer
+        # it, 0 = whole-region sweeps (fused triples where possible), 3 = pipelined whole-region pairs, 4 = pipelined
+        # triples; copy "s" = pack kernel stores into the peer
         # inbox, "e" = DMA engine copy (the transports then need fewer CUs: also tried with a quarter of the reserve)
         copies = ["s", "e"] if colo and args.colo_copy == "auto" else ["e" if args.colo_copy == "engine" else "s"]
         cands = []
@@ -681,6 +682,8 @@ def main(argv=None):
             # pack-kernel stores
             if cp == "s" and model.can_pipeline():
                 cands += [(3, r0, cp), (3, max(1, r0 // 2), cp), (3, 2 * r0, cp)]
+            if cp == "s" and model.can_pipeline_triples():  # mode 4: pipelined triples
+                cands += [(4, r0, cp), (4, max(1, r0 // 2), cp), (4, 2 * r0, cp)]
             cands += [(1, r0, cp), (1, max(1, r0 // 2), cp), (1, 2 * r0, cp), (2, r0, cp), (0, r0, cp)]
             if cp == "e":
                 cands.append((1, max(1, r0 // 4), cp))

@@ -116,8 +116,11 @@ public:
   // xGMI stores and unpack run beside the rest of this sweep on the CUs it leaves free, and no sweep is split into
   // interior and slabs. Needs remote halos along z only, the whole-row kernel and fused co-located transports.
   void set_overlap_mode(int mode);
-  int overlap_mode() const { return pipelined_ ? 3 : (overlap_ ? (slabsAfter_ ? 2 : 1) : 0); }
+  int overlap_mode() const { return pipelined3_ ? 4 : (pipelined_ ? 3 : (overlap_ ? (slabsAfter_ ? 2 : 1) : 0)); }
   bool can_pipeline() const { return pipeOk_; }
+  // 4 = pipelined triples: fused triples that publish their boundary z planes early, each depth-3 exchange gated on
+  // them and running beside the rest of the sweep
+  bool can_pipeline_triples() const { return pipeOk_ && triplesOk_; }
   // CUs the overlapped sweeps leave to the transport kernels (StencilTune::x2reserve); synchronizes first
   void set_comm_reserve(int cus);
   int comm_reserve() const { return cfg_.tune.x2reserve; }
@@ -149,6 +152,8 @@ private:
   bool slabsAfter_ = false; // overlap mode 2 (see set_overlap_mode)
   bool pipeOk_ = false;      // overlap mode 3 possible (see init)
   bool pipelined_ = false;   // overlap mode 3
+  bool pipelined3_ = false;  // overlap mode 4
+  int pubDepth_ = 2;         // boundary z planes a sweep publishes at each face (the exchange's z depth)
   bool lastPublished_ = false; // the last enqueued sweep published its boundary planes into pubCounter_
   uint64_t *pubCounter_ = nullptr; // device word (uncached), cumulative boundary cells published
   uint64_t pubTotal_ = 0;          // its value once every published sweep so far is done

@@ -800,6 +800,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_overlap_mode", &StencilModel::set_overlap_mode, py::call_guard<py::gil_scoped_release>())
       .def("overlap_mode", &StencilModel::overlap_mode)
       .def("can_pipeline", &StencilModel::can_pipeline)
+      .def("can_pipeline_triples", &StencilModel::can_pipeline_triples)
       .def("set_comm_reserve", &StencilModel::set_comm_reserve, py::call_guard<py::gil_scoped_release>())
       .def("comm_reserve", &StencilModel::comm_reserve)
       .def("set_overlap", &StencilModel::set_overlap, py::call_guard<py::gil_scoped_release>())

@@ -50,7 +50,9 @@ __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<float> &a, uint32
     const uint32_t qq = lb / cm, col = lb % cm;
     r.s = col * nzt + qq * nzt / P;
     r.e = col * nzt + (qq + 1) * nzt / P;
-    r.odd = (qq & 1) != 0;
+    // publishing boundary planes (a.pub): the first part marches up from the low z face and the last one down
+    // from the high face, so both faces' planes come out in the first steps of the sweep
+    r.odd = a.pub != nullptr ? (qq + 1 == P || (qq != 0 && (qq & 1) != 0)) : (qq & 1) != 0;
     const uint64_t LW = uint64_t(ncols - cm) * nzt;
     r.s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
     r.e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
@@ -111,7 +113,11 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
   auto body = [&](auto roleTag) {
     constexpr int R = decltype(roleTag)::value;
     bool odd = sg.odd;
-    for (int pass = 0; pass < 2; ++pass) {
+    const bool pubOrder = a.pub != nullptr;
+    for (int pp = 0; pp < 2; ++pp) {
+      // publishing: the leftover row groups' short second segments first (their face planes would otherwise come
+      // out last), the main lockstep segment in its fixed direction
+      const int pass = pubOrder ? 1 - pp : pp;
       uint32_t s = pass == 0 ? sg.s : sg.s2;
       const uint32_t e = pass == 0 ? sg.e : sg.e2;
       while (s < e) { // block-uniform
@@ -121,8 +127,11 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
         s += uint32_t(nzs);
         const int zs = a.loz + zo;
         const int ze = zs + nzs;
-        const bool down = odd != (a.flip != 0);
-        odd = !odd;
+        bool down = pass == 0 && sg.odd;
+        if (!pubOrder) {
+          down = odd != (a.flip != 0);
+          odd = !odd;
+        }
         const int yblk = a.loy + YO * int(by);
         const int y = yblk - 3 + w;
         if (yblk >= a.hiy) continue;
@@ -357,7 +366,17 @@ stencil7x3_row_kernel(StencilArgs<float> a) {
               if constexpr (R >= 1 && !EARLYW) us[nbuf][w][h][lane] = U1a[h];
               if constexpr (R >= 2 && !EARLYW) vs[nbuf][w][h][lane] = U2a[h];
             }
+            // boundary-plane publication (block-uniform, as the pairs): every wave's stores of output plane z
+            // complete before the barrier, then one thread writes the L2 back (release) and counts the block's cells
+            const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
+            if (pubStep) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            if (pubStep && lane == 0 && w == 0) {
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+              const unsigned long long cells =
+                  (unsigned long long)(min(YO, a.hiy - yblk)) * (unsigned long long)(a.hix - a.lox);
+              __hip_atomic_fetch_add(a.pub, cells, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             buf = nbuf;
 #pragma unroll
             for (int h = 0; h < H; ++h) {
@@ -482,7 +501,18 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.gy = (ny + YO - 1) / YO;
   const void *kern = (const void *)stencil7x3_row_kernel<NW, PF, KIND, CONTIG, VAR>;
   const int64_t cols = a.gy;
-  const int64_t slots = x3_resident_blocks(kern, 64 * NW);
+  const int64_t resident = x3_resident_blocks(kern, 64 * NW);
+  // CUs left to the transport kernels running beside the sweep (pipelined triples: the gated exchange)
+  int cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dom.gpu()) != hipSuccess) cus = 256;
+  const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
+  const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
+  if (tune.publish) {
+    a.pub = reinterpret_cast<unsigned long long *>(tune.publish);
+    a.pubLo = a.loz + tune.publishDepth;
+    a.pubHi = a.hiz - tune.publishDepth;
+    a.flip = 0; // fixed march directions (x3_segments)
+  }
   a.seg = 1;
   uint32_t blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 24)));
   X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);

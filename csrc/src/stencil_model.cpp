@@ -10,6 +10,7 @@ namespace stencil {
 
 StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::ProcGroup> pg) : cfg_(cfg) {
   dd_.reset(new DistributedDomain(cfg.size.x, cfg.size.y, cfg.size.z, pg));
+  pubDepth_ = cfg.temporal >= 3 ? 3 : 2;
   Radius r = Radius::constant(0);
   if (cfg.allDirections) {
     r = Radius::constant(cfg.radius);
@@ -168,12 +169,13 @@ void StencilModel::init() {
     const auto li = dd_->get_local_interior(2);
     const Rect3 c = doms0[0].get_compute_region();
     bool ok = li[0].lo.x == c.lo.x && li[0].hi.x == c.hi.x && li[0].lo.y == c.lo.y && li[0].hi.y == c.hi.y &&
-              dd_->gated_send_supported(pairTune_.wrap) && c.extent().z >= 8;
+              dd_->gated_send_supported(pairTune_.wrap) && c.extent().z >= 4 * pubDepth_;
     for (int64_t q = 0; q < doms0[0].num_data() && ok; ++q) ok = stencil7x2_row_kernel_used(doms0[0], q, c, pairTune_);
     if (ok) {
       pipeOk_ = true;
       const Dim3 e = c.extent();
-      pubCells_ = uint64_t(e.x) * uint64_t(e.y) * uint64_t(std::min<int64_t>(e.z, 4)) * uint64_t(doms0[0].num_data());
+      pubCells_ = uint64_t(e.x) * uint64_t(e.y) * uint64_t(std::min<int64_t>(e.z, 2 * pubDepth_)) *
+                  uint64_t(doms0[0].num_data());
       doms0[0].set_device();
       HIP_CHECK(hipExtMallocWithFlags((void **)&pubCounter_, 256, hipDeviceMallocUncached));
       HIP_CHECK(hipMemset(pubCounter_, 0, 256));
@@ -320,7 +322,7 @@ void StencilModel::step() {
   dd_->swap();
   // the next exchange must follow this step's compute; in single-stream mode stream order already guarantees it
   const bool device = !compute_.empty();
-  const bool singleStream = device && !overlap_ && doms.size() == 1;
+  const bool singleStream = device && !overlap_ && !pipelined3_ && doms.size() == 1;
   if (device && !singleStream)
     for (size_t di = 0; di < doms.size(); ++di) dd_->record_ready(di, compute_[di]);
   ++steps_;
@@ -341,7 +343,7 @@ void StencilModel::run(int iters) {
     iters -= gsteps;
   }
   const bool device = !compute_.empty();
-  const bool singleStream = device && !overlap_ && doms.size() == 1;
+  const bool singleStream = device && !overlap_ && !pipelined3_ && doms.size() == 1;
   while (triples_ && iters >= 3) {
     enqueue_step(3);
     dd_->swap();
@@ -407,7 +409,7 @@ void StencilModel::enqueue_step(int k) {
     const bool pub = dd_->gated_send_supported(pairTune_.wrap);
     if (pub) {
       ti.publish = pubCounter_;
-      ti.publishDepth = 2;
+      ti.publishDepth = pubDepth_; // the exchange reads this many planes at each z face
       // fixed march directions: the lockstep schedule's outer z parts march away from the domain's z faces, so the
       // boundary planes the next exchange waits for come out at the start of every sweep; the per-pair flip
       // (alternateZ) would write them last on every other pair and leave that exchange nothing to overlap
@@ -448,6 +450,32 @@ void StencilModel::enqueue_step(int k) {
         stencil7x2_apply_exterior(doms[di], q, pairInteriors_[di], cfg_.kind, sph_, s, pairTune_);
       exteriorDone_[di].record(s);
       exteriorDone_[di].wait_on(compute_[di]);
+    }
+    return;
+  }
+  if (k == 3 && pipelined3_) {
+    // pipelined triples (mode 4): as the pipelined pairs, this sweep's exchange was gated on the previous sweep's
+    // boundary planes and ran beside the rest of that sweep; the sweep waits for it, leaves x2reserve CUs to the
+    // next gated exchange and publishes its own first / last 3 z planes early (fixed march directions)
+    const bool gate = gateOk && dd_->gated_send_supported(pairTune_.wrap);
+    if (gate) dd_->set_send_gate(pubCounter_, pubTotal_);
+    dd_->exchange_async(nullptr, pairTune_.wrap);
+    dd_->wait_exchange(0, compute_[0]);
+    StencilTune ti = pairTune_;
+    ti.reserveCUs = cfg_.tune.x2reserve;
+    const Rect3 c = doms[0].get_compute_region();
+    const bool pub = dd_->gated_send_supported(pairTune_.wrap);
+    if (pub) {
+      ti.publish = pubCounter_;
+      ti.publishDepth = pubDepth_;
+      ti.alternateZ = false;
+    }
+    for (int64_t q = 0; q < doms[0].num_data(); ++q)
+      STENCIL_REQUIRE(stencil7x3_apply(doms[0], q, c, cfg_.kind, sph_, compute_[0].get(), ti),
+                      "fused triple not supported for quantity " << q);
+    if (pub) {
+      pubTotal_ += pubCells_;
+      lastPublished_ = true;
     }
     return;
   }
@@ -558,12 +586,16 @@ void StencilModel::set_overlap(bool on) {
 }
 
 void StencilModel::set_overlap_mode(int mode) {
-  STENCIL_REQUIRE(mode >= 0 && mode <= 3, "overlap mode " << mode);
+  STENCIL_REQUIRE(mode >= 0 && mode <= 4, "overlap mode " << mode);
   STENCIL_REQUIRE(mode != 3 || pipeOk_, "overlap mode 3 (pipelined pairs) is not possible for this model");
+  STENCIL_REQUIRE(mode != 4 || can_pipeline_triples(), "overlap mode 4 (pipelined triples) is not possible for this model");
   if (mode == overlap_mode()) return;
-  set_overlap(mode != 0);
+  set_overlap(mode != 0 && mode != 4);
   slabsAfter_ = mode == 2;
   pipelined_ = mode == 3;
+  pipelined3_ = mode == 4;
+  // the gated exchanges of modes 3 / 4 run beside the sweep on the CUs it leaves free
+  dd_->set_comm_max_blocks(mode != 0 ? cfg_.tune.x2reserve : 0);
 }
 
 void StencilModel::set_comm_reserve(int cus) {
@@ -573,7 +605,7 @@ void StencilModel::set_comm_reserve(int cus) {
   cfg_.tune.x2reserve = cus;
   pairTune_.x2reserve = cus;
   stepTune_.x2reserve = cus;
-  if (overlap_) dd_->set_comm_max_blocks(cus);
+  if (overlap_ || pipelined3_) dd_->set_comm_max_blocks(cus);
   if (confinedSelf_) dd_->set_translate_max_blocks(cus);
 }
 

@@ -110,6 +110,10 @@ class StencilModel:
         """Overlap mode 3 is possible: one device, remote halos along z only, whole-row kernel, fused IPC stores."""
         return self._m.can_pipeline()
 
+    def can_pipeline_triples(self) -> bool:
+        """True when overlap mode 4 is possible: fused triples whose boundary z planes gate the next depth-3 exchange."""
+        return self._m.can_pipeline_triples()
+
     def overlap_mode(self) -> int:
         return self._m.overlap_mode()
 

@@ -884,19 +884,23 @@ def test_colocated_ipc_overlap_toggle_two_ranks():
 
 
 # cuts follow the interface cost (NodePartition): 4*Y*Z for an x cut against 2*X*Z (y, cost 4,2,3) / 2*X*Y (z, 4,3,2)
-@pytest.mark.parametrize("kind,size,cost,ranks", [("astaroth", "512,264,16", "4,2,3", 2), ("astaroth", "512,16,300", "4,3,2", 2),
-                                                  ("jacobi", "512,300,128", "4,2,3", 2),
-                                                  ("astaroth", "512,600,24", "4,2,3", 4)])
-def test_triples_across_ranks(kind, size, cost, ranks):
+# modes 3 / 4 (pipelined) need every remote halo along z
+@pytest.mark.parametrize("kind,size,cost,ranks,mode", [
+    ("astaroth", "512,264,16", "4,2,3", 2, "0"), ("jacobi", "512,300,128", "4,2,3", 2, "0"),
+    ("astaroth", "512,600,24", "4,2,3", 4, "0"),
+    *[("astaroth", "512,16,300", "4,3,2", 2, md) for md in ("0", "4", "3")],
+    ("jacobi", "512,192,600", "4,3,2", 2, "4"), ("astaroth", "512,16,600", "4,3,2", 4, "4")])
+def test_triples_across_ranks(kind, size, cost, ranks, mode):
     """Fused triples with remote halos (multi-GPU layout rehearsed by ranks sharing one GPU over HIP IPC): x wrapped
     in-kernel, the cut axes read the 3-deep halos of one exchange per three steps. The overlapped pairs are the
-    auto default; set_overlap_mode(0) (the bench's whole-region candidate) switches to triples. Bitwise vs the
-    oracle through single steps, pairs and triples."""
+    auto default; set_overlap_mode(0) (the bench's whole-region candidate) switches to triples, mode 4 to pipelined
+    triples (each depth-3 exchange gated on the previous triple's published boundary planes), mode 3 to pipelined
+    pairs publishing 3 planes per face. Bitwise vs the oracle through single steps, pairs and triples."""
     outs = run_ranks(ranks, WORKER, ["jacobi", size],
                      env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
                                 "MP_TEMPORAL": "3", "MP_KIND": kind, "MP_RANDOM": "1", "MP_AXIS_COST": cost,
-                                "MP_TOGGLE_OVERLAP": "1", "MP_TOGGLE_MODES": "0", "MP_TOGGLE_STEPS": "10",
-                                "MP_EXPECT_TRIPLES": "1"})
+                                "MP_TOGGLE_OVERLAP": "1", "MP_TOGGLE_MODES": mode, "MP_TOGGLE_STEPS": "10",
+                                "MP_EXPECT_TRIPLES": "0" if mode == "3" else "1"})
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out, out[-2000:]
@@ -1020,6 +1024,24 @@ def test_headline_two_rank_exact_grid_bitwise(mode):
         assert rc == 0, out[-3000:]
         assert "jacobi bad 0" in out and "dim (1, 1, 2)" in out.replace("Dim3", ""), out[-2000:]
         assert f"overlap {mode[-1] != '0'}" in out, out[-2000:]
+
+
+@pytest.mark.parametrize("mode", ["0", "4", "3", "1", "4304"])
+def test_headline_two_rank_triples_bitwise(mode):
+    """The same 2-GPU weak-scaling grid with temporal=3 (bench.py's default): depth-3 halos, whole-region fused
+    triples (0), pipelined triples (4: each triple publishes its first / last 3 z planes early, the next depth-3
+    exchange is gated on them), pipelined pairs publishing 3 planes (3), overlapped pairs (1), and switching
+    4 -> 3 -> 0 -> 4; bitwise vs the torch oracle (on the GPU) after 1 + 8 + 16 steps."""
+    outs = run_ranks(2, WORKER, ["jacobi", "512,512,1024"],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "30",
+                                "MP_TEMPORAL": "3", "MP_RANDOM": "1", "MP_PREPARE": "1", "MP_SINGLE_STEPS": "1",
+                                "MP_RUN_STEPS": "8", "MP_TOGGLE_OVERLAP": "1", "MP_TOGGLE_MODES": mode,
+                                "MP_EXPECT_TRIPLES": "1" if mode[-1] in "04" else "0"},
+                     timeout=200)
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out and "dim (1, 1, 2)" in out.replace("Dim3", ""), out[-2000:]
+        assert f"overlap {mode[-1] in '123'}" in out, out[-2000:]
 
 
 def test_smoke_entry():
