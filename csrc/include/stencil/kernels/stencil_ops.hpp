@@ -54,6 +54,7 @@ struct StencilTune {
   int x3layout = 0;       // fused triples: 1 = 8 adjacent cells per lane (one rotate per x side), 0 = chunks 256 apart
   int x3var = 7;          // fused triples: bit 0 = publish u1/u2 right after their update, bit 1 = no fences between
                           // levels, bit 2 = publish the src row right after u1 (7: 1431-1443 vs 0: 1381-1392 Gcells/s)
+  int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
   int x3pf = 1;           // fused triples: src planes of lookahead in registers (1, 2)
   bool x2early = true;    // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
                           // (row kernel 208.6 vs 216.6 us per pair, col2 226.9 vs 234.1)

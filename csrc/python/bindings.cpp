@@ -737,6 +737,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("x3var", &StencilTune::x3var)
       .def_readwrite("x2early", &StencilTune::x2early)
       .def_readwrite("x3pf", &StencilTune::x3pf)
+      .def_readwrite("x3parts", &StencilTune::x3parts)
       .def_readwrite("x2nw", &StencilTune::x2nw)
       .def_readwrite("x2row", &StencilTune::x2row)
       .def_readwrite("x2sched", &StencilTune::x2sched)

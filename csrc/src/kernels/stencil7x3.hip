@@ -524,6 +524,7 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     ls = X2Schedule();
     double best = 1e30;
     for (int64_t P = 2; P <= 8; ++P) {
+      if (tune.x3parts > 0 && P != tune.x3parts) continue;
       const int64_t cm = std::min<int64_t>(cols, slots / P);
       if (cm < 1 || nz / P < 16) continue;
       const int64_t blocksP = P * cm, left = cols - cm;
