@@ -55,6 +55,8 @@ struct StencilTune {
   int x3var = 7;          // fused triples: bit 0 = publish u1/u2 right after their update, bit 1 = no fences between
                           // levels, bit 2 = publish the src row right after u1 (7: 1431-1443 vs 0: 1381-1392 Gcells/s)
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
+  float x3sphw = 0.4f;    // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z
+                          // parts are cut per row group (0: equal parts)
   int x3pf = 1;           // fused triples: src planes of lookahead in registers (1, 2)
   bool x2early = true;    // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
                           // (row kernel 208.6 vs 216.6 us per pair, col2 226.9 vs 234.1)
@@ -102,6 +104,8 @@ struct StencilTune {
   // word, system-scope release after each such plane), so a gated exchange (DistributedDomain::set_send_gate) packs
   // the boundary planes while the rest of the sweep is still running. Other fused-pair kernels refuse it.
   uint64_t *publish = nullptr;
+  // measurement: stencil7x3 writes every block's start / end wall clock (2 x uint64 per block) here when set
+  uint64_t *blockClock = nullptr;
   int publishDepth = 0;
 };
 // the whole-row fused-pair kernel (the one that can publish its boundary planes) takes this region

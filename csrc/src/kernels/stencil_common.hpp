@@ -75,6 +75,7 @@ template <typename T> struct StencilArgs {
   // fused triples: rows past the region's y end store here instead of being skipped (same memory ops on every path)
   char *sink;
   int early; // stencil7x2 row / col2: publish the src and u1 rows right after the u1 update, not before the barrier
+  unsigned long long *clk; // stencil7x3 measurement: per-block start / end wall clock (null: off)
 };
 
 // periodic image of raw coordinate c along axis ax (identity unless the axis wraps)

@@ -10,3 +10,7 @@ for y in 510 512; do run j$y 512 $y 512 jacobi; run a$y 512 $y 512 astaroth; don
 for i in 1 2 3; do
   timeout -k 10 120 python bench.py --steps 20 --warmup 5 > $O/drv_$i.json 2> $O/drv_$i.err || exit 1
 done
+for c in "jacobi 512" "jacobi 510"; do
+  set -- $c
+  timeout -k 10 120 python scripts/mi355x/lab/x3_blocks.py $1 $2 > $O/blocks_$1_$2.txt 2>&1 || exit 1
+done
