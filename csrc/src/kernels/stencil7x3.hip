@@ -197,13 +197,16 @@ stencil7x3_row_kernel(StencilArgs<float> a, X3Bounds zbounds) {
         // sweep's longest, which the host evens out with sphere-weighted z parts (x3sphw, profiles/r5/ao)
         auto sphere_row = [&](const RowSph &rs, NV(&o)[H]) {
           if (KIND == 0 && rs.hit) {
+            // (x - c)^2 + d < r1sq <=> (x - c)^2 < r1sq - d: the row's bound is one scalar per sphere, the per-cell
+            // squared distances loop invariants, so a cell costs a compare and a select per sphere
+            const int Dh = a.r1sq - rs.dh, Dc = a.r1sq - rs.dc;
 #pragma unroll
             for (int h = 0; h < H; ++h)
 #pragma unroll
               for (int k = 0; k < V; ++k) {
                 const int x = xb + h * CS + k;
-                const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
-                const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+                const bool hot = (x - a.hx) * (x - a.hx) < Dh;
+                const bool cold = (x - a.cx) * (x - a.cx) < Dc;
                 o[h][k] = hot ? T(1) : (cold ? T(0) : o[h][k]);
               }
           }
