@@ -122,8 +122,8 @@ __global__ __launch_bounds__(256) void stencil7_kernel(StencilArgs<T> a) {
 #pragma unroll
           for (int e = 0; e < V; ++e) {
             const int x = xb + e;
-            const bool hot = (x - a.hx) * (x - a.hx) + dyzh < r1sq;
-            const bool cold = (x - a.cx) * (x - a.cx) + dyzc < r1sq;
+            const bool hot = (x - a.hx) * (x - a.hx) < r1sq - dyzh;
+            const bool cold = (x - a.cx) * (x - a.cx) < r1sq - dyzc;
             out[e] = hot ? T(1) : (cold ? T(0) : out[e]);
           }
         }
@@ -435,8 +435,8 @@ __global__ __launch_bounds__(64 * NW, (TY <= 4 && sizeof(T) == 4 ? 4 : 1)) void 
 #pragma unroll
           for (int e = 0; e < V; ++e) {
             const int x = xb + e;
-            const bool hot = (x - a.hx) * (x - a.hx) + dyzh < r1sq;
-            const bool cold = (x - a.cx) * (x - a.cx) + dyzc < r1sq;
+            const bool hot = (x - a.hx) * (x - a.hx) < r1sq - dyzh;
+            const bool cold = (x - a.cx) * (x - a.cx) < r1sq - dyzc;
             out[e] = hot ? T(1) : (cold ? T(0) : out[e]);
           }
         }

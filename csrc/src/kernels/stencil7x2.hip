@@ -157,8 +157,8 @@ __attribute__((amdgpu_waves_per_eu(NW == 12 ? 3 : 4, NW == 12 ? 3 : 4))) void st
     return r;
   };
   auto fix = [&](const RowSph &rs, int x, T v) -> T {
-    const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
-    const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+    const bool hot = (x - a.hx) * (x - a.hx) < a.r1sq - rs.dh;
+    const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - rs.dc;
     return hot ? T(1) : (cold ? T(0) : v);
   };
   // S at this wave's row chunk `cm`: x-neighbours by DPP lane shifts (+ edge scalars at the wave edges)
@@ -493,8 +493,8 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
       hot = unsigned(x - rs.hlo) <= unsigned(rs.hhi - rs.hlo);
       cold = unsigned(x - rs.clo) <= unsigned(rs.chi - rs.clo);
     } else {
-      hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
-      cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+      hot = (x - a.hx) * (x - a.hx) < a.r1sq - rs.dh;
+      cold = (x - a.cx) * (x - a.cx) < a.r1sq - rs.dc;
     }
     return hot ? T(1) : (cold ? T(0) : v);
   };
@@ -796,8 +796,8 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
     return r;
   };
   auto fix = [&](const RowSph &rs, int x, T v) -> T {
-    const bool hot = (x - a.hx) * (x - a.hx) + rs.dh < a.r1sq;
-    const bool cold = (x - a.cx) * (x - a.cx) + rs.dc < a.r1sq;
+    const bool hot = (x - a.hx) * (x - a.hx) < a.r1sq - rs.dh;
+    const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - rs.dc;
     return hot ? T(1) : (cold ? T(0) : v);
   };
   // S of the wave's column: x-neighbours by lane rotates, eL / eR beyond the column ends
