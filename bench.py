@@ -387,6 +387,7 @@ def build_args(argv=None):
     ap.add_argument("--x2early", type=int, default=1, help="fused pairs: publish src/u1 rows right after the u1 update")
     ap.add_argument("--x3sphw", type=float, default=0.4,
                     help="fused triples (Jacobi): sphere-row weight of the per-row-group z part boundaries (0: equal parts)")
+    ap.add_argument("--x2sphw", type=float, default=0.15, help="fused pairs (Jacobi): sphere-row weight of the z parts")
     ap.add_argument("--x3pf", type=int, default=1, help="fused triples: src planes of lookahead (1, 2)")
     ap.add_argument("--x3var", type=int, default=7,
                     help="fused triples: bit 0 = early u1/u2 LDS writes, bit 1 = no fences between levels, bit 2 = early src row")
@@ -570,6 +571,7 @@ def main(argv=None):
     tune.x3var = args.x3var
     tune.x3pf = args.x3pf
     tune.x3sphw = args.x3sphw
+    tune.x2sphw = args.x2sphw
     tune.x2early = bool(args.x2early)
     tune.x2row = args.x2row
     tune.zchunk = args.zchunk
@@ -753,7 +755,7 @@ def main(argv=None):
         "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
         "x_face_lines": bool(args.x_face_lines), "shared_halo_line": args.shared_halo_line == 1,
         "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
-        "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x3sched": args.x3sched, "x3layout": args.x3layout, "x3var": args.x3var, "x3pf": args.x3pf, "x3sphw": args.x3sphw, "x2early": args.x2early, "x2row": args.x2row, "x2sched": args.x2sched,
+        "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x3sched": args.x3sched, "x3layout": args.x3layout, "x3var": args.x3var, "x3pf": args.x3pf, "x3sphw": args.x3sphw, "x2sphw": args.x2sphw, "x2early": args.x2early, "x2row": args.x2row, "x2sched": args.x2sched,
         "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": 3 if model.temporal_triples() else (2 if model.temporal_blocking() else 1),
         "wrap_axes": wrap_axes, "backend": "host" if args.cpu else "device",
         "transport": {"inbox": str(dd.transport_options().inbox).split(".")[-1].lower(),

@@ -57,6 +57,7 @@ struct StencilTune {
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
   float x3sphw = 0.4f;    // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z
                           // parts are cut per row group (0: equal parts)
+  float x2sphw = 0.15f;   // fused pairs (Jacobi, row / col2 kernels): sphere weight of the z parts (r5/at, r5/au)
   int x3pf = 1;           // fused triples: src planes of lookahead in registers (1, 2)
   bool x2early = true;    // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
                           // (row kernel 208.6 vs 216.6 us per pair, col2 226.9 vs 234.1)

@@ -739,6 +739,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("x3pf", &StencilTune::x3pf)
       .def_readwrite("x3parts", &StencilTune::x3parts)
       .def_readwrite("x3sphw", &StencilTune::x3sphw)
+      .def_readwrite("x2sphw", &StencilTune::x2sphw)
       .def_property(
           "block_clock", [](const StencilTune &t) { return reinterpret_cast<uintptr_t>(t.blockClock); },
           [](StencilTune &t, uintptr_t p) { t.blockClock = reinterpret_cast<uint64_t *>(p); })

@@ -329,7 +329,7 @@ struct X2Segs {
 };
 template <typename T>
 __device__ __forceinline__ X2Segs x2_segments(const StencilArgs<T> &a, uint32_t lb, uint32_t nb, uint32_t ncols,
-                                              uint32_t nzt) {
+                                              uint32_t nzt, const ZPartBounds *B = nullptr, bool useB = true) {
   X2Segs r{0, 0, 0, 0, false};
   if (a.seg == 3) { // rounds (x2_pass): parts alternate their z direction as in seg 2
     r.odd = ((lb / (nb / uint32_t(a.zparts))) & 1) != 0;
@@ -340,8 +340,13 @@ __device__ __forceinline__ X2Segs x2_segments(const StencilArgs<T> &a, uint32_t 
     const uint32_t cm = nb / P;
     // part-major: consecutive blocks take y-adjacent columns of one part (column-major: 1146 vs 1164 Gcells/s, r2s3)
     const uint32_t qq = lb / cm, col = lb % cm;
-    r.s = col * nzt + qq * nzt / P;
-    r.e = col * nzt + (qq + 1) * nzt / P;
+    uint32_t zlo = qq * nzt / P, zhi = (qq + 1) * nzt / P;
+    if (useB && B && B->on && col < uint32_t(kZPartMaxCols)) { // sphere-weighted parts (Jacobi, sphere_part_bounds)
+      zlo = qq > 0 ? uint32_t(B->zb[col][qq - 1]) : 0;
+      zhi = qq + 1 < P ? uint32_t(B->zb[col][qq]) : nzt;
+    }
+    r.s = col * nzt + zlo;
+    r.e = col * nzt + zhi;
     r.odd = (qq & 1) != 0;
     const uint64_t LW = uint64_t(ncols - cm) * nzt;
     r.s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
@@ -380,7 +385,7 @@ __device__ __forceinline__ bool x2_pass(const StencilArgs<T> &a, const X2Segs &s
 
 template <int NW, int PF, int KIND, int H = 2, bool RAG = false, bool TL = false>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
-stencil7x2_row_kernel(StencilArgs<float> a) {
+stencil7x2_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
   using T = float;
   using NV = nf4;
   constexpr int V = 4;          // H = chunks per lane
@@ -409,7 +414,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
   // z-march direction alternates between neighbouring segments (their shared boundary planes meet in cache); in the
   // part-major lockstep order it alternates by part, so y-adjacent blocks march together
-  const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gy), nzt);
+  const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gy), nzt, &zbounds);
   uint32_t s = 0, e = 0;
   bool odd = sg.odd;
   for (int pass = 0; x2_pass(a, sg, pass, lb, nb, uint32_t(a.gy), nzt, s, e); ++pass) {
@@ -708,7 +713,7 @@ stencil7x2_row_kernel(StencilArgs<float> a) {
 // as everywhere: bitwise equal to two single steps.
 template <typename T, int NW, int PF, int KIND, int WRAP>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void stencil7x2_col2_kernel(
-    StencilArgs<T> a) {
+    StencilArgs<T> a, ZPartBounds zbounds) {
   using NV = typename Vec16<T>::native;
   using P2 = typename Pk<T>::t;
   constexpr int V = int(16 / sizeof(T)), H = 2; // chunks per lane
@@ -728,7 +733,8 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
   // lockstep parts as the whole-row kernel (y-adjacent columns of one 512-cell column strip are consecutive unless
   // xfast): 1024x512x256, 128 columns, marches 2 parts on 256 blocks
-  const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gx) * uint32_t(a.gy), nzt);
+  // (no pointer select on the kernel argument: that made the compiler copy it to scratch, 1.5 KB per lane)
+  const X2Segs sg = x2_segments(a, lb, nb, uint32_t(a.gx) * uint32_t(a.gy), nzt, &zbounds, a.gx == 1);
   uint32_t s = 0, e = 0;
   bool odd = sg.odd;
   for (int pass = 0; x2_pass(a, sg, pass, lb, nb, uint32_t(a.gx) * uint32_t(a.gy), nzt, s, e); ++pass) {
@@ -1286,7 +1292,10 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
     blocks = uint32_t(cols * a.gz);
   }
   dom.set_device();
-  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG, TL>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  ZPartBounds zb{};
+  zb.on = 0;
+  if (KIND == 0 && a.seg == 2) sphere_part_bounds(zb, a, int64_t(blocks) / a.zparts, a.zparts, NW, YO, 2, tune.x2sphw);
+  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG, TL>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   HIP_CHECK(hipGetLastError());
   return true;
 }
@@ -1338,7 +1347,11 @@ static void apply_x2col2_t(const LocalDomain &dom, int64_t qi, const Rect3 &regi
     blocks = uint32_t(cols * a.gz);
   }
   dom.set_device();
-  hipLaunchKernelGGL((stencil7x2_col2_kernel<T, NW, PF, KIND, WRAP>), dim3(blocks), dim3(64, NW), 0, stream, a);
+  ZPartBounds zb{};
+  zb.on = 0;
+  if (KIND == 0 && a.seg == 2 && a.gx == 1)
+    sphere_part_bounds(zb, a, int64_t(blocks) / a.zparts, a.zparts, NW, YO, 2, tune.x2sphw);
+  hipLaunchKernelGGL((stencil7x2_col2_kernel<T, NW, PF, KIND, WRAP>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   HIP_CHECK(hipGetLastError());
 }
 

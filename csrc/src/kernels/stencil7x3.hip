@@ -39,28 +39,19 @@
 
 namespace stencil {
 
-// per-column z part boundaries (plane offsets from the region's first plane) for the lockstep parts: the Jacobi
-// sweep weights the planes where a row group's rows cross the spheres (their per-cell tests make those steps ~1.75x
-// as long, profiles/r5/ak), so no block holds all of a sphere's planes; on = 0: equal parts
-constexpr int kX3MaxCols = 256, kX3MaxParts = 4;
-struct X3Bounds {
-  int on;
-  uint16_t zb[kX3MaxCols][kX3MaxParts - 1];
-};
-
 // (column, plane) segment of a block: lockstep parts as the fused pairs (x2_segments), kept local to this file
 struct X3Seg {
   uint32_t s, e, s2, e2;
   bool odd;
 };
-__device__ __forceinline__ X3Seg x3_segments(const StencilArgs<float> &a, const X3Bounds &B, uint32_t lb, uint32_t nb,
+__device__ __forceinline__ X3Seg x3_segments(const StencilArgs<float> &a, const ZPartBounds &B, uint32_t lb, uint32_t nb,
                                              uint32_t ncols, uint32_t nzt) {
   X3Seg r{0, 0, 0, 0, false};
   if (a.seg == 2) {
     const uint32_t P = uint32_t(a.zparts), cm = nb / P;
     const uint32_t qq = lb / cm, col = lb % cm;
     uint32_t zlo = qq * nzt / P, zhi = (qq + 1) * nzt / P;
-    if (B.on && col < uint32_t(kX3MaxCols)) {
+    if (B.on && col < uint32_t(kZPartMaxCols)) {
       zlo = qq > 0 ? uint32_t(B.zb[col][qq - 1]) : 0;
       zhi = qq + 1 < P ? uint32_t(B.zb[col][qq]) : nzt;
     }
@@ -83,7 +74,7 @@ __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<float> &a, const 
 
 template <int NW, int PF, int KIND, bool CONTIG, int VAR>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
-stencil7x3_row_kernel(StencilArgs<float> a, X3Bounds zbounds) {
+stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
   using T = float;
   using NV = nf4;
   constexpr int V = 4, H = 2;
@@ -571,48 +562,10 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     a.zparts = ls.parts;
     blocks = uint32_t(ls.blocks);
   }
-  X3Bounds zb{};
+  ZPartBounds zb{};
   zb.on = 0;
-  const int64_t cm = a.seg == 2 ? int64_t(blocks) / a.zparts : 0;
-  if (KIND == 0 && a.r1sq > 0 && a.seg == 2 && a.zparts <= kX3MaxParts && cm <= kX3MaxCols && tune.x3sphw > 0 &&
-      nz < 65536) {
-    // plane weights per row group: 1 + x3sphw * (rows of the block's 12 that cross a sphere there) / 12
-    const int P = a.zparts, R1 = a.r1sq;
-    auto isqrt_below = [](int d) { // largest h >= 0 with h * h < d (d > 0)
-      int h = int(std::sqrt(double(d - 1)));
-      while (h > 0 && h * h > d - 1) --h;
-      while ((h + 1) * (h + 1) <= d - 1) ++h;
-      return h;
-    };
-    std::vector<double> w(static_cast<size_t>(nz));
-    bool any = false;
-    for (int64_t col = 0; col < cm; ++col) {
-      std::fill(w.begin(), w.end(), 12.0);
-      const int yblk = a.loy + YO * int(col);
-      for (int r = 0; r < NW; ++r) {
-        const int y = yblk - 3 + r;
-        for (const auto &c : {std::make_pair(a.hy, a.hz), std::make_pair(a.cy, a.cz)}) {
-          const int d = R1 - (y - c.first) * (y - c.first);
-          if (d <= 0) continue;
-          const int h = isqrt_below(d);
-          for (int z = std::max(a.loz, c.second - h); z <= std::min(a.hiz - 1, c.second + h); ++z) {
-            w[size_t(z - a.loz)] += tune.x3sphw;
-            any = true;
-          }
-        }
-      }
-      double total = 0;
-      for (double v : w) total += v;
-      double acc = 0;
-      int q = 1;
-      for (int z = 0; z < nz && q < P; ++z) {
-        acc += w[size_t(z)];
-        while (q < P && acc >= total * q / P) zb.zb[col][(q++) - 1] = uint16_t(z + 1);
-      }
-      while (q < P) zb.zb[col][(q++) - 1] = uint16_t(nz);
-    }
-    zb.on = any ? 1 : 0;
-  }
+  if (KIND == 0 && a.seg == 2)
+    sphere_part_bounds(zb, a, int64_t(blocks) / a.zparts, a.zparts, NW, YO, 3, tune.x3sphw);
   dom.set_device();
   a.sink = x3_sink(dom.gpu(), false);
   a.clk = reinterpret_cast<unsigned long long *>(tune.blockClock);

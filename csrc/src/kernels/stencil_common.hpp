@@ -1,4 +1,8 @@
 #pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
 // Private device helpers shared by the 7-point stencil kernels (stencil7.hip, stencil7x2.hip).
 #include <hip/hip_runtime.h>
 
@@ -198,6 +202,59 @@ __device__ __forceinline__ T sum6(T vpx, T vmx, T vpy, T vmy, T vpz, T vmz) {
     val += vpz;
   }
   return div6<T>(val);
+}
+
+// per-row-group z part boundaries (plane offsets from the region's first plane) of a lockstep fused sweep (pairs,
+// triples): the Jacobi blocks whose rows cross the hot / cold spheres pay the per-cell sphere tests on those planes
+// and set the sweep's time (profiles/r5/ak), so the host cuts each group's z range by plane weights
+// 1 + w * (the group's rows crossing a sphere at that plane) / rows; on = 0: equal parts
+constexpr int kZPartMaxCols = 256, kZPartMaxParts = 4;
+struct ZPartBounds {
+  int on;
+  uint16_t zb[kZPartMaxCols][kZPartMaxParts - 1];
+};
+// fills b for cm row groups of YO output rows, each block holding rows [yblk - rowOff, yblk - rowOff + rows)
+template <typename T>
+inline void sphere_part_bounds(ZPartBounds &b, const StencilArgs<T> &a, int64_t cm, int P, int rows, int YO,
+                               int rowOff, float w) {
+  b.on = 0;
+  const int nz = a.hiz - a.loz;
+  if (a.r1sq <= 0 || w <= 0 || P < 2 || P > kZPartMaxParts || cm > kZPartMaxCols || nz >= 65536) return;
+  auto isqrt_below = [](int d) { // largest h >= 0 with h * h < d (d > 0)
+    int h = int(std::sqrt(double(d - 1)));
+    while (h > 0 && h * h > d - 1) --h;
+    while ((h + 1) * (h + 1) <= d - 1) ++h;
+    return h;
+  };
+  std::vector<double> wz(static_cast<size_t>(nz));
+  bool any = false;
+  for (int64_t col = 0; col < cm; ++col) {
+    std::fill(wz.begin(), wz.end(), double(rows));
+    const int yblk = a.loy + YO * int(col);
+    for (int r = 0; r < rows; ++r) {
+      const int y = yblk - rowOff + r;
+      const int cy[2] = {a.hy, a.cy}, cz[2] = {a.hz, a.cz};
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        const int d = a.r1sq - (y - cy[sidx]) * (y - cy[sidx]);
+        if (d <= 0) continue;
+        const int h = isqrt_below(d);
+        for (int z = std::max(a.loz, cz[sidx] - h); z <= std::min(a.hiz - 1, cz[sidx] + h); ++z) {
+          wz[static_cast<size_t>(z - a.loz)] += w;
+          any = true;
+        }
+      }
+    }
+    double total = 0;
+    for (double v : wz) total += v;
+    double acc = 0;
+    int q = 1;
+    for (int z = 0; z < nz && q < P; ++z) {
+      acc += wz[static_cast<size_t>(z)];
+      while (q < P && acc >= total * q / P) b.zb[col][(q++) - 1] = uint16_t(z + 1);
+    }
+    while (q < P) b.zb[col][(q++) - 1] = uint16_t(nz);
+  }
+  b.on = any ? 1 : 0;
 }
 
 // hot/cold sphere override of the Jacobi app at raw (x, y, z)
