@@ -385,7 +385,7 @@ def build_args(argv=None):
     ap.add_argument("--x3sched", type=int, default=1, help="fused three-step schedule (0: the pairs', 1: lockstep)")
     ap.add_argument("--x3layout", type=int, default=0, help="fused triples: 1 = 8 adjacent cells per lane, 0 = chunks 256 apart")
     ap.add_argument("--x2early", type=int, default=1, help="fused pairs: publish src/u1 rows right after the u1 update")
-    ap.add_argument("--x3sphw", type=float, default=0.4,
+    ap.add_argument("--x3sphw", type=float, default=0.3,
                     help="fused triples (Jacobi): sphere-row weight of the per-row-group z part boundaries (0: equal parts)")
     ap.add_argument("--x2sphw", type=float, default=0.15, help="fused pairs (Jacobi): sphere-row weight of the z parts")
     ap.add_argument("--x3pf", type=int, default=1, help="fused triples: src planes of lookahead (1, 2)")

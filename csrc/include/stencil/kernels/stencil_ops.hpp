@@ -55,7 +55,7 @@ struct StencilTune {
   int x3var = 7;          // fused triples: bit 0 = publish u1/u2 right after their update, bit 1 = no fences between
                           // levels, bit 2 = publish the src row right after u1 (7: 1431-1443 vs 0: 1381-1392 Gcells/s)
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
-  float x3sphw = 0.4f;    // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z
+  float x3sphw = 0.3f;    // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z
                           // parts are cut per row group (0: equal parts)
   float x2sphw = 0.15f;   // fused pairs (Jacobi, row / col2 kernels): sphere weight of the z parts (r5/at, r5/au)
   int x3pf = 1;           // fused triples: src planes of lookahead in registers (1, 2)

@@ -213,7 +213,9 @@ struct ZPartBounds {
   int on;
   uint16_t zb[kZPartMaxCols][kZPartMaxParts - 1];
 };
-// fills b for cm row groups of YO output rows, each block holding rows [yblk - rowOff, yblk - rowOff + rows)
+// fills b for cm row groups of YO output rows, each block holding rows [yblk - rowOff, yblk - rowOff + rows); a row
+// r that crosses a sphere adds w * levels(r) / (sum of levels) to the plane's weight, levels(r) = the number of
+// updates the row's wave computes per step (min(r, rows - 1 - r, rowOff): the edge rows only load)
 template <typename T>
 inline void sphere_part_bounds(ZPartBounds &b, const StencilArgs<T> &a, int64_t cm, int P, int rows, int YO,
                                int rowOff, float w) {
@@ -228,18 +230,22 @@ inline void sphere_part_bounds(ZPartBounds &b, const StencilArgs<T> &a, int64_t 
   };
   std::vector<double> wz(static_cast<size_t>(nz));
   bool any = false;
+  double levelSum = 0;
+  for (int r = 0; r < rows; ++r) levelSum += std::min(std::min(r, rows - 1 - r), rowOff);
   for (int64_t col = 0; col < cm; ++col) {
-    std::fill(wz.begin(), wz.end(), double(rows));
+    std::fill(wz.begin(), wz.end(), 1.0);
     const int yblk = a.loy + YO * int(col);
     for (int r = 0; r < rows; ++r) {
       const int y = yblk - rowOff + r;
+      const double lw = w * std::min(std::min(r, rows - 1 - r), rowOff) / levelSum;
+      if (lw <= 0) continue;
       const int cy[2] = {a.hy, a.cy}, cz[2] = {a.hz, a.cz};
       for (int sidx = 0; sidx < 2; ++sidx) {
         const int d = a.r1sq - (y - cy[sidx]) * (y - cy[sidx]);
         if (d <= 0) continue;
         const int h = isqrt_below(d);
         for (int z = std::max(a.loz, cz[sidx] - h); z <= std::min(a.hiz - 1, cz[sidx] + h); ++z) {
-          wz[static_cast<size_t>(z - a.loz)] += w;
+          wz[static_cast<size_t>(z - a.loz)] += lw;
           any = true;
         }
       }
