@@ -231,7 +231,6 @@ def transport_sweep(st, env, args, world, rank, device, ndev, axis_cost, objecti
                 dd.set_axis_cost(st.Dim3(*cost))
                 dd.set_partition_objective(obj)
                 dd.set_plan_file("")
-                dd.set_x_halo_align(bool(args.x_halo_align))
                 dd.set_interior_align(args.interior_align)
                 dd.set_shared_halo_line(args.shared_halo_line == 1)
                 topt = st.TransportOptions()
@@ -370,57 +369,22 @@ def build_args(argv=None):
     ap.add_argument("--cpu", action="store_true",
                     help="host backend, no GPU (BASELINE config 1's CPU path; the CPU tests of this script)")
     ap.add_argument("--exchange-iters", type=int, default=20)
-    ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--methods", default="all")
-    ap.add_argument("--nt", type=int, default=1, help="non-temporal stencil stores")
-    ap.add_argument("--altz", type=int, default=1,
-                    help="alternate the z-march direction every pair (128-B-aligned rows: 1276-1290 with vs 1256-1272 "
-                         "Gcells/s without, profiles/r4/q)")
-    ap.add_argument("--ty", type=int, default=2, help="rows per lane of the stencil kernel (2/4/8)")
-    ap.add_argument("--variant", type=int, default=2,
-                    help="single-step kernel variant (2: VALU LDS z-march, 8: MFMA x-line update; needs --temporal 1)")
-    ap.add_argument("--nw", type=int, default=8, help="waves per block of the stencil kernel")
-    ap.add_argument("--x2nw", type=int, default=12, help="waves per block of the fused two-step kernel (8/12/16)")
-    ap.add_argument("--x2pf", type=int, default=1, help="planes of z lookahead of the fused two-step kernel (1/2/3)")
-    ap.add_argument("--x3sched", type=int, default=1, help="fused three-step schedule (0: the pairs', 1: lockstep)")
-    ap.add_argument("--x3layout", type=int, default=0, help="fused triples: 1 = 8 adjacent cells per lane, 0 = chunks 256 apart")
-    ap.add_argument("--x2early", type=int, default=1, help="fused pairs: publish src/u1 rows right after the u1 update")
-    ap.add_argument("--x3sphw", type=float, default=0.3,
-                    help="fused triples (Jacobi): sphere-row weight of the per-row-group z part boundaries (0: equal parts)")
-    ap.add_argument("--x2sphw", type=float, default=0.15, help="fused pairs (Jacobi): sphere-row weight of the z parts")
-    ap.add_argument("--x3pf", type=int, default=1, help="fused triples: src planes of lookahead (1, 2)")
-    ap.add_argument("--x3var", type=int, default=7,
-                    help="fused triples: bit 0 = early u1/u2 LDS writes, bit 1 = no fences between levels, bit 2 = early src row")
-    ap.add_argument("--x2row", type=int, default=1,
-                    help="fused pairs: one wave per whole 512-cell row when x wraps in-kernel (fp32); 0 = columns")
-    ap.add_argument("--x2reserve", type=int, default=8,
-                    help="overlapped fused pairs: CUs the interior sweep leaves to the transport kernels")
-    ap.add_argument("--zchunk", type=int, default=0, help="z planes per block (0 = auto)")
-    ap.add_argument("--x2sched", type=int, default=1,
-                    help="fused-pair work split: 1 = balanced segments over the resident blocks, 0 = fixed z-chunks")
     ap.add_argument("--temporal", type=int, default=3,
-                    help="steps fused per sweep: 3 = fused triples S(S(S(u))) where every axis wraps in-kernel (one GPU, "
-                         "512-cell fp32 rows: the driver's command 1334-1349 vs 1270-1296 Gcells/s with pairs, "
-                         "profiles/r5/g; elsewhere pairs), 2 = temporal blocking (one depth-2 halo exchange + one fused "
-                         "S(S(u)) sweep per two steps), 1 = one exchange + sweep per step; all bitwise equal to single steps")
-    ap.add_argument("--x2xfast", type=int, default=0, help="fused-pair column order: 1 x-major, 0 y-major")
+                    help="steps fused per sweep: 3 = fused triples S(S(S(u))) (one depth-3 exchange per three steps, x "
+                         "wrapped in-kernel or read from halos; elsewhere pairs), 2 = fused pairs (one depth-2 exchange "
+                         "per two steps), 1 = one exchange + sweep per step; all bitwise equal to single steps")
     ap.add_argument("--wrap", type=int, default=1,
-                    help="fused pairs read the periodic image along axes the decomposition leaves whole (no self-copy "
+                    help="the sweeps read the periodic image along axes the decomposition leaves whole (no self-copy "
                          "of those halos); 0 = copy every halo")
     ap.add_argument("--with-exchange", choices=["auto", "on", "off"], default="auto",
                     help="after the headline, time the same steps with every halo copied (BASELINE config 2 as "
                          "defined: intra-GPU pack/unpack + compute, the reference's exchange() every iteration) -> "
                          "extra.gcells_with_exchange (auto: on unless --wrap 0 already copies every halo)")
-    ap.add_argument("--x-halo-align", type=int, default=0,
-                    help="x halos inside the interior's first / last 64-B sector (LocalDomain::set_x_halo_align): "
-                         "one sector per row end for x-face copies; every row spans one more sector")
     ap.add_argument("--shared-halo-line", type=int, default=-1,
-                    help="17-line row pitch at 512^3: row r's +x and row r+1's -x halo share one 128-B line, written once "
-                         "per row by the x-face self copies (LocalDomain::set_shared_halo_line). -1 (auto): on for the "
-                         "with-exchange model, whose sweeps read the x-halo lines (967 -> 1027 Gcells/s, "
-                         "profiles/r5/f), off for the headline (wrapped sweeps: no change; exchange-only -1 %%)")
-    ap.add_argument("--x-face-lines", type=int, default=0,
-                    help="same-GPU x-face copies as whole 128-B lines (TransportOptions.x_face_sectors)")
+                    help="row r's +x and row r+1's -x halo share one 128-B line, written once per row by the x-face "
+                         "self copies (LocalDomain::set_shared_halo_line). -1 (auto): on for the with-exchange model, "
+                         "whose sweeps read the x-halo lines (967 -> 1027 Gcells/s, profiles/r5/f), off for the headline")
     ap.add_argument("--interior-align", type=int, default=128, choices=[64, 128],
                     help="byte alignment of every row's first interior cell: 128 = whole L2 lines per 512-cell row "
                          "(1150-1194 -> 1285-1287 Gcells/s on one MI355X, profiles/r4/i/), 64 = one sector (r1-r3)")
@@ -436,16 +400,18 @@ def build_args(argv=None):
                          "(bin/jacobi3d.cu:167-169: 645^3 / 813^3 / 1024^3 at N = 2 / 4 / 8, ragged sub-domains)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="interior/exchange/exterior overlap (auto: only when some halo leaves the GPU, and then "
-                         "overlapped or whole-region pairs, whichever runs faster in the warm-up)")
+                         "overlapped, pipelined or whole-region sweeps, whichever runs fastest in the warm-up)")
+    ap.add_argument("--x2reserve", type=int, default=8,
+                    help="overlapped / pipelined sweeps: CUs left to the transport kernels (the warm-up also tries "
+                         "half and double)")
     ap.add_argument("--transport", choices=["auto", "fixed"], default="auto",
                     help="N > 1: auto = the warm-up times whole steps (max over ranks) with Colocated over uncached / "
                          "fine-grained / coarse-grained inboxes and with Rccl, and keeps the fastest for the timed loop "
-                         "(extra.transport_tuned); fixed = --methods / --inbox as given")
+                         "(config.transport_tuned); fixed = --methods / --inbox as given")
     ap.add_argument("--colo-copy", choices=["auto", "store", "engine"], default="store",
                     help="co-located (HIP IPC) halos: the pack kernel stores into the peer's inbox (store, default), or "
                          "a DMA engine copies the packed message (engine); auto: both tried in the warm-up. Engine "
-                         "copies never won on one MI355X and, with 4 ranks sharing it, ran at 0.6-1.7 s per step and "
-                         "left the store path 3.5x slower afterwards (profiles/r3/check4), so they are opt-in")
+                         "copies never won on one MI355X (profiles/r3/check4, r4/engine), so they are opt-in")
     ap.add_argument("--inbox", choices=["uncached", "fine", "coarse"], default="uncached",
                     help="memory of the co-located receive slots (TransportOptions.inbox)")
     ap.add_argument("--completion", choices=["kernel", "streamop", "ipcevent"], default="kernel",
@@ -458,6 +424,9 @@ def build_args(argv=None):
                          "Colocated -> Rccl -> Staged until every halo arrives correctly")
     ap.add_argument("--tune-steps", type=int, default=8,
                     help="steps per timed round of the transport / overlap choice (N > 1; 0 = no choice)")
+    ap.add_argument("--tune-budget", type=float, default=150.0,
+                    help="seconds of warm-up tuning (transport + overlap choice, agreed over ranks): once spent, the "
+                         "remaining candidates are skipped and the fastest timed so far is kept (config.phases_s)")
     ap.add_argument("--transport-sweep", choices=["auto", "on", "off"], default="auto",
                     help="after the headline: exchange-only GB/s of every transport set on the same decomposition, the "
                          "reference-rule cube, config 4's 8-quantity radius-3 exchange and the single-process "
@@ -469,7 +438,25 @@ def build_args(argv=None):
                          "headline line it already printed (a transport hanging on real links cannot take it)")
     ap.add_argument("--launch-timeout", type=float, default=3000,
                     help="--gpus N>1 without a launcher: seconds before the spawned ranks are stopped (0 = none)")
+    ap.add_argument("--tune", default="",
+                    help="lab switch: StencilTune fields as name=value[,name=value] (e.g. x3sphw=0.4,nontemporal=0); "
+                         "the defaults are the measured best (StencilTune in csrc/include/stencil/kernels/stencil_ops.hpp)")
     return ap.parse_args(argv)
+
+
+def make_tune(st, args):
+    """StencilTune defaults (the measured best) plus --tune overrides; the effective values go into config.tune."""
+    tune = st.StencilTune()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=", 1)
+        cur = getattr(tune, k)  # AttributeError names an unknown field
+        setattr(tune, k, type(cur)(float(v)) if not isinstance(cur, bool) else bool(int(v)))
+    return tune
+
+
+def tune_record(tune) -> dict:
+    return {k: getattr(tune, k) for k in ("x3sched", "x3parts", "x3sphw", "x2sphw", "x2early", "x2row", "x2pf",
+                                          "x2nw", "nontemporal", "alternate_z", "xcd_remap", "variant")}
 
 
 def make_transport(st, args, inbox=None):
@@ -480,7 +467,6 @@ def make_transport(st, args, inbox=None):
     topt.completion = {"kernel": topt.Completion.Kernel, "streamop": topt.Completion.StreamOp,
                        "ipcevent": topt.Completion.IpcEvent}[args.completion]
     topt.fuse_flags = bool(args.fuse_flags)
-    topt.x_face_sectors = bool(args.x_face_lines)
     if os.environ.get("STENCIL_PREFLIGHT_FORCE_FAIL"):  # rehearses the fallback (scripts): IPC probe reports failure
         topt.fail_ipc_probe = True
     if os.environ.get("STENCIL_RCCL_STALL_RANK") is not None:  # rehearses a rank stuck in RCCL creation
@@ -521,6 +507,42 @@ def arm_deadline(seconds: float, rank: int):
     return t
 
 
+class Phases:
+    """Wall time of each bench phase (config.phases_s), so the time an N-GPU run spends before its headline line is
+    known; `spent()` is the tuning clock the --tune-budget is checked against (agreed over ranks)."""
+
+    def __init__(self):
+        self.t = {}
+        self.t0 = time.perf_counter()
+        self.tune0 = None
+
+    def mark(self, name: str, since: float):
+        self.t[name] = round(self.t.get(name, 0.0) + time.perf_counter() - since, 3)
+
+    def tuning_spent(self, env) -> float:
+        if self.tune0 is None:
+            self.tune0 = time.perf_counter()
+        return env.agreed_max(time.perf_counter() - self.tune0)
+
+
+def exchange_trimean(env, dd, iters: int, xbytes: int) -> dict:
+    """The reference's exchange statistic (bin/bench_exchange.cu:39-63): each exchange()+swap() timed on its own
+    behind a barrier, the max over ranks per iteration, then the trimean (bin/statistics.cpp: (Q1 + 2 Q2 + Q3) / 4);
+    GB/s = aggregate halo bytes over all ranks / trimean."""
+    import stencil2_amd as st
+    stats = st._C.Statistics()
+    for _ in range(iters):
+        env.barrier()
+        t = time.perf_counter()
+        dd.exchange()
+        dd.swap()
+        env.sync()
+        stats.insert(env.agreed_max(time.perf_counter() - t))
+    tm = stats.trimean()
+    return {"trimean_ms": round(tm * 1e3, 4), "trimean_GBps": round(xbytes / tm / 1e9, 3) if tm > 0 else None,
+            "min_ms": round(stats.min() * 1e3, 4)}
+
+
 def main(argv=None):
     args = build_args(argv)
     rc = rank_setup(args.gpus, args.launch_timeout, sys.argv[1:] if argv is None else list(argv))
@@ -532,6 +554,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
+    ph = Phases()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -557,28 +580,9 @@ def main(argv=None):
     objective = st.PartitionObjective.MaxLink if args.partition == "maxlink" else st.PartitionObjective.Interface
     grid = weak_grid(st, args.per_gpu, n, args.grid, axis_cost, objective)
     methods = parse_methods(st, args.methods)
-
-    tune = st.StencilTune()
-    tune.nontemporal = bool(args.nt)
-    tune.alternate_z = bool(args.altz)
-    tune.ty = args.ty
-    tune.nw = args.nw
-    tune.variant = args.variant
-    tune.x2nw = args.x2nw
-    tune.x2pf = args.x2pf
-    tune.x3sched = args.x3sched
-    tune.x3layout = args.x3layout
-    tune.x3var = args.x3var
-    tune.x3pf = args.x3pf
-    tune.x3sphw = args.x3sphw
-    tune.x2sphw = args.x2sphw
-    tune.x2early = bool(args.x2early)
-    tune.x2row = args.x2row
-    tune.zchunk = args.zchunk
+    tune = make_tune(st, args)
     tune.x2reserve = args.x2reserve
-    tune.x2sched = args.x2sched
-    tune.x2xfast = args.x2xfast
-    overlap = not args.no_overlap and args.overlap != "off"
+    ph.mark("startup", ph.t0)
 
     # Transport self-test (multi-process only, DistributedDomain::set_self_test, run inside realize): a
     # coordinate-encoded field on a small probe domain with the model's radius, placement and transports is exchanged
@@ -586,10 +590,11 @@ def main(argv=None):
     # scaling run never times silently corrupted halos. An RCCL communicator that fails to form (or never forms:
     # bounded non-blocking creation) falls back to the host-staged path on every rank as well.
     def build(topt, meth, wrap_self=None, shared=None):
-        model = st.Jacobi3D(grid, gpus=[device], methods=meth, overlap=overlap, auto_overlap=args.overlap == "auto",
-                            tune=tune, temporal=args.temporal, group=pg, axis_cost=axis_cost, partition=objective,
+        model = st.Jacobi3D(grid, gpus=[device], methods=meth, overlap=args.overlap != "off",
+                            auto_overlap=args.overlap == "auto", tune=tune, temporal=args.temporal, group=pg,
+                            axis_cost=axis_cost, partition=objective,
                             wrap_self=bool(args.wrap) if wrap_self is None else wrap_self, transport=topt,
-                            self_test=bool(args.self_test) and world > 1, x_halo_align=bool(args.x_halo_align),
+                            self_test=bool(args.self_test) and world > 1,
                             interior_align=args.interior_align, backend=st.Backend.Host if args.cpu else None,
                             shared_halo_line=bool(args.shared_halo_line == 1 if shared is None else shared))
         model.init()
@@ -607,6 +612,7 @@ def main(argv=None):
         return env.agreed_max(time.perf_counter() - t) / k * 1e3
 
     def release(model):
+        """every rank, whether or not it holds a model (the barrier keeps the harness collectives in step)"""
         del model
         import gc
         gc.collect()
@@ -615,10 +621,11 @@ def main(argv=None):
     # Transport chosen by measurement (N > 1): whole steps, max over ranks, best of two rounds, for Colocated over the
     # three inbox memories and for Rccl (the reference ladder's next rung). A default picked where "xGMI" was local
     # HBM must not decide the first multi-GPU record (reference: per-rung runs,
-    # scripts/summit/weak_256n.sh:26-30, ladder src/stencil.cu:163-194).
+    # scripts/summit/weak_256n.sh:26-30, ladder src/stencil.cu:163-194). Bounded by --tune-budget.
     topt = make_transport(st, args)
     transport_tuned = None
     model = None
+    t_ph = time.perf_counter()
     if world > 1 and args.transport == "auto" and args.tune_steps > 0:
         M = st.MethodFlags
         cands = [("colo_uncached", methods, "uncached"), ("colo_fine", methods, "fine"),
@@ -629,7 +636,11 @@ def main(argv=None):
         transport_tuned = {}
         for name, meth, inbox in cands:
             rec = {}
+            if ph.tuning_spent(env) >= args.tune_budget:
+                transport_tuned[name] = {"skipped": f"tune budget {args.tune_budget:.0f} s spent"}
+                continue
             cand = None
+            t_ = None
             try:
                 t_ = make_transport(st, args, inbox)
                 cand = build(t_, meth)
@@ -641,34 +652,39 @@ def main(argv=None):
             except Exception as e:  # noqa: BLE001 -- a candidate failing on this rank: the others learn it below
                 rec["error"] = f"{type(e).__name__}: {str(e)[:200]}"
                 ms = float("inf")
-            if env.agreed_max(0.0 if "error" not in rec else 1.0) > 0:
+            # agreed before any rank-local branch: every rank keeps or releases the same candidate
+            failed = env.agreed_max(0.0 if "error" not in rec else 1.0) > 0
+            if failed:
                 ms = float("inf")
                 rec.setdefault("error", "failed on another rank")
+            ms = env.agreed_max(ms)
             transport_tuned[name] = rec
             if rank == 0:
                 print(f"[bench] transport choice {name}: {rec}", file=sys.stderr, flush=True)
-            if cand is not None and (best is None or ms < best[0]):
+            if not failed and (best is None or ms < best[0]):
                 if best is not None:
                     release(best[1])
                 best = (ms, cand, name, t_, meth)
-            elif cand is not None:
+            else:
                 release(cand)
-        if best is None or best[0] == float("inf"):
-            if best is not None:
-                release(best[1])
-            transport_tuned["chosen"] = "fixed (every candidate failed)"
+        if best is None:
+            transport_tuned["chosen"] = "fixed (every candidate failed or was skipped)"
         else:
             _, model, chosen, topt, methods = best
             transport_tuned["chosen"] = chosen
+        ph.mark("transport_warmup", t_ph)
     if model is None:
+        t_b = time.perf_counter()
         model = build(topt, methods)
+        ph.mark("build", t_b)
     methods = model.domain.methods()
     preflight = model.domain.self_test_report() or "skipped"
     colo = model.domain.exchange_bytes_for_method(st.MethodFlags.Colocated) > 0
 
-    # overlapped vs whole-region pairs (remote halos only): both run, the faster one (max over ranks, best of two
+    # overlapped vs whole-region sweeps (remote halos only): all run, the fastest (max over ranks, best of two
     # rounds) is kept for the timed loop -- part of the warm-up, every rank takes the same decision
     overlap_tuned = None
+    t_ph = time.perf_counter()
     if args.overlap == "auto" and args.tune_steps > 0 and model.can_toggle_overlap():
         best = {}
         # whole-region candidates (mode 0) run fused triples where the model can (temporal 3): probe and time whole
@@ -678,18 +694,19 @@ def main(argv=None):
         r0 = args.x2reserve
         # (mode, CUs left to the transports, co-located copy): mode 1 = slabs beside the sweep, 2 = slabs after
         # it, 0 = whole-region sweeps (fused triples where possible), 3 = pipelined whole-region pairs, 4 = pipelined
-        # triples; copy "s" = pack kernel stores into the peer
-        # inbox, "e" = DMA engine copy (the transports then need fewer CUs: also tried with a quarter of the reserve)
+        # triples; copy "s" = pack kernel stores into the peer inbox, "e" = DMA engine copy (the transports then need
+        # fewer CUs: also tried with a quarter of the reserve). Whole-region first: the default if the budget ends
         copies = ["s", "e"] if colo and args.colo_copy == "auto" else ["e" if args.colo_copy == "engine" else "s"]
         cands = []
         for cp in copies:
-            # mode 3 (pipelined pairs: the next exchange gated on the sweep's published boundary planes) needs the
+            cands.append((0, r0, cp))
+            # modes 3 / 4 (pipelined: the next exchange gated on the sweep's published boundary planes) need the
             # pack-kernel stores
+            if cp == "s" and model.can_pipeline_triples():
+                cands += [(4, r0, cp), (4, max(1, r0 // 2), cp), (4, 2 * r0, cp)]
             if cp == "s" and model.can_pipeline():
                 cands += [(3, r0, cp), (3, max(1, r0 // 2), cp), (3, 2 * r0, cp)]
-            if cp == "s" and model.can_pipeline_triples():  # mode 4: pipelined triples
-                cands += [(4, r0, cp), (4, max(1, r0 // 2), cp), (4, 2 * r0, cp)]
-            cands += [(1, r0, cp), (1, max(1, r0 // 2), cp), (1, 2 * r0, cp), (2, r0, cp), (0, r0, cp)]
+            cands += [(1, r0, cp), (1, max(1, r0 // 2), cp), (1, 2 * r0, cp), (2, r0, cp)]
             if cp == "e":
                 cands.append((1, max(1, r0 // 4), cp))
 
@@ -698,9 +715,13 @@ def main(argv=None):
             model.set_overlap_mode(c[0])
             model.set_comm_reserve(c[1])
 
-        skip = set()
+        skip, over = set(), []
         for c in cands + cands:
             if c in skip:
+                continue
+            if ph.tuning_spent(env) >= args.tune_budget:
+                if c not in best:
+                    over.append(c)
                 continue
             apply(c)
             model.run(sweep)
@@ -717,14 +738,18 @@ def main(argv=None):
             if rank == 0:
                 print(f"[bench] overlap choice {c}: {best[c]:.4f} ms/step{' (skipped)' if c in skip else ''}",
                       file=sys.stderr, flush=True)
-        choice = min(cands, key=lambda c: best[c])
+        timed = [c for c in cands if c in best]
+        choice = min(timed, key=lambda c: best[c]) if timed else (model.overlap_mode(), r0, copies[0])
         apply(choice)
         model.run(sweep)
         model.synchronize()
         env.barrier()
         overlap_tuned = {"mode": choice[0], "reserve": choice[1], "colo_copy": "engine" if choice[2] == "e" else "store",
                          "triples": bool(model.temporal_triples()),
-                         **{f"m{c[0]}_r{c[1]}_{c[2]}_ms": round(best[c], 4) for c in cands}}
+                         **{f"m{c[0]}_r{c[1]}_{c[2]}_ms": round(best[c], 4) for c in timed}}
+        if over:
+            overlap_tuned["skipped_by_budget"] = [f"m{c[0]}_r{c[1]}_{c[2]}" for c in over]
+        ph.mark("overlap_warmup", t_ph)
 
     # ---- the timed loop: exactly --steps steps, bracketed by a barrier + device synchronize on both sides ----
     env.barrier()
@@ -736,57 +761,38 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     elapsed = env.agreed_max(elapsed)
+    ph.mark("timed_loop", t0)
     cells = grid[0] * grid[1] * grid[2]
     gcells = cells * args.steps / elapsed / 1e9
 
-    # exchange-only loop on the same decomposition (halo-exchange GB/s, bench_exchange definition)
+    # exchange-only loops on the same decomposition (halo-exchange GB/s, bench_exchange definition)
+    t_ph = time.perf_counter()
     dd = model.domain
     dd.set_comm_max_blocks(0)  # the exchange alone may use the whole GPU (the overlapped steps confine it to 8 CUs)
     xbytes = int(dd.exchange_bytes_for_method(st.MethodFlags.All))
     colo_log = colo and topt.completion != topt.Completion.StreamOp and not args.cpu
     xrec = time_exchanges(env, dd, args.exchange_iters, xbytes, log=colo_log)
+    xrec.update(exchange_trimean(env, dd, args.exchange_iters, xbytes))
+    ph.mark("exchange_loops", t_ph)
 
     pdim = dd.placement_dim()
     wrap_axes = "".join(c for i, c in enumerate("xyz") if model.wrap_axes() >> i & 1) or "none"
     model_cfg = {
         "decomposition": f"{pdim.x}x{pdim.y}x{pdim.z}", "methods": st.methods_to_string(methods), "preflight": preflight,
         "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
-        "transport_tuned": transport_tuned,
-        "x_halo_align": bool(args.x_halo_align), "interior_align": args.interior_align,
-        "x_face_lines": bool(args.x_face_lines), "shared_halo_line": args.shared_halo_line == 1,
-        "nontemporal": bool(args.nt), "alternate_z": bool(args.altz), "ty": args.ty, "nw": args.nw,
-        "variant": args.variant, "x2nw": args.x2nw, "x2pf": args.x2pf, "x3sched": args.x3sched, "x3layout": args.x3layout, "x3var": args.x3var, "x3pf": args.x3pf, "x3sphw": args.x3sphw, "x2sphw": args.x2sphw, "x2early": args.x2early, "x2row": args.x2row, "x2sched": args.x2sched,
-        "x2xfast": args.x2xfast, "zchunk": args.zchunk, "temporal": 3 if model.temporal_triples() else (2 if model.temporal_blocking() else 1),
-        "wrap_axes": wrap_axes, "backend": "host" if args.cpu else "device",
+        "transport_tuned": transport_tuned, "interior_align": args.interior_align,
+        "shared_halo_line": args.shared_halo_line == 1,
+        "temporal": 3 if model.temporal_triples() else (2 if model.temporal_blocking() else 1),
+        "wrap_axes": wrap_axes, "backend": "host" if args.cpu else "device", "tune": tune_record(tune),
         "transport": {"inbox": str(dd.transport_options().inbox).split(".")[-1].lower(),
                       "colo_copy": str(dd.transport_options().colo_copy).split(".")[-1].lower(),
                       "completion": args.completion, "fuse_flags": bool(args.fuse_flags)},
+        "phases_s": ph.t,
     }
+    mode_tuned = model.overlap_mode()
     del dd
     release(model)
     model = None
-
-    # BASELINE config 2 as the reference times it (bin/jacobi3d.cu:265-346: exchange() every iteration): the same
-    # steps with every halo copied -- the intra-GPU pack/unpack (same-GPU copy-plan kernel) plus the compute kernels
-    with_x = None
-    if args.with_exchange == "on" or (args.with_exchange == "auto" and wrap_axes != "none"):
-        m2 = build(topt, methods, wrap_self=False, shared=args.shared_halo_line != 0)
-        if model_cfg["overlap_tuned"] is not None and m2.can_toggle_overlap():
-            m2.set_overlap_mode(overlap_tuned["mode"])
-            m2.set_comm_reserve(overlap_tuned["reserve"])
-            m2.run(2)
-            m2.synchronize()
-        env.barrier()
-        t = time.perf_counter()
-        m2.run(args.steps)
-        m2.synchronize()
-        env.sync()
-        el = env.agreed_max(time.perf_counter() - t)
-        with_x = {"gcells": round(cells * args.steps / el / 1e9, 3), "ms_per_step": round(el / args.steps * 1e3, 4),
-                  "wrap_axes": "".join(c for i, c in enumerate("xyz") if m2.wrap_axes() >> i & 1) or "none",
-                  "shared_halo_line": bool(m2.domain.domain(0).shared_halo_line()),
-                  "halo_bytes_per_exchange": int(m2.domain.exchange_bytes_for_method(st.MethodFlags.All))}
-        release(m2)
 
     out = {
         "metric": "Jacobi3D Gcells/s (512^3/GPU weak scaling; halo-exchange GB/s in extra)",
@@ -807,20 +813,62 @@ def main(argv=None):
                    **model_cfg,
                    "build": st.build_info()["git_sha"]},
         "extra": {"halo_exchange_GBps": xrec["GBps"], "halo_exchange_stream_GBps": xrec.get("stream_GBps"),
+                  "halo_exchange_trimean_GBps": xrec.get("trimean_GBps"),
                   "halo_bytes_per_exchange": xbytes, "exchange_ms": xrec["exchange_ms"],
+                  "exchange_trimean_ms": xrec.get("trimean_ms"),
                   "gcells_per_gpu": round(gcells / n, 3), "colo_kernels_us": xrec.get("colo_kernels_us"),
-                  "gcells_with_exchange": with_x["gcells"] if with_x else None, "with_exchange": with_x,
+                  "gcells_with_exchange": None, "with_exchange": None,
                   "transports": "pending" if (args.transport_sweep == "on" or
                                               (args.transport_sweep == "auto" and world > 1)) else None},
     }
+
+    # BASELINE config 2 as the reference times it (bin/jacobi3d.cu:265-346: exchange() every iteration): the same
+    # steps with every halo copied -- the intra-GPU pack/unpack (same-GPU copy-plan kernel) plus the compute kernels
+    # (fused triples reading x from 3-deep halos where the layout allows). A failure here costs this entry, not the
+    # headline
+    if args.with_exchange == "on" or (args.with_exchange == "auto" and wrap_axes != "none"):
+        t_ph = time.perf_counter()
+        m2 = None
+        try:
+            m2 = build(topt, methods, wrap_self=False, shared=args.shared_halo_line != 0)
+            if overlap_tuned is not None and m2.can_toggle_overlap():
+                # the tuned mode only where this model supports it (pipelined modes need the gate / the triples)
+                md = mode_tuned
+                if (md == 4 and not m2.can_pipeline_triples()) or (md == 3 and not m2.can_pipeline()):
+                    md = 0
+                m2.set_overlap_mode(md)
+                m2.set_comm_reserve(overlap_tuned["reserve"])
+                m2.run(6)
+                m2.synchronize()
+            env.barrier()
+            t = time.perf_counter()
+            m2.run(args.steps)
+            m2.synchronize()
+            env.sync()
+            el = env.agreed_max(time.perf_counter() - t)
+            out["extra"]["with_exchange"] = {
+                "gcells": round(cells * args.steps / el / 1e9, 3), "ms_per_step": round(el / args.steps * 1e3, 4),
+                "wrap_axes": "".join(c for i, c in enumerate("xyz") if m2.wrap_axes() >> i & 1) or "none",
+                "temporal": 3 if m2.temporal_triples() else (2 if m2.temporal_blocking() else 1),
+                "overlap_mode": m2.overlap_mode(),
+                "shared_halo_line": bool(m2.domain.domain(0).shared_halo_line()),
+                "halo_bytes_per_exchange": int(m2.domain.exchange_bytes_for_method(st.MethodFlags.All))}
+            out["extra"]["gcells_with_exchange"] = out["extra"]["with_exchange"]["gcells"]
+        except Exception as e:  # noqa: BLE001
+            out["extra"]["with_exchange"] = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+        release(m2)
+        ph.mark("with_exchange", t_ph)
+
     if rank == 0:
         emit(out)  # line 1: the headline, before anything that could hang
 
     if out["extra"]["transports"] == "pending":
+        t_ph = time.perf_counter()
         timer = arm_deadline(args.sweep_deadline, rank)
         out["extra"]["transports"] = transport_sweep(st, env, args, world, rank, device, ndev, axis_cost, objective,
                                                      topt, methods)
         timer.cancel()
+        ph.mark("sweep", t_ph)
         if rank == 0:
             emit(out)  # line 2: the same headline with the sweep
     if world > 1:

@@ -389,8 +389,11 @@ private:
   std::string poisoned_;
   void poison(const std::string &why);
   void init_rccl(const std::function<bool(int, int)> &sharedDev); // realize(): communicator or staged fallback
+  // Completion::IpcEvent: consume the last two exchanges' Acks so a later domain on the same group starts clean.
+  // Polls at most timeout_s seconds and returns false if they did not all arrive; timeout_s <= 0 uses the group's
+  // blocking receive (bounded by its own wait timeout).
   bool drain_ipc_acks(double timeout_s);
-  bool x_face_lines(const LocalDomain &s, const LocalDomain &d) const; // translate s -> d copies x faces as lines // Completion::IpcEvent: consume the last two exchanges' Acks
+  bool x_face_lines(const LocalDomain &s, const LocalDomain &d) const; // translate s -> d copies x faces as lines
   std::string planPrefix_ = "plan";
   int numaNode_ = -1; // NUMA node the calling thread was bound to in realize() (-1: none)
 

@@ -51,14 +51,10 @@ struct StencilTune {
   // one MI355X, 512^3, bench.py: 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s
   int x2nw = 12, x2pf = 1; // one plane of lookahead: best for the whole-row kernel once its edge waves skip u1/u2
   int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
-  int x3layout = 0;       // fused triples: 1 = 8 adjacent cells per lane (one rotate per x side), 0 = chunks 256 apart
-  int x3var = 7;          // fused triples: bit 0 = publish u1/u2 right after their update, bit 1 = no fences between
-                          // levels, bit 2 = publish the src row right after u1 (7: 1431-1443 vs 0: 1381-1392 Gcells/s)
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
   float x3sphw = 0.3f;    // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z
                           // parts are cut per row group (0: equal parts)
   float x2sphw = 0.15f;   // fused pairs (Jacobi, row / col2 kernels): sphere weight of the z parts (r5/at, r5/au)
-  int x3pf = 1;           // fused triples: src planes of lookahead in registers (1, 2)
   bool x2early = true;    // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
                           // (row kernel 208.6 vs 216.6 us per pair, col2 226.9 vs 234.1)
   // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells
@@ -170,8 +166,9 @@ void stencil7_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, Ste
 bool stencil7x2_supported(const LocalDomain &dom, int64_t qi);
 void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune = StencilTune());
-// Three fused steps: dst = S(S(S(src))) on the whole compute region of a fp32 sub-domain of 512-cell rows whose
-// every axis wraps in-kernel (tune.wrap == 7: one GPU, no halo read at all), bitwise equal to three single steps.
+// Three fused steps: dst = S(S(S(src))) on the whole compute region, bitwise equal to three single steps. x either
+// wraps in-kernel (tune.wrap & 1: fp32 rows of exactly 512 cells) or is read from 3-deep halos (fp32 x a multiple of
+// 512, fp64 of 256; faces, edges and corners exchanged); y / z wrap in-kernel or read 3-deep halos.
 // Returns false (nothing launched) when this layout / region / tune is not supported.
 bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune);
 bool stencil7x3_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,

@@ -145,9 +145,10 @@ private:
   bool graphs_ = false;
   bool forward_ = false;
   bool pairs_ = false; // temporal blocking active
+  // fused triples active: three steps per sweep (run() then uses pairs / single steps only for remainders)
   bool triples_ = false;
   bool triplesOk_ = false; // triples possible for whole-region sweeps (triples_ = triplesOk_ && !overlap_)
-  bool confinedSelf_ = false; // overlapped single steps with only same-GPU halos: translate on x2reserve CUs // ... by three steps per sweep (run() then uses pairs / single steps only for remainders)
+  bool confinedSelf_ = false; // overlapped single steps with only same-GPU halos: translate on x2reserve CUs
   bool overlapToggle_ = false;
   bool slabsAfter_ = false; // overlap mode 2 (see set_overlap_mode)
   bool pipeOk_ = false;      // overlap mode 3 possible (see init)

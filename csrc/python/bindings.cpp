@@ -733,10 +733,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("nw", &StencilTune::nw)
       .def_readwrite("x2pf", &StencilTune::x2pf)
       .def_readwrite("x3sched", &StencilTune::x3sched)
-      .def_readwrite("x3layout", &StencilTune::x3layout)
-      .def_readwrite("x3var", &StencilTune::x3var)
       .def_readwrite("x2early", &StencilTune::x2early)
-      .def_readwrite("x3pf", &StencilTune::x3pf)
       .def_readwrite("x3parts", &StencilTune::x3parts)
       .def_readwrite("x3sphw", &StencilTune::x3sphw)
       .def_readwrite("x2sphw", &StencilTune::x2sphw)

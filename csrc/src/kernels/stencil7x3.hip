@@ -1,28 +1,33 @@
-// Three fused 7-point steps per sweep (deeper temporal blocking): dst = S(S(S(src))) on a whole periodic sub-domain
-// of 512-cell fp32 rows, for gfx950.
+// Three fused 7-point steps per sweep (deeper temporal blocking): dst = S(S(S(src))) on a whole sub-domain, for
+// gfx950. Two forms of one kernel:
+//   * whole periodic rows (x wrapped in-kernel, fp32 rows of exactly 512 cells): the x-neighbours and the wrap are DPP
+//     lane rotates of the wave's own registers, nothing is read beyond the row;
+//   * columns with x halos (XH: fp32 x a multiple of 512, fp64 of 256): the same two-chunk lane layout per column of
+//     CW cells, and only the 3 cells beyond each column end come from outside the wave - one 16-B load per lane half
+//     (cells x-3 .. x of the left end into lanes 0-31, x+CW-1 .. x+CW+2 of the right end into lanes 32-63; lanes 0
+//     and 63 use them). The intermediate levels are computed on the cells the next level needs there: u1 at x-2, x-1
+//     and x+CW, x+CW+1, u2 at x-1 and x+CW, with the neighbour rows' edge values through LDS. So a sub-domain whose
+//     x faces come from an exchange (the reference's every-iteration exchange on one GPU, x cut across GPUs, fp64)
+//     runs one depth-3 exchange and one read + write of the field per three steps.
 //
-// The fused pair (stencil7x2_row_kernel) streams the field once per two steps and sits at ~95 % of a plain copy of
-// its access shape (205 us per 512^3 pair, profiles/r4/j). Fewer bytes per step is the only lever left: a triple
-// reads and writes the field once per THREE steps (8 B per cell per 3 steps instead of per 2). What it costs is
-// compute on the redundant y halo: a block of NW waves (one 512-cell row each, x-neighbours and the x wrap by DPP lane
-// rotates exactly as in the pair kernel) holds NW src rows and computes
-//   u1 on the inner NW-2 rows, u2 on the inner NW-4, u3 (the output) on the inner NW-6,
-// so 12 waves write 6 rows with 10 + 8 + 6 = 24 row updates (4 per output row for 3 steps: 1.33 per row and step,
-// against the pair's (10 + 8) / 8 / 2 = 1.13). The round-2 lab triple computed all three levels on every row
-// (6 updates per output row: 2.0 per row and step) and was VALU-bound at 134 us per step (profiles/r2/r2_lab_triple.txt);
-// here each wave only computes the levels some output row needs (wave-uniform), as the pair's edge waves do.
+// The fused pair (stencil7x2_row_kernel) streams the field once per two steps at ~95 % of a plain copy of its access
+// shape (205 us per 512^3 pair, profiles/r4/j); a triple reads and writes the field once per THREE steps. What it
+// costs is compute on the redundant y halo: a block of 12 waves (one row each) holds 12 src rows and computes
+//   u1 on the inner 10 rows, u2 on the inner 8, u3 (the output) on the inner 6,
+// i.e. 24 row updates per 6 output rows; each wave only computes the levels some output row needs (wave-uniform).
 //
 //   step t (output plane z, march direction dz):
-//     1. issue the load of src plane z + (3 + PF) dz                      (PF planes of lookahead in registers)
-//     2. u1 at plane z+2dz from the src window + LDS y-neighbours          (waves 1 .. NW-2)
-//     3. u2 at plane z+dz  from the u1 window (z, z+dz, z+2dz) + LDS       (waves 2 .. NW-3)
-//     4. u3 at plane z     from the u2 window (z-dz, z, z+dz) + LDS        (waves 3 .. NW-4)  -> store
-//     5. publish src(z+3dz), u1(z+2dz), u2(z+dz) rows into the other LDS buffer; one barrier
-// A segment of nzs output planes runs nzs + 4 steps (u3 needs u2 one plane behind it, which needs u1 two planes
-// behind). Summation order, the exact /6 and the spheres are those of the single step, every intermediate value is
-// computed exactly as the single step computes it (y and z by in-kernel wrap), so S(S(S(src))) is bitwise equal to
-// three single steps (tests/test_gpu.py::test_temporal3_matches_three_single_steps).
-// Reference step being fused: bin/jacobi3d.cu:40-87 (Jacobi), bin/astaroth_sim.cu:65-83 (Astaroth).
+//     1. issue the load of src plane z + 4dz                               (one plane of lookahead in registers)
+//     2. u1 at plane z+2dz from the src window + LDS y-neighbours          (waves 1 .. 10)   publish src(z+3dz), u1
+//     3. u2 at plane z+dz  from the u1 window (z, z+dz, z+2dz) + LDS       (waves 2 .. 9)    publish u2
+//     4. u3 at plane z     from the u2 window (z-dz, z, z+dz) + LDS        (waves 3 .. 8)  -> store
+//     5. one barrier (every LDS row is written into the other buffer right after its update: the step is bound by
+//        the chain LDS write -> barrier -> LDS read -> update, three times per step, profiles/r5/v)
+// A segment of nzs output planes runs nzs + 4 steps. Summation order, the exact /6 and the spheres are those of the
+// single step, every intermediate value is computed exactly as the single step computes it, so S(S(S(src))) is
+// bitwise equal to three single steps (tests/test_gpu.py::test_temporal3_*).
+// Reference step being fused: bin/jacobi3d.cu:40-87 (Jacobi), bin/astaroth_sim.cu:65-83 (Astaroth); the exchange the
+// XH form reads once per three steps: bin/jacobi3d.cu:291 (dd.exchange() every iteration).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,21 +44,24 @@
 
 namespace stencil {
 
-// (column, plane) segment of a block: lockstep parts as the fused pairs (x2_segments), kept local to this file
+// (column, plane) segment of a block: lockstep parts as the fused pairs (x2_segments), kept local to this file.
+// Columns are numbered y-major inside an x strip (col = bx * gy + by); the z-part bounds are per row group (by)
 struct X3Seg {
   uint32_t s, e, s2, e2;
   bool odd;
 };
-__device__ __forceinline__ X3Seg x3_segments(const StencilArgs<float> &a, const ZPartBounds &B, uint32_t lb, uint32_t nb,
-                                             uint32_t ncols, uint32_t nzt) {
+template <typename T>
+__device__ __forceinline__ X3Seg x3_segments(const StencilArgs<T> &a, const ZPartBounds &B, uint32_t lb, uint32_t nb,
+                                             uint32_t ncols, uint32_t gy, uint32_t nzt) {
   X3Seg r{0, 0, 0, 0, false};
   if (a.seg == 2) {
     const uint32_t P = uint32_t(a.zparts), cm = nb / P;
     const uint32_t qq = lb / cm, col = lb % cm;
+    const uint32_t grp = col % gy;
     uint32_t zlo = qq * nzt / P, zhi = (qq + 1) * nzt / P;
-    if (B.on && col < uint32_t(kZPartMaxCols)) {
-      zlo = qq > 0 ? uint32_t(B.zb[col][qq - 1]) : 0;
-      zhi = qq + 1 < P ? uint32_t(B.zb[col][qq]) : nzt;
+    if (B.on && grp < uint32_t(kZPartMaxCols)) {
+      zlo = qq > 0 ? uint32_t(B.zb[grp][qq - 1]) : 0;
+      zhi = qq + 1 < P ? uint32_t(B.zb[grp][qq]) : nzt;
     }
     r.s = col * nzt + zlo;
     r.e = col * nzt + zhi;
@@ -72,42 +80,47 @@ __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<float> &a, const 
   return r;
 }
 
-template <int NW, int PF, int KIND, bool CONTIG, int VAR>
-__global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
-stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
-  using T = float;
-  using NV = nf4;
-  constexpr int V = 4, H = 2;
-  // CONTIG: a lane holds 8 adjacent cells (chunk h = cells 8 lane + 4h ..): the row's x-neighbours and the periodic
-  // wrap are one rotate each way and no lane-0 / lane-63 selects. Otherwise chunk h = cells 256 h + 4 lane .. (every
-  // memory op a contiguous 1 KiB; each rotate needs a select between the two chunks at lanes 0 / 63)
-  constexpr int CS = CONTIG ? V : 64 * V; // cells between a lane's chunks
-  constexpr int LS = CONTIG ? H * V : V;  // cells between adjacent lanes
-  // VAR bit 0: publish u1 / u2 rows right after their update (LDS writes spread over the step instead of all before
-  // the barrier); bit 1: no scheduling fences between the levels; bit 2: publish the src row right after the u1 update (its load was waited for there); bit 3: every
-  // level's LDS reads at the top of the step
-  constexpr bool EARLYW = (VAR & 1) != 0, NOSB = (VAR & 2) != 0, EARLYC = (VAR & 4) != 0, HOIST = (VAR & 8) != 0;
-  constexpr int YO = NW - 6; // output rows per block
-  constexpr int NC = 3 + PF; // src planes in registers
-  static_assert(NW == 12, "12 waves: 3 per SIMD (168 VGPRs), 3 x 48 KiB of LDS");
-  static_assert(PF == 1 || PF == 2, "slot rotations of 4 or 5 planes (4 unrolled warm-up steps, then the cycle)");
+// 16 B of the source at byte offset voff + soff (buffer load: the plane offset in an SGPR)
+template <typename X>
+__device__ __forceinline__ X x3_load16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(X, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+template <typename T, int KIND, bool XH>
+__global__ __launch_bounds__(64 * 12, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
+stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
+  using NV = typename Vec16<T>::native;
+  using P2 = typename Pk<T>::t;
+  typedef T E4 __attribute__((ext_vector_type(4)));
+  constexpr int NW = 12;              // 3 waves per SIMD (168 VGPRs), 3 x 48 KiB of LDS
+  constexpr int V = int(16 / sizeof(T)), H = 2;
+  constexpr int CS = 64 * V;          // cells between a lane's two chunks
+  constexpr int CW = H * CS;          // cells per column (the whole row when x wraps in-kernel)
+  constexpr int YO = NW - 6;          // output rows per block
+  constexpr int NC = 4;               // src planes in registers (one plane of lookahead)
+  static_assert(XH || sizeof(T) == 4, "whole periodic rows: fp32 (512 cells)");
   __shared__ NV cs[2][NW][H][64]; // src rows  (plane z+3dz at publish)
   __shared__ NV us[2][NW][H][64]; // u1 rows   (plane z+2dz at publish)
   __shared__ NV vs[2][NW][H][64]; // u2 rows   (plane z+dz at publish)
+  __shared__ P2 ce[2][NW][2];     // XH: src at (x-2, x-1) [0] and (x+CW, x+CW+1) [1] of the published rows
+  __shared__ T ue[2][NW][2];      // XH: u1 at x-1 [0] and x+CW [1]
 
   const uint32_t nb = gridDim.x;
   const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.y)); // the wave's block row (wave-uniform: SGPR)
   const uint32_t nzt = uint32_t(a.hiz - a.loz);
-  const X3Seg sg = x3_segments(a, zbounds, lb, nb, uint32_t(a.gy), nzt);
+  const uint32_t gy = uint32_t(a.gy);
+  const X3Seg sg = x3_segments(a, zbounds, lb, nb, uint32_t(a.gx) * gy, gy, nzt);
   const bool lane0 = lane == 0, lane63 = lane == 63;
+  // XH: lanes 32-63 hold the right column end's cells (lane 63 uses them), lanes 0-31 the left end's (lane 0)
+  const int side = lane >> 5;
+  const bool isR = side != 0;
+  const bool edgeLane = lane0 || lane63;
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
-  const int xb = a.lox + lane * LS; // chunk h at xb + h * CS
   const int zwn = a.wn[2], zwlo = a.wlo[2], zwhi = a.wlo[2] + a.wn[2];
   // raw buffer over the source field (offsets from raw [0,0,0] are non-negative and below 4 GiB: checked by the host)
-  const __amdgpu_buffer_rsrc_t srcRsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.src), 0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t srcRsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(a.src), 0, -1, 0x00020000);
   auto zcl = [&](int zz) {
     zz += zz < zwlo ? zwn : 0;
     zz -= zz >= zwhi ? zwn : 0;
@@ -116,7 +129,8 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
   // The wave's role = the levels its row computes (wave-uniform): 0 on rows 0 / 11 (source rows only), 1 (u1) on 1 /
   // 10, 2 (u1, u2) on 2 / 9, 3 (u1, u2, u3 = output) on 3..8. The whole march is instantiated per role, and the
   // warm-up steps (fewer valid levels) are unrolled separately, so the steady-state step has no role or level
-  // branches: per step one tiny-sum test (ballot) and, for Jacobi, one sphere test per level.
+  // branches. XH edges: u1 at the column ends feeds the u2 of the row itself and of its y-neighbours (roles >= 2
+  // compute it), u2 at the column ends only the row's own u3 (role 3).
   auto body = [&](auto roleTag) {
     constexpr int R = decltype(roleTag)::value;
     bool odd = sg.odd;
@@ -128,10 +142,12 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
       uint32_t s = pass == 0 ? sg.s : sg.s2;
       const uint32_t e = pass == 0 ? sg.e : sg.e2;
       while (s < e) { // block-uniform
-        const uint32_t by = s / nzt;
-        const int zo = int(s - by * nzt);
+        const uint32_t col = s / nzt;
+        const int zo = int(s - col * nzt);
         const int nzs = int(min(nzt - uint32_t(zo), e - s));
         s += uint32_t(nzs);
+        const int bx = XH ? int(col / gy) : 0;
+        const int by = int(col - uint32_t(bx) * gy);
         const int zs = a.loz + zo;
         const int ze = zs + nzs;
         bool down = pass == 0 && sg.odd;
@@ -139,14 +155,20 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
           down = odd != (a.flip != 0);
           odd = !odd;
         }
-        const int yblk = a.loy + YO * int(by);
+        const int yblk = a.loy + YO * by;
         const int y = yblk - 3 + w;
         if (yblk >= a.hiy) continue;
         const bool outRow = R == 3 && y < a.hiy;
         int yw = y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y);
         yw = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
+        const int xcol = a.x0 + bx * CW; // first cell of the column
+        const int xb = xcol + lane * V;  // chunk h at xb + h * CS
         const uint32_t rowoff = uint32_t((yw * int64_t(a.px) + xb) * int64_t(sizeof(T)));
         const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+        // XH: 4 cells from x-3 (left half) / x+CW-1 (right half): the edge cells (e[1], e[2]) and their outer and
+        // inner x-neighbours (e[0], e[3]), so both ends compute u1 at (e[1], e[2]) with the same lane code
+        const int xe = isR ? xcol + CW - 1 : xcol - 3;
+        const uint32_t edgeoff = uint32_t((yw * int64_t(a.px) + xe) * int64_t(sizeof(T)));
 
         // spheres (Jacobi): the planes P of this row that cross the hot / cold sphere form two intervals
         // |P - c.z| <= h (h * h < r1sq - dy^2), computed once per segment; per-cell tests only on those planes
@@ -183,85 +205,73 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
           }
           return r;
         };
-        // per-cell tests on the rows that cross a sphere (cheaper variants measured slower: an x interval per row,
-        // tests only on the chunk the sphere reaches; profiles/r5/ai, aj, ap). Those rows make their blocks the
-        // sweep's longest, which the host evens out with sphere-weighted z parts (x3sphw, profiles/r5/ao)
+        // (x - c)^2 + d < r1sq <=> (x - c)^2 < r1sq - d: the row's bound is one scalar per sphere, the per-cell squared
+        // distances loop invariants, so a cell costs a compare and a select per sphere. Cheaper variants measured
+        // slower (an x interval per row, tests only on the chunk the sphere reaches; profiles/r5/ai, aj, ap); the
+        // blocks of sphere-crossing rows are evened out by sphere-weighted z parts (x3sphw, profiles/r5/ao)
+        auto sph_fix = [&](const RowSph &rs, int x, T v) -> T {
+          const bool hot = (x - a.hx) * (x - a.hx) < a.r1sq - rs.dh;
+          const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - rs.dc;
+          return hot ? T(1) : (cold ? T(0) : v);
+        };
         auto sphere_row = [&](const RowSph &rs, NV(&o)[H]) {
           if (KIND == 0 && rs.hit) {
-            // (x - c)^2 + d < r1sq <=> (x - c)^2 < r1sq - d: the row's bound is one scalar per sphere, the per-cell
-            // squared distances loop invariants, so a cell costs a compare and a select per sphere
+            // XH: the cell coordinates through an opaque copy, so the per-cell squared distances are recomputed on
+            // the sphere rows instead of held in 16 VGPRs over the march (the XH edges need them: 44 spilled)
+            int x0 = xb;
+            if constexpr (XH) asm volatile("v_mov_b32 %0, %1" : "=v"(x0) : "v"(xb));
+#ifdef X3_EXP_SPH2
+            // interval form: per row-plane x ranges [lo, lo + len) of the two spheres (uniform), per cell one
+            // unsigned compare per sphere
             const int Dh = a.r1sq - rs.dh, Dc = a.r1sq - rs.dc;
+            auto rng = [&](int D, int c, int &lo, unsigned &len) {
+              if (D <= 0) { lo = 0; len = 0; return; }
+              int h = int(__builtin_sqrtf(float(D - 1)));
+              while (h > 0 && h * h > D - 1) --h;
+              while ((h + 1) * (h + 1) <= D - 1) ++h;
+              lo = c - h; len = unsigned(2 * h + 1);
+            };
+            int lh, lc; unsigned nh, nc;
+            rng(Dh, a.hx, lh, nh);
+            rng(Dc, a.cx, lc, nc);
+            lh = __builtin_amdgcn_readfirstlane(lh); lc = __builtin_amdgcn_readfirstlane(lc);
+            nh = __builtin_amdgcn_readfirstlane(nh); nc = __builtin_amdgcn_readfirstlane(nc);
 #pragma unroll
             for (int h = 0; h < H; ++h)
 #pragma unroll
               for (int k = 0; k < V; ++k) {
-                const int x = xb + h * CS + k;
-                const bool hot = (x - a.hx) * (x - a.hx) < Dh;
-                const bool cold = (x - a.cx) * (x - a.cx) < Dc;
-                o[h][k] = hot ? T(1) : (cold ? T(0) : o[h][k]);
+                const int x = x0 + h * CS + k;
+                o[h][k] = unsigned(x - lh) < nh ? T(1) : (unsigned(x - lc) < nc ? T(0) : o[h][k]);
               }
+#else
+#pragma unroll
+            for (int h = 0; h < H; ++h)
+#pragma unroll
+              for (int k = 0; k < V; ++k) o[h][k] = sph_fix(rs, x0 + h * CS + k, o[h][k]);
+#endif
           }
         };
-        // S of the wave's row (both chunks), x-neighbours and the periodic x wrap by lane rotates. EXACT: the
-        // corrected quotient with the true division for |sum| < 2^-100 (div6v); otherwise the FMA-corrected quotient
-        // for every cell and the smallest |sum| returned (the caller redoes the step exactly when it is tiny)
-        auto row_update = [&](auto exactTag, const NV(&cm)[H], const NV(&up)[H], const NV(&dn)[H], const NV(&zp)[H],
-                              const NV(&zm)[H], NV(&o)[H]) -> T {
-          constexpr bool EXACT = decltype(exactTag)::value;
+        // S of the wave's row (both chunks), x-neighbours by lane rotates; at the row / column ends lane 0 and lane
+        // 63 take the periodic wrap (whole rows) or e, their own end's cell beyond the column (XH). Exact /6 (div6v)
+        auto row_update = [&](const NV(&cm)[H], const NV(&up)[H], const NV(&dn)[H], const NV(&zp)[H], const NV(&zm)[H],
+                              T ev, NV(&o)[H]) {
           static_assert(H == 2, "two chunks per lane");
-          if constexpr (CONTIG) {
-            // cells c0..c7 of the lane; left of c0 = c7 of lane - 1 (lane 0: lane 63, the wrap), right of c7 = c0 of
-            // lane + 1
-            const T L = rot_prev(cm[1][V - 1]), Rr = rot_next(cm[0][0]);
-            const NV vmx0 = {L, cm[0][0], cm[0][1], cm[0][2]}, vpx0 = {cm[0][1], cm[0][2], cm[0][3], cm[1][0]};
-            const NV vmx1 = {cm[0][3], cm[1][0], cm[1][1], cm[1][2]}, vpx1 = {cm[1][1], cm[1][2], cm[1][3], Rr};
-            const NV sm0 = sum6v<T, KIND>(vpx0, vmx0, dn[0], up[0], zp[0], zm[0]);
-            const NV sm1 = sum6v<T, KIND>(vpx1, vmx1, dn[1], up[1], zp[1], zm[1]);
-            if constexpr (EXACT) {
-              // one tiny-sum test for the lane's 8 quotients
-              using NV8 = float __attribute__((ext_vector_type(8)));
-              const NV8 q = div6v<T, NV8, 2 * V>(__builtin_shufflevector(sm0, sm1, 0, 1, 2, 3, 4, 5, 6, 7));
-              o[0] = __builtin_shufflevector(q, q, 0, 1, 2, 3);
-              o[1] = __builtin_shufflevector(q, q, 4, 5, 6, 7);
-              return T(1);
-            } else {
-              T m = T(1);
-              const NV c = NV(1.0f / 6.0f), six = NV(6.0f);
-              const NV q0 = sm0 * c, q1 = sm1 * c;
-              o[0] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q0, six, sm0), c, q0);
-              o[1] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, six, sm1), c, q1);
-#pragma unroll
-              for (int k = 0; k < V; ++k) m = __builtin_fminf(m, __builtin_fminf(__builtin_fabsf(sm0[k]), __builtin_fabsf(sm1[k])));
-              return m;
-            }
-          }
           // named scalars, not arrays: a select between two array elements became a dynamically indexed private
           // array (scratch stores + loads on every row update, 449 vs 304 us per triple)
           const T r30 = rot_prev(cm[0][V - 1]), r31 = rot_prev(cm[1][V - 1]);
           const T l00 = rot_next(cm[0][0]), l01 = rot_next(cm[1][0]);
-          T m = T(1);
 #pragma unroll
           for (int h = 0; h < H; ++h) {
-            const T left = h == 0 ? (lane0 ? r31 : r30) : (lane0 ? r30 : r31);
-            const T right = h == 0 ? (lane63 ? l01 : l00) : (lane63 ? l00 : l01);
+            const T left = h == 0 ? (lane0 ? (XH ? ev : r31) : r30) : (lane0 ? r30 : r31);
+            const T right = h == 0 ? (lane63 ? l01 : l00) : (lane63 ? (XH ? ev : l00) : l01);
             NV vpx, vmx;
 #pragma unroll
             for (int k = 0; k < V; ++k) {
               vpx[k] = k < V - 1 ? cm[h][k + 1] : right;
               vmx[k] = k > 0 ? cm[h][k - 1] : left;
             }
-            const NV sm = sum6v<T, KIND>(vpx, vmx, dn[h], up[h], zp[h], zm[h]);
-            if constexpr (EXACT) {
-              o[h] = div6v<T, NV, V>(sm);
-            } else {
-              const NV c = NV(1.0f / 6.0f), six = NV(6.0f);
-              const NV q0 = sm * c;
-              o[h] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q0, six, sm), c, q0);
-              m = __builtin_fminf(m, __builtin_fminf(__builtin_fminf(__builtin_fabsf(sm[0]), __builtin_fabsf(sm[1])),
-                                                     __builtin_fminf(__builtin_fabsf(sm[2]), __builtin_fabsf(sm[3]))));
-            }
+            o[h] = div6v<T, NV, V>(sum6v<T, KIND>(vpx, vmx, dn[h], up[h], zp[h], zm[h]));
           }
-          return m;
         };
 
         auto march = [&](auto downTag) {
@@ -269,8 +279,11 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
           constexpr int dz = DOWN ? -1 : 1;
           const int z0 = DOWN ? ze - 1 : zs;
           NV C[NC][H];
+          E4 E[NC];                  // XH: the column-end cells of the src window planes
           NV U1a[H], U1b[H], U1c[H]; // u1 at planes z+2dz (new), z, z+dz
           NV U2a[H], U2b[H], U2c[H]; // u2 at planes z+dz (new), z-dz, z
+          P2 U1Ea, U1Eb, U1Ec;       // XH: u1 at (e[1], e[2]) of the end, planes as U1
+          T U2Ea, U2Eb, U2Ec;        // XH: u2 at the end's adjacent cell, planes as U2
           // buffer loads: the plane offset in an SGPR (soffset), the row offset a per-segment constant VGPR. With
           // 64-bit VGPR addresses recomputed every step, the address write landed on registers of the slot's
           // previous load and the compiler waited for every outstanding memory op (s_waitcnt vmcnt(0)) before each
@@ -279,20 +292,36 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
             const uint32_t po = uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
 #pragma unroll
             for (int h = 0; h < H; ++h)
-              C[k][h] = __builtin_bit_cast(
-                  NV, __builtin_amdgcn_raw_buffer_load_b128(srcRsrc, rowoff + uint32_t(h * CS * int(sizeof(T))), po, 0));
+              C[k][h] = x3_load16<NV>(srcRsrc, rowoff + uint32_t(h * CS * int(sizeof(T))), po);
+            if constexpr (XH) {
+              if constexpr (sizeof(T) == 4) {
+                E[k] = x3_load16<E4>(srcRsrc, edgeoff, po);
+              } else {
+                const NV lo = x3_load16<NV>(srcRsrc, edgeoff, po), hi = x3_load16<NV>(srcRsrc, edgeoff + 16, po);
+                E[k] = E4{lo[0], lo[1], hi[0], hi[1]};
+              }
+            }
           };
-          // step t = -4 starts with src planes z+dz .. z+(NC-1)dz, z = z0 - 4dz, and the src row of its u1 plane
+          auto publish_src = [&](int bi, int k) {
+#pragma unroll
+            for (int h = 0; h < H; ++h) cs[bi][w][h][lane] = C[k][h];
+            if constexpr (XH)
+              if (edgeLane) ce[bi][w][side] = P2{E[k][1], E[k][2]};
+          };
+          // the end's cell adjacent to the column: x-1 (left, e[2] / the pair's [1]) or x+CW (right, e[1] / [0])
+          auto adj = [&](const P2 &p) -> T { return isR ? p[0] : p[1]; };
+          // step t = -4 starts with src planes z+dz .. z+3dz, z = z0 - 4dz, and the src row of its u1 plane
           // (z+2dz: slot 1) published
           {
             const int zw = z0 - 3 * dz;
 #pragma unroll
             for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, k);
+            publish_src(0, 1);
 #pragma unroll
-            for (int h = 0; h < H; ++h) {
-              cs[0][w][h][lane] = C[1][h];
+            for (int h = 0; h < H; ++h)
               U1a[h] = U1b[h] = U1c[h] = U2a[h] = U2b[h] = U2c[h] = C[1][h]; // overwritten before any use
-            }
+            U1Ea = U1Eb = U1Ec = P2{T(0), T(0)};
+            U2Ea = U2Eb = U2Ec = T(0);
             __syncthreads();
           }
           int buf = 0;
@@ -301,68 +330,85 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
           auto step = [&](auto phase, auto lvTag) -> bool {
             constexpr int k = decltype(phase)::value;
             constexpr int LV = decltype(lvTag)::value;
-            // slots: s0 = plane z+dz, s1 = z+2dz, s2 = z+3dz; sn receives z + NC dz (it held plane z)
+            // slots: s0 = plane z+dz, s1 = z+2dz, s2 = z+3dz; sn receives z + 4dz (it held plane z)
             constexpr int s0 = k % NC, s1 = (k + 1) % NC, s2 = (k + 2) % NC, sn = (k + NC - 1) % NC;
             if (t >= nzs) return false;
             const int z = z0 + t * dz;
+            const int nbuf = buf ^ 1;
             load_row(z + NC * dz, sn);
             NV o[H];
-            auto levels = [&](auto exactTag) -> T {
-              T m = T(1);
-              // every level reads the previous step's rows (buf): no level waits for another's LDS writes, so HOIST
-              // issues all of them right after the barrier (one LDS latency per step instead of three)
-              NV A1[H], B1[H], A2[H], B2[H], A3[H], B3[H];
-              auto rd = [&](NV(&sh)[2][NW][H][64], NV(&A)[H], NV(&B)[H]) {
+            // every level reads the previous step's rows (buf) and publishes into the other buffer (its readers
+            // finished last step) right after its update
+            if constexpr (LV >= 1) {
+              NV A[H], B[H];
 #pragma unroll
-                for (int h = 0; h < H; ++h) {
-                  A[h] = sh[buf][wA][h][lane];
-                  B[h] = sh[buf][wB][h][lane];
+              for (int h = 0; h < H; ++h) {
+                A[h] = cs[buf][wA][h][lane];
+                B[h] = cs[buf][wB][h][lane];
+              }
+              const RowSph rs = row_sph(z + 2 * dz);
+              row_update(C[s1], A, B, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0],
+                         XH ? (isR ? E[s1][1] : E[s1][2]) : T(0), U1a);
+              sphere_row(rs, U1a);
+              if constexpr (XH && R >= 2) {
+                // u1 at the end's cells (e[1], e[2]): x-neighbours in the lane's own load, y from LDS, z from the
+                // window's other planes
+                const P2 ya = ce[buf][wA][side], yb = ce[buf][wB][side];
+                const E4 &ec = E[s1], &ep = DOWN ? E[s0] : E[s2], &em = DOWN ? E[s2] : E[s0];
+                U1Ea = div6v<T, P2, 2>(sum6v<T, KIND>(P2{ec[2], ec[3]}, P2{ec[0], ec[1]}, yb, ya, P2{ep[1], ep[2]},
+                                                       P2{em[1], em[2]}));
+                if (KIND == 0 && rs.hit) {
+                  const int x1 = isR ? xcol + CW : xcol - 2;
+                  U1Ea[0] = sph_fix(rs, x1, U1Ea[0]);
+                  U1Ea[1] = sph_fix(rs, x1 + 1, U1Ea[1]);
                 }
-              };
-              if constexpr (HOIST) {
-                if constexpr (LV >= 1) rd(cs, A1, B1);
-                if constexpr (LV >= 2) rd(us, A2, B2);
-                if constexpr (LV >= 3) rd(vs, A3, B3);
+                if (edgeLane) ue[nbuf][w][side] = adj(U1Ea);
               }
-              if constexpr (LV >= 1) {
-                if constexpr (!HOIST) rd(cs, A1, B1);
-                m = __builtin_fminf(m, row_update(exactTag, C[s1], A1, B1, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], U1a));
-                sphere_row(row_sph(z + 2 * dz), U1a);
-                if constexpr (EARLYC)
+              publish_src(nbuf, s2);
+              if constexpr (R >= 1)
 #pragma unroll
-                  for (int h = 0; h < H; ++h) cs[buf ^ 1][w][h][lane] = C[s2][h];
-                if constexpr (EARLYW) // publish u1 now (the other buffer: its readers finished last step)
+                for (int h = 0; h < H; ++h) us[nbuf][w][h][lane] = U1a[h];
+            }
+            if constexpr (LV >= 2) {
+              NV A[H], B[H];
 #pragma unroll
-                  for (int h = 0; h < H; ++h) us[buf ^ 1][w][h][lane] = U1a[h];
+              for (int h = 0; h < H; ++h) {
+                A[h] = us[buf][wA][h][lane];
+                B[h] = us[buf][wB][h][lane];
               }
-              // (!NOSB) keep each level's LDS reads next to its update: at 144 VGPRs, hoisting all three levels'
-              // neighbour rows (48 VGPRs) to the top of the step spilled
-              if constexpr (!NOSB) __builtin_amdgcn_sched_barrier(0);
-              if constexpr (LV >= 2) {
-                if constexpr (!HOIST) rd(us, A2, B2);
-                m = __builtin_fminf(m, row_update(exactTag, U1c, A2, B2, DOWN ? U1b : U1a, DOWN ? U1a : U1b, U2a));
-                sphere_row(row_sph(z + dz), U2a);
-                if constexpr (EARLYW)
+              const RowSph rs = row_sph(z + dz);
+              row_update(U1c, A, B, DOWN ? U1b : U1a, DOWN ? U1a : U1b, XH ? adj(U1Ec) : T(0), U2a);
+              sphere_row(rs, U2a);
+              if constexpr (XH && R == 3) {
+                // u2 at the end's adjacent cell: x-neighbours the end's far u1 cell and the row's own first / last
+                // u1 cell, y from LDS, z the adjacent u1 cells of the planes before / after
+                const T far = isR ? U1Ec[1] : U1Ec[0];
+                const T inner = isR ? U1c[H - 1][V - 1] : U1c[0][0];
+                const T vmx = isR ? inner : far, vpx = isR ? far : inner;
+                const T ya = ue[buf][wA][side], yb = ue[buf][wB][side];
+                const T za = adj(U1Ea), zb = adj(U1Eb);
+                // (a pair: sum6v / div6v map an all -0 sum to +0 exactly as the single step's 0-started sum does)
+                U2Ea = div6v<T, P2, 2>(sum6v<T, KIND>(P2{vpx, vpx}, P2{vmx, vmx}, P2{yb, yb}, P2{ya, ya},
+                                                       DOWN ? P2{zb, zb} : P2{za, za}, DOWN ? P2{za, za} : P2{zb, zb}))[0];
+                if (KIND == 0 && rs.hit) U2Ea = sph_fix(rs, isR ? xcol + CW : xcol - 1, U2Ea);
+              }
+              if constexpr (R >= 2)
 #pragma unroll
-                  for (int h = 0; h < H; ++h) vs[buf ^ 1][w][h][lane] = U2a[h];
-              }
-              if constexpr (!NOSB) __builtin_amdgcn_sched_barrier(0);
-              if constexpr (LV >= 3) {
-                if constexpr (!HOIST) rd(vs, A3, B3);
-                m = __builtin_fminf(m, row_update(exactTag, U2c, A3, B3, DOWN ? U2b : U2a, DOWN ? U2a : U2b, o));
-                sphere_row(row_sph(z), o);
-              }
-              return m;
-            };
-            // exact quotients inline (div6v: the FMA-corrected quotient, a per-lane branch no lane normally takes for
-            // |sum| < 2^-100). A branch-free fast pass with a wave-uniform exact redo of the whole step needs more
-            // registers (the fast results stay live across the redo: 168 VGPRs + 21 spilled for Jacobi), so not used
-            (void)levels(std::true_type{});
+                for (int h = 0; h < H; ++h) vs[nbuf][w][h][lane] = U2a[h];
+            }
             if constexpr (LV >= 3) {
+              NV A[H], B[H];
+#pragma unroll
+              for (int h = 0; h < H; ++h) {
+                A[h] = vs[buf][wA][h][lane];
+                B[h] = vs[buf][wB][h][lane];
+              }
+              row_update(U2c, A, B, DOWN ? U2b : U2a, DOWN ? U2a : U2b, XH ? U2Ec : T(0), o);
+              sphere_row(row_sph(z), o);
               // unconditional: a row past the region's y end (the last row group) stores into a per-device sink, so
               // every path has the same vector-memory ops and the next step's load wait counts past these stores
               char *dp = outRow ? reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff
-                                : a.sink + lane * LS * int(sizeof(T));
+                                : a.sink + lane * V * int(sizeof(T));
 #pragma unroll
               for (int h = 0; h < H; ++h) {
                 NV *q = reinterpret_cast<NV *>(dp + h * CS * int(sizeof(T)));
@@ -372,13 +418,7 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
                   *q = o[h];
               }
             }
-            const int nbuf = buf ^ 1;
-#pragma unroll
-            for (int h = 0; h < H; ++h) {
-              if constexpr (!EARLYC || LV < 1) cs[nbuf][w][h][lane] = C[s2][h];
-              if constexpr (R >= 1 && !EARLYW) us[nbuf][w][h][lane] = U1a[h];
-              if constexpr (R >= 2 && !EARLYW) vs[nbuf][w][h][lane] = U2a[h];
-            }
+            if constexpr (LV < 1) publish_src(nbuf, s2);
             // boundary-plane publication (block-uniform, as the pairs): every wave's stores of output plane z
             // complete before the barrier, then one thread writes the L2 back (release) and counts the block's cells
             const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
@@ -387,7 +427,7 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
             if (pubStep && lane == 0 && w == 0) {
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
               const unsigned long long cells =
-                  (unsigned long long)(min(YO, a.hiy - yblk)) * (unsigned long long)(a.hix - a.lox);
+                  (unsigned long long)(min(YO, a.hiy - yblk)) * (unsigned long long)(XH ? CW : a.hix - a.lox);
               __hip_atomic_fetch_add(a.pub, cells, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             buf = nbuf;
@@ -398,6 +438,10 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
               U2b[h] = U2c[h];
               U2c[h] = U2a[h];
             }
+            U1Eb = U1Ec;
+            U1Ec = U1Ea;
+            U2Eb = U2Ec;
+            U2Ec = U2Ea;
             ++t;
             return true;
           };
@@ -405,7 +449,6 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
           using I1 = std::integral_constant<int, 1>;
           using I2 = std::integral_constant<int, 2>;
           using I3 = std::integral_constant<int, 3>;
-          using I4 = std::integral_constant<int, 4 % NC>;
           using L1 = std::integral_constant<int, (R < 1 ? R : 1)>;
           using L2 = std::integral_constant<int, (R < 2 ? R : 2)>;
           using LR = std::integral_constant<int, R>;
@@ -414,11 +457,7 @@ stencil7x3_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
           step(I1{}, L1{});
           step(I2{}, L2{});
           step(I3{}, L2{});
-          if constexpr (NC == 5)
-            while (step(I4{}, LR{}) && step(I0{}, LR{}) && step(I1{}, LR{}) && step(I2{}, LR{}) && step(I3{}, LR{})) {
-            }
-          else
-            while (step(I0{}, LR{}) && step(I1{}, LR{}) && step(I2{}, LR{}) && step(I3{}, LR{})) {
+          while (step(I0{}, LR{}) && step(I1{}, LR{}) && step(I2{}, LR{}) && step(I3{}, LR{})) {
           }
         };
         if (down)
@@ -483,32 +522,51 @@ static char *x3_sink(int dev, bool create) {
   return p;
 }
 
+// the column width of the XH form: two 16-B chunks per lane
+static int64_t x3_column_cells(int64_t elemSize) { return 2 * 64 * (16 / elemSize); }
+
 bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &region, const StencilTune &tune) {
-  // x wraps in-kernel (whole 512-cell rows, DPP rotates); y / z either wrap in-kernel too (one GPU: nothing is
-  // exchanged) or read 3-deep halos the exchange filled (an axis cut across GPUs / sub-domains)
-  if (dom.backend() != Backend::Device || !(tune.wrap & 1)) return false;
-  if (!(dom.dtype(qi) == DType::F32 || (dom.dtype(qi) == DType::Bytes && dom.elem_size(qi) == 4))) return false;
-  if (!(stencil7x2_wrappable_axes(dom, qi, 1) & 1)) return false;
+  if (dom.backend() != Backend::Device) return false;
+  const int64_t es = dom.elem_size(qi);
+  const bool f32 = dom.dtype(qi) == DType::F32 || (dom.dtype(qi) == DType::Bytes && es == 4);
+  const bool f64 = dom.dtype(qi) == DType::F64 || (dom.dtype(qi) == DType::Bytes && es == 8);
+  if (!f32 && !f64) return false;
   const Radius &rad = dom.radius();
-  if (!(tune.wrap & 2) && (rad.y(-1) < 3 || rad.y(1) < 3)) return false;
-  if (!(tune.wrap & 4) && (rad.z(-1) < 3 || rad.z(1) < 3)) return false;
+  const Dim3 n = dom.size();
+  const int wrapm = tune.wrap & 7;
+  if (wrapm & 1) {
+    // whole periodic rows: x wraps in-kernel by DPP rotates (fp32, exactly 512 cells)
+    if (!f32 || n.x != 512 || !(stencil7x2_wrappable_axes(dom, qi, 1) & 1)) return false;
+  } else {
+    // x from 3-deep halos, in columns of CW cells
+    if (rad.x(-1) < 3 || rad.x(1) < 3 || n.x % x3_column_cells(es) != 0) return false;
+  }
+  if (!(wrapm & 2) && (rad.y(-1) < 3 || rad.y(1) < 3)) return false;
+  if (!(wrapm & 4) && (rad.z(-1) < 3 || rad.z(1) < 3)) return false;
+  // S o S o S reaches (1, 2) / (2, 1) cells along two axes and (1, 1, 1) along three: every edge / corner halo whose
+  // axes are all read from halos must be exchanged (its extent spans the face depths, LocalDomain::halo_extent)
+  for (int i = 0; i < 27; ++i) {
+    const Dim3 d = dir_from_index(i);
+    const int nzc = (d.x != 0) + (d.y != 0) + (d.z != 0);
+    const bool halo = !((d.x != 0 && (wrapm & 1)) || (d.y != 0 && (wrapm & 2)) || (d.z != 0 && (wrapm & 4)));
+    if (nzc >= 2 && halo && rad.dir(d) < 1) return false;
+  }
   const Rect3 cr = dom.get_compute_region();
   if (!(region.lo == cr.lo && region.hi == cr.hi)) return false; // the kernel sweeps whole sub-domains
-  const Dim3 n = dom.size();
-  if (n.x != 512 || n.y < 3 || n.z < 16) return false;
+  if (n.y < 3 || n.z < 16) return false;
   if (dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096) return false; // 32-bit buffer-load offsets
   (void)x3_sink(dom.gpu(), true);
-  const int64_t lox = dom.radius().x(-1);
-  return (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + lox * 4) % 16 == 0) &&
-         (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + lox * 4) % 16 == 0) &&
-         (dom.pitch(qi).x * 4) % 16 == 0;
+  const int64_t lox = rad.x(-1);
+  return (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + lox * es) % 16 == 0) &&
+         (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.next_data(qi)) + lox * es) % 16 == 0) &&
+         (dom.pitch(qi).x * es) % 16 == 0;
 }
 
-template <int KIND, int PF, bool CONTIG, int VAR>
+template <typename T, int KIND, bool XH>
 static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
                        const StencilTune &tune) {
   constexpr int NW = 12, YO = NW - 6;
-  StencilArgs<float> a = make_args<float>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
+  StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
   a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
   a.nt = tune.nontemporal ? 1 : 0;
   a.wrapm = tune.wrap & 7;
@@ -517,11 +575,11 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   if (!(a.wrapm & 4)) a.wn[2] = 0;
   a.x0 = a.lox;
   a.remap = tune.xcdRemap ? 1 : 0;
-  const int ny = a.hiy - a.loy, nz = a.hiz - a.loz;
-  a.gx = 1;
+  const int nx = a.hix - a.lox, ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  a.gx = XH ? int(nx / x3_column_cells(int64_t(sizeof(T)))) : 1;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = (const void *)stencil7x3_row_kernel<NW, PF, KIND, CONTIG, VAR>;
-  const int64_t cols = a.gy;
+  const void *kern = (const void *)stencil7x3_row_kernel<T, KIND, XH>;
+  const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x3_resident_blocks(kern, 64 * NW);
   // CUs left to the transport kernels running beside the sweep (pipelined triples: the gated exchange)
   int cus = 256;
@@ -565,41 +623,29 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   ZPartBounds zb{};
   zb.on = 0;
   if (KIND == 0 && a.seg == 2)
-    sphere_part_bounds(zb, a, int64_t(blocks) / a.zparts, a.zparts, NW, YO, 3, tune.x3sphw);
+    sphere_part_bounds(zb, a, std::min<int64_t>(int64_t(blocks) / a.zparts, a.gy), a.zparts, NW, YO, 3, tune.x3sphw);
   dom.set_device();
   a.sink = x3_sink(dom.gpu(), false);
   a.clk = reinterpret_cast<unsigned long long *>(tune.blockClock);
   STENCIL_REQUIRE(a.sink, "stencil7x3: no store sink on device " << dom.gpu() << " (stencil7x3_supported first)");
-  hipLaunchKernelGGL((stencil7x3_row_kernel<NW, PF, KIND, CONTIG, VAR>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+  hipLaunchKernelGGL((stencil7x3_row_kernel<T, KIND, XH>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   HIP_CHECK(hipGetLastError());
 }
 
 bool stencil7x3_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
                       hipStream_t stream, const StencilTune &tune) {
   if (!stencil7x3_supported(dom, qi, region, tune)) return false;
-  // instantiated: x3var 7 (the default) and 0 (r5/s: everything published before the barrier), both layouts, one or
-  // two planes of lookahead; r5/v measured 1 / 3 / 5 between them (profiles/r5/v/summary.txt)
-  STENCIL_REQUIRE(tune.x3var == 0 || tune.x3var == 7 || tune.x3var == 15,
-                  "stencil7x3: x3var " << tune.x3var << " not instantiated (0, 7, 15)");
-  STENCIL_REQUIRE(tune.x3pf == 1 || tune.x3pf == 2, "stencil7x3: x3pf " << tune.x3pf << " (1, 2)");
-  const bool contig = tune.x3layout == 1, pf2 = tune.x3pf == 2;
-  auto go = [&](auto kindTag, auto pfTag) {
-    constexpr int K = decltype(kindTag)::value, P = decltype(pfTag)::value;
-    if (contig)
-      tune.x3var == 7 ? apply_x3_t<K, P, true, 7>(dom, qi, region, sph, stream, tune)
-                      : apply_x3_t<K, P, true, 0>(dom, qi, region, sph, stream, tune);
-    else if (tune.x3var == 15)
-      apply_x3_t<K, P, false, 15>(dom, qi, region, sph, stream, tune);
-    else
-      tune.x3var == 7 ? apply_x3_t<K, P, false, 7>(dom, qi, region, sph, stream, tune)
-                      : apply_x3_t<K, P, false, 0>(dom, qi, region, sph, stream, tune);
-  };
-  using P1 = std::integral_constant<int, 1>;
-  using P2 = std::integral_constant<int, 2>;
-  if (kind == StencilKind::Jacobi)
-    pf2 ? go(std::integral_constant<int, 0>{}, P2{}) : go(std::integral_constant<int, 0>{}, P1{});
-  else
-    pf2 ? go(std::integral_constant<int, 1>{}, P2{}) : go(std::integral_constant<int, 1>{}, P1{});
+  const bool jac = kind == StencilKind::Jacobi, xh = !(tune.wrap & 1);
+  if (dom.elem_size(qi) == 8) {
+    jac ? apply_x3_t<double, 0, true>(dom, qi, region, sph, stream, tune)
+        : apply_x3_t<double, 1, true>(dom, qi, region, sph, stream, tune);
+  } else if (xh) {
+    jac ? apply_x3_t<float, 0, true>(dom, qi, region, sph, stream, tune)
+        : apply_x3_t<float, 1, true>(dom, qi, region, sph, stream, tune);
+  } else {
+    jac ? apply_x3_t<float, 0, false>(dom, qi, region, sph, stream, tune)
+        : apply_x3_t<float, 1, false>(dom, qi, region, sph, stream, tune);
+  }
   return true;
 }
 

@@ -19,15 +19,16 @@ StencilModel::StencilModel(const StencilModelConfig &cfg, std::shared_ptr<comm::
   }
   if (cfg.temporal >= 2) {
     // S o S of a 7-point stencil reaches 2 cells along an axis and 1 cell diagonally (edges), never corners;
-    // S o S o S 3 along an axis and (1, 2) / (2, 1) on edges (an edge halo spans the face depths of its two axes,
-    // LocalDomain::halo_extent, so a nonzero edge radius is enough). Its (1, 1, 1) corners involve x, which the
-    // triples always wrap in-kernel (stencil7x3_supported), so corners stay out of the exchange
+    // S o S o S 3 along an axis, (1, 2) / (2, 1) on edges and (1, 1, 1) in corners (an edge / corner halo spans the
+    // face depths of its axes, LocalDomain::halo_extent, so a nonzero radius is enough). Corners matter only where x
+    // is read from halos (the triples' XH form); wherever x wraps in-kernel their messages are skipped with the other
+    // self copies or carry a few hundred bytes
     const int64_t face = cfg.temporal >= 3 ? 3 : 2;
     for (int i = 0; i < 27; ++i) {
       const Dim3 d = dir_from_index(i);
       const int nz = (d.x != 0) + (d.y != 0) + (d.z != 0);
       if (nz == 1) r.dir(d) = std::max<int64_t>(r.dir(d), face);
-      if (nz == 2) r.dir(d) = std::max<int64_t>(r.dir(d), 1);
+      if (nz == 2 || (nz == 3 && cfg.temporal >= 3)) r.dir(d) = std::max<int64_t>(r.dir(d), 1);
     }
   }
   dd_->set_radius(r);
@@ -243,11 +244,12 @@ void StencilModel::init() {
   if (confinedSelf_) dd_->set_translate_max_blocks(cfg_.tune.x2reserve);
   // overlapped pairs with the slabs after the interior sweep (set_overlap_mode(2)) from the start
   slabsAfter_ = pairs_ && overlap_ && cfg_.overlapMode == 2;
-  // fused triples: device sub-domains whose x axis wraps in-kernel (whole 512-cell rows); y / z wrap in-kernel too
-  // (one GPU: nothing is exchanged) or read the 3-deep halos of a depth-3 exchange, one per three steps (multi-GPU).
+  // fused triples: device sub-domains of whole 512-cell fp32 rows wrapped in-kernel, or of 512-cell fp32 / 256-cell
+  // fp64 columns whose x halos come from the exchange (stencil7x3_supported); each other axis wraps in-kernel (its
+  // self copies leave the exchange) or reads the 3-deep halos of a depth-3 exchange, one per three steps.
   // Whole regions only, so not beside an overlapped exchange (set_overlap switches between the two). The spheres at
   // least 3 cells from the periodic faces (the intermediate steps evaluate them at unwrapped halo coordinates)
-  triples_ = pairs_ && cfg_.temporal >= 3 && stepDevice && (pairTune_.wrap & 1);
+  triples_ = pairs_ && cfg_.temporal >= 3 && stepDevice;
   if (triples_ && sph_.enabled) {
     const Dim3 L = cfg_.size;
     for (const Dim3 &c : {sph_.hot, sph_.cold}) {
@@ -583,6 +585,8 @@ void StencilModel::set_overlap(bool on) {
   overlap_ = on;
   triples_ = triplesOk_ && !on; // whole-region sweeps: triples where supported
   dd_->set_comm_max_blocks(on ? cfg_.tune.x2reserve : 0);
+  // the same-GPU translate stays confined only while an overlapped sweep leaves it those CUs
+  dd_->set_translate_max_blocks(on && confinedSelf_ ? cfg_.tune.x2reserve : 0);
 }
 
 void StencilModel::set_overlap_mode(int mode) {
@@ -606,7 +610,7 @@ void StencilModel::set_comm_reserve(int cus) {
   pairTune_.x2reserve = cus;
   stepTune_.x2reserve = cus;
   if (overlap_ || pipelined3_) dd_->set_comm_max_blocks(cus);
-  if (confinedSelf_) dd_->set_translate_max_blocks(cus);
+  if (confinedSelf_ && overlap_) dd_->set_translate_max_blocks(cus);
 }
 
 void StencilModel::synchronize() {

@@ -67,3 +67,30 @@ def test_two_ranks_transport_chosen_by_measurement():
     assert tr["peer_store"]["devices_used"] >= 1
     assert tr["astaroth_q8"]["halo_bytes"] > tr["ref_rule"]["halo_bytes"]
     assert lines[-1]["n_gpus"] == 2 and lines[-1]["config"]["decomposition"] == "1x1x2"
+
+
+def test_tune_budget_skips_candidates_and_phases_are_reported():
+    """--tune-budget bounds the N > 1 warm-up: with no budget every transport candidate is skipped (agreed over ranks)
+    and the model is built with the fixed transports; config.phases_s names every phase that ran, and the reference's
+    trimean exchange statistic (bin/bench_exchange.cu:39-63) is reported next to the mean."""
+    r = subprocess.run([sys.executable, BENCH, *ARGS, "--gpus", "2", "--tune-budget", "0", "--transport-sweep", "off"],
+                       env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _lines(r.stdout)
+    assert len(lines) == 1
+    cfg, extra = lines[0]["config"], lines[0]["extra"]
+    tt = cfg["transport_tuned"]
+    assert all("skipped" in tt[k] for k in ("colo_uncached", "colo_fine", "colo_coarse", "rccl")), tt
+    assert tt["chosen"].startswith("fixed")
+    for k in ("startup", "transport_warmup", "build", "timed_loop", "exchange_loops"):
+        assert k in cfg["phases_s"], cfg["phases_s"]
+    assert extra["halo_exchange_trimean_GBps"] is not None and extra["exchange_trimean_ms"] > 0
+    assert cfg["tune"]["x3sched"] == 1
+
+
+def test_tune_switch_sets_stencil_tune_fields():
+    r = subprocess.run([sys.executable, BENCH, *ARGS, "--tune", "x3sphw=0.5,nontemporal=0"], env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    t = _lines(r.stdout)[0]["config"]["tune"]
+    assert abs(t["x3sphw"] - 0.5) < 1e-6 and t["nontemporal"] is False

@@ -148,14 +148,14 @@ def test_device_exchange_float_views(st):
     assert check_exchange(dd, q, radius) == 0
 
 
-def _gather(model):
+def _gather(model, q=0):
     dd = model.domain
     L = dd.size()
     g = None
     for di in range(dd.num_domains()):
         d = dd.domain(di)
         o, s = d.origin(), d.size()
-        t = model.interior(di).cpu()
+        t = model.interior(di, q).cpu()
         if g is None:
             g = torch.zeros(L.z, L.y, L.x, dtype=t.dtype)
         g[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x] = t
@@ -300,27 +300,21 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
             assert torch.equal(_gather(m), u), f"wrap_axes={m.wrap_axes()} after run({n})"
 
 
-@pytest.mark.parametrize("sched,layout,var,pf,scale", [(0, 0, 7, 1, 1.0), (1, 0, 7, 1, 1.0), (1, 1, 7, 1, 1.0),
-                                                       (1, 0, 0, 1, 1.0), (1, 0, 7, 2, 1.0), (1, 1, 0, 2, 1.0),
-                                                       (1, 0, 7, 1, 1e-33), (1, 1, 7, 2, 1e-33),
-                                                       (1, 0, 15, 1, 1.0), (1, 0, 15, 2, 1e-33)])
+@pytest.mark.parametrize("sched,scale", [(0, 1.0), (1, 1.0), (1, 1e-33)])
 @pytest.mark.parametrize("kind,size", [("jacobi", (512, 120, 116)), ("jacobi", (512, 128, 120)),
                                        ("jacobi", (512, 512, 112)), ("astaroth", (512, 36, 28)),
                                        ("astaroth", (512, 13, 17)), ("astaroth", (512, 3, 16))])
-def test_temporal3_matches_three_single_steps(st, kind, size, sched, layout, var, pf, scale):
+def test_temporal3_matches_three_single_steps(st, kind, size, sched, scale):
     """Fused triples (stencil7x3_row_kernel, temporal=3, one GPU, every axis wrapped in-kernel): S(S(S(u))) bitwise
     equal to three single steps of the torch oracle; run(n) covers whole hipGraph blocks (18 steps), triples and the
     pair / single-step remainders; y extents that are not a multiple of the block's 6 output rows and a 3-row grid
-    (every block row wraps onto itself twice). Both lane layouts (x3layout: 8 adjacent cells per lane, or chunks 256
-    apart); scale 1e-33 puts every sum below 2^-100, where the quotient is the true division."""
+    (every block row wraps onto itself twice). scale 1e-33 puts every sum below 2^-100, where the quotient is the
+    true division."""
     from stencil2_amd.ops import astaroth_step_reference
     cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
                     else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
     t = st.StencilTune()
     t.x3sched = sched
-    t.x3layout = layout
-    t.x3var = var
-    t.x3pf = pf
     m = cls(size, gpus=[0], temporal=3, tune=t, **kw)
     m.init()
     assert m.temporal_triples() and m.wrap_axes() == 7
@@ -337,6 +331,56 @@ def test_temporal3_matches_three_single_steps(st, kind, size, sched, layout, var
         m.synchronize()
         for q in range(kw.get("quantities", 1)):
             got = m.interior(0, q)
+            bad = int((got != u).sum())
+            assert bad == 0, f"run({n}) q{q}: {bad} cells differ, max {(got - u).abs().max().item()}"
+
+
+def _set_field(m, u, quantities=1):
+    for di in range(m.domain.num_domains()):
+        d = m.domain.domain(di)
+        o, s = d.origin(), d.size()
+        for q in range(quantities):
+            m.interior(di, q).copy_(u[o.z:o.z + s.z, o.y:o.y + s.y, o.x:o.x + s.x].to(m.interior(di, q).dtype))
+    torch.cuda.synchronize()
+
+
+# x cut by cost (1, 4, 4); (4, 3, 2) keeps x whole (z, then y cut)
+@pytest.mark.parametrize("kind,size,fp64,gpus,cost,scale", [
+    ("jacobi", (512, 120, 116), False, [0], None, 1.0), ("jacobi", (1024, 240, 232), False, [0], None, 1.0),
+    ("astaroth", (512, 36, 28), False, [0], None, 1.0), ("astaroth", (1536, 13, 17), False, [0], None, 1.0),
+    ("astaroth", (512, 3, 16), False, [0], None, 1e-33), ("jacobi", (512, 120, 116), False, [0], None, 1e-33),
+    ("jacobi", (256, 64, 64), True, [0], None, 1.0), ("astaroth", (512, 20, 24), True, [0], None, 1.0),
+    ("astaroth", (256, 12, 16), True, [0], None, 1e-300),
+    ("jacobi", (1024, 240, 232), False, [0, 0], (1, 4, 4), 1.0), ("astaroth", (2048, 30, 20), False, [0, 0, 0, 0], (1, 4, 4), 1.0),
+    ("astaroth", (512, 40, 64), False, [0, 0, 0, 0], (4, 3, 2), 1.0), ("jacobi", (512, 240, 232), False, [0, 0], (4, 2, 3), 1.0),
+    ("astaroth", (512, 24, 40), True, [0, 0], (1, 4, 4), 1.0)])
+def test_temporal3_x_halos(st, kind, size, fp64, gpus, cost, scale):
+    """Fused triples reading x from 3-deep halos (stencil7x3 XH form: 512-cell fp32 / 256-cell fp64 columns, the 3
+    cells beyond each column end loaded per lane half, u1 / u2 computed on the column-end cells): every halo copied
+    each triple (wrap_self=False: BASELINE config 2 as defined, one depth-3 exchange per three steps), on one
+    sub-domain and on 2 / 4 sub-domains of one GPU with x, y or z cut; 1-3 columns per row; fp64; tiny sums (true
+    division). Bitwise equal to single steps of the torch oracle, through graph blocks, triples and remainders."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 2}))
+    if cost is not None:
+        kw["axis_cost"] = cost
+    m = cls(size, gpus=gpus, temporal=3, fp64=fp64, wrap_self=False, **kw)
+    m.init()
+    assert m.temporal_triples() and m.wrap_axes() == 0, f"triples {m.temporal_triples()} wrap {m.wrap_axes()}"
+    m.prepare()
+    dt = torch.float64 if fp64 else torch.float32
+    u = torch.rand((size[2], size[1], size[0]), device="cuda", dtype=dt,
+                   generator=torch.Generator(device="cuda").manual_seed(7)) * scale
+    nq = kw.get("quantities", 1)
+    _set_field(m, u, nq)
+    for n in (3, 7, 2, 20, 1):
+        m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        m.synchronize()
+        for q in range(nq):
+            got = _gather(m, q).to(u.device)
             bad = int((got != u).sum())
             assert bad == 0, f"run({n}) q{q}: {bad} cells differ, max {(got - u).abs().max().item()}"
 
@@ -988,21 +1032,28 @@ def test_staged_two_ranks_one_gpu():
         assert rc == 0, out[-3000:]
 
 
-def test_headline_config_bitwise(st):
-    """BASELINE config 2 exactly as bench.py runs it: 512^3 Jacobi3D fp32 on one GPU, bench.py's default StencilTune
-    (whole-row fused pairs, lockstep quarter-major schedule, x/y/z wrapped in-kernel so no halo is copied),
-    prepare()'d hipGraph blocks of 16 steps, 20 steps from a random field; bitwise vs the torch oracle on GPU
-    tensors (reference test style: test/test_exchange.cu:135-201)."""
-    m = st.Jacobi3D((512, 512, 512), gpus=[0], temporal=2, tune=st.StencilTune())
+@pytest.mark.parametrize("with_exchange", [False, True])
+def test_headline_config_bitwise(st, with_exchange):
+    """The driver's exact path: `bench.py --gpus 1 --steps 20 --warmup 5` builds this model (512^3 Jacobi3D fp32 on
+    one GPU, temporal=3, bench.py's default StencilTune: lockstep triples with 0.3-weighted sphere parts, 128-B
+    interiors, MaxLink decomposition), prepare()s the 18-step hipGraph blocks, runs 5 warm-up steps and times 20.
+    with_exchange: the same with every halo copied each triple (wrap_self=False, shared halo lines: bench.py's
+    extra.gcells_with_exchange model, BASELINE config 2 as defined, fused triples reading x from halos). From a
+    random field, bitwise vs the torch oracle on GPU tensors (reference test style: test/test_exchange.cu:135-201)."""
+    m = st.Jacobi3D((512, 512, 512), gpus=[0], temporal=3, tune=st.StencilTune(), axis_cost=(4, 3, 2),
+                    partition=st.PartitionObjective.MaxLink, wrap_self=not with_exchange,
+                    shared_halo_line=with_exchange)
     m.init()
-    assert m.temporal_blocking() and m.wrap_axes() == 7 and not m.overlapping()
+    assert m.temporal_triples() and not m.overlapping()
+    assert m.wrap_axes() == (0 if with_exchange else 7)
     m.prepare()
     u = torch.rand((512, 512, 512), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
     m.interior(0).copy_(u)
     torch.cuda.synchronize()
+    m.run(5)
     m.run(20)
     m.synchronize()
-    for _ in range(20):
+    for _ in range(25):
         u = jacobi_step_reference(u)
     got = m.interior(0)
     assert torch.equal(got, u), f"{int((got != u).sum())} cells differ"
