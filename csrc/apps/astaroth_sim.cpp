@@ -19,7 +19,7 @@ int main(int argc, char **argv) {
   ArgParser p("Astaroth proxy (reference bin/astaroth_sim.cu)");
   p.option(&x, "--x", "x").option(&y, "--y", "y").option(&z, "--z", "z").option(&iters, "-n,--iters", "iterations")
       .option(&nq, "--q", "quantities")
-      .option(&temporal, "--temporal", "steps fused per sweep (1 or 2)")
+      .option(&temporal, "--temporal", "steps fused per sweep (1, 2, or 3: fused triples, one depth-3 exchange per three steps)")
       .flag(&noOverlap, "--no-overlap", "no overlap")
       .flag(&forceOverlap, "--overlap", "overlap the interior sweep with the exchange even when every halo is a "
                                         "same-GPU copy (one GPU, --no-wrap: the reference's iteration)")
@@ -54,7 +54,10 @@ int main(int argc, char **argv) {
   cfg.wrapSelf = !noWrap;
   StencilModel m(cfg, pg);
   m.init();
-  const int per = m.temporal_blocking() ? 2 : 1; // timed unit = one sweep, reported per step
+  const int per = m.steps_per_sweep(); // timed unit = one sweep (1, 2 or 3 steps), reported per step
+  if (pg->rank() == 0)
+    std::fprintf(stderr, "# astaroth_sim: %d step(s) per sweep, in-kernel wrap axes %d, overlap %d\n", per, m.wrap_axes(),
+                 int(m.overlapping()));
   m.run(per);
   m.synchronize();
   Statistics st;

@@ -35,7 +35,7 @@ int main(int argc, char **argv) {
       .option(&iters, "-n,--iters", "iterations")
       .option(&warmup, "--warmup", "untimed warmup iterations")
       .option(&period, "-q,--period", "ParaView dump period")
-      .option(&temporal, "--temporal", "steps fused per sweep (2: temporal blocking, one depth-2 exchange per pair)")
+      .option(&temporal, "--temporal", "steps fused per sweep (2: fused pairs, one depth-2 exchange per pair; 3: fused triples, one depth-3 exchange per three steps)")
       .positional(&x, "x", "per-GPU x")
       .positional(&y, "y", "per-GPU y")
       .positional(&z, "z", "per-GPU z");
@@ -73,8 +73,11 @@ int main(int argc, char **argv) {
     StencilModel model(cfg, pg);
     model.init();
     if (paraview) model.domain().write_paraview(prefix + "jacobi3d_init");
-    // one timed unit = one sweep: a step, or a fused pair of steps with --temporal 2 (time reported per step)
-    const int per = model.temporal_blocking() ? 2 : 1;
+    // one timed unit = one sweep: a step, a fused pair or a fused triple (time reported per step)
+    const int per = model.steps_per_sweep();
+    if (pg->rank() == 0)
+      std::fprintf(stderr, "# jacobi3d: %d step(s) per sweep, in-kernel wrap axes %d, overlap %d\n", per,
+                   model.wrap_axes(), int(model.overlapping()));
     for (int i = 0; i < warmup; ++i) model.run(per);
     model.synchronize();
     for (int i = 0; i < iters; ++i) {

@@ -465,6 +465,7 @@ PYBIND11_MODULE(_C, m) {
       .def("halo_coords", &LocalDomain::halo_coords)
       .def("halo_extent", py::overload_cast<const Dim3 &>(&LocalDomain::halo_extent, py::const_))
       .def("halo_bytes", &LocalDomain::halo_bytes)
+      .def("buffer_bytes", &LocalDomain::buffer_bytes)
       .def("accessor_origin", &LocalDomain::accessor_origin)
       .def("parity", &LocalDomain::parity)
       .def("curr_ptr", [](const LocalDomain &d, int64_t q) { return reinterpret_cast<uintptr_t>(d.curr_data(q)); })

@@ -54,6 +54,10 @@ template <typename T>
 __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<T> &a, const ZPartBounds &B, uint32_t lb, uint32_t nb,
                                              uint32_t ncols, uint32_t gy, uint32_t nzt) {
   X3Seg r{0, 0, 0, 0, false};
+  if (a.seg == 3) { // rounds of whole column groups (x3_round): parts alternate their z direction as in seg 2
+    r.odd = ((lb / (nb / uint32_t(a.zparts))) & 1) != 0;
+    return r;
+  }
   if (a.seg == 2) {
     const uint32_t P = uint32_t(a.zparts), cm = nb / P;
     const uint32_t qq = lb / cm, col = lb % cm;
@@ -86,6 +90,27 @@ __device__ __forceinline__ X x3_load16(__amdgpu_buffer_rsrc_t rs, uint32_t voff,
   return __builtin_bit_cast(X, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 }
 
+// whole-wave DPP row shifts (16-lane rows; the XH edge waves keep rows 0..11 in lanes 0..11): lane i <- lane i+1 /
+// lane i-1 (the lanes shifted in from outside a row are never used)
+__device__ __forceinline__ float x3_row_next(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x101, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float x3_row_prev(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x111, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double x3_row_next(double v) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp(int(b), 0x101, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), 0x101, 0xf, 0xf, false);
+  return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
+}
+__device__ __forceinline__ double x3_row_prev(double v) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp(int(b), 0x111, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), 0x111, 0xf, 0xf, false);
+  return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
+}
+
 template <typename T, int KIND, bool XH>
 __global__ __launch_bounds__(64 * 12, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
@@ -102,8 +127,9 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
   __shared__ NV cs[2][NW][H][64]; // src rows  (plane z+3dz at publish)
   __shared__ NV us[2][NW][H][64]; // u1 rows   (plane z+2dz at publish)
   __shared__ NV vs[2][NW][H][64]; // u2 rows   (plane z+dz at publish)
-  __shared__ P2 ce[2][NW][2];     // XH: src at (x-2, x-1) [0] and (x+CW, x+CW+1) [1] of the published rows
-  __shared__ T ue[2][NW][2];      // XH: u1 at x-1 [0] and x+CW [1]
+  // XH: each row's cell just beyond its column end ([0] x-1, [1] x+CW) for the row's own updates: src (z+3dz), u1
+  // (z+2dz), u2 (z+dz) at publish, written by the edge waves
+  __shared__ T es[2][NW][2], eu[2][NW][2], ev[2][NW][2];
 
   const uint32_t nb = gridDim.x;
   const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
@@ -113,34 +139,47 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
   const uint32_t gy = uint32_t(a.gy);
   const X3Seg sg = x3_segments(a, zbounds, lb, nb, uint32_t(a.gx) * gy, gy, nzt);
   const bool lane0 = lane == 0, lane63 = lane == 63;
-  // XH: lanes 32-63 hold the right column end's cells (lane 63 uses them), lanes 0-31 the left end's (lane 0)
-  const int side = lane >> 5;
-  const bool isR = side != 0;
-  const bool edgeLane = lane0 || lane63;
+  const int side = lane >> 5; // XH: lane 0 reads the left end's cells, lane 63 the right end's
   const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
   const int zwn = a.wn[2], zwlo = a.wlo[2], zwhi = a.wlo[2] + a.wn[2];
-  // raw buffer over the source field (offsets from raw [0,0,0] are non-negative and below 4 GiB: checked by the host)
-  const __amdgpu_buffer_rsrc_t srcRsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(a.src), 0, -1, 0x00020000);
   auto zcl = [&](int zz) {
     zz += zz < zwlo ? zwn : 0;
     zz -= zz >= zwhi ? zwn : 0;
     return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
   };
+  auto ywrap = [&](int yy) {
+    yy = yy < a.wlo[1] ? yy + a.wn[1] : (yy >= a.wlo[1] + a.wn[1] ? yy - a.wn[1] : yy);
+    return yy < 0 ? 0 : (yy > a.rawYm1 ? a.rawYm1 : yy);
+  };
   // The wave's role = the levels its row computes (wave-uniform): 0 on rows 0 / 11 (source rows only), 1 (u1) on 1 /
   // 10, 2 (u1, u2) on 2 / 9, 3 (u1, u2, u3 = output) on 3..8. The whole march is instantiated per role, and the
   // warm-up steps (fewer valid levels) are unrolled separately, so the steady-state step has no role or level
-  // branches. XH edges: u1 at the column ends feeds the u2 of the row itself and of its y-neighbours (roles >= 2
-  // compute it), u2 at the column ends only the row's own u3 (role 3).
+  // branches. XH: rows 0 / 11 are role 4, the edge waves: besides their source row, wave 0 computes the left column
+  // end of all 12 rows (lane r = row r) and wave 11 the right end - src loads, u1 at the two cells beyond the end, u2
+  // at the adjacent one, y-neighbours by DPP row shifts - and publishes each row's adjacent cell per level through
+  // LDS. The output waves then carry no edge state: one LDS read per level on lanes 0 / 63.
   auto body = [&](auto roleTag) {
     constexpr int R = decltype(roleTag)::value;
+    constexpr int RM = R == 4 ? 0 : R; // levels of the wave's own row
+    constexpr bool EDGE = XH && R == 4;
     bool odd = sg.odd;
     const bool pubOrder = a.pub != nullptr;
-    for (int pp = 0; pp < 2; ++pp) {
+    const uint32_t ncols = uint32_t(a.gx) * gy;
+    const int npass = XH && a.seg == 3 ? a.zrounds : 2; // rounds: XH only (many columns), fewer SGPRs elsewhere
+    for (int pp = 0; pp < npass; ++pp) {
       // publishing: the leftover row groups' short second segments first (their face planes would otherwise come
       // out last), the main lockstep segment in its fixed direction
       const int pass = pubOrder ? 1 - pp : pp;
       uint32_t s = pass == 0 ? sg.s : sg.s2;
-      const uint32_t e = pass == 0 ? sg.e : sg.e2;
+      uint32_t e = pass == 0 ? sg.e : sg.e2;
+      if (XH && a.seg == 3) {
+        // round pp: column group pp cm + lb % cm, z part lb / cm (every block on y-adjacent columns in step)
+        const uint32_t P = uint32_t(a.zparts), cm = nb / P, qq = lb / cm;
+        const uint32_t colr = uint32_t(pp) * cm + lb % cm;
+        if (colr >= ncols) break;
+        s = colr * nzt + qq * nzt / P;
+        e = colr * nzt + (qq + 1) * nzt / P;
+      }
       while (s < e) { // block-uniform
         const uint32_t col = s / nzt;
         const int zo = int(s - col * nzt);
@@ -159,16 +198,19 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
         const int y = yblk - 3 + w;
         if (yblk >= a.hiy) continue;
         const bool outRow = R == 3 && y < a.hiy;
-        int yw = y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y);
-        yw = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
+        const int yw = ywrap(y);
         const int xcol = a.x0 + bx * CW; // first cell of the column
         const int xb = xcol + lane * V;  // chunk h at xb + h * CS
         const uint32_t rowoff = uint32_t((yw * int64_t(a.px) + xb) * int64_t(sizeof(T)));
         const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
-        // XH: 4 cells from x-3 (left half) / x+CW-1 (right half): the edge cells (e[1], e[2]) and their outer and
-        // inner x-neighbours (e[0], e[3]), so both ends compute u1 at (e[1], e[2]) with the same lane code
-        const int xe = isR ? xcol + CW - 1 : xcol - 3;
-        const uint32_t edgeoff = uint32_t((yw * int64_t(a.px) + xe) * int64_t(sizeof(T)));
+        // XH edge waves: lane r holds row r's 4 cells from x-3 (wave 0) / x+CW-1 (wave 11): the two cells beyond the
+        // end (e[1], e[2]) and their outer and inner x-neighbours (e[0], e[3])
+        const int eside = w == NW - 1 ? 1 : 0;
+        const int er = lane < NW ? lane : NW - 1;
+        const int ey = yblk - 3 + er;
+        const int eyh = (ey - a.hy) * (ey - a.hy), eyc = (ey - a.cy) * (ey - a.cy); // Jacobi spheres, edge lanes
+        const uint32_t edgeoff =
+            uint32_t((ywrap(ey) * int64_t(a.px) + (eside ? xcol + CW - 1 : xcol - 3)) * int64_t(sizeof(T)));
 
         // spheres (Jacobi): the planes P of this row that cross the hot / cold sphere form two intervals
         // |P - c.z| <= h (h * h < r1sq - dy^2), computed once per segment; per-cell tests only on those planes
@@ -183,7 +225,7 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
           return h;
         };
         int hzlo = 1, hzhi = 0, czlo = 1, czhi = 0; // empty intervals
-        if (KIND == 0 && a.r1sq > 0) {
+        if (KIND == 0 && a.r1sq > 0 && !EDGE) {
           const int dyh = a.r1sq - (y - a.hy) * (y - a.hy), dyc = a.r1sq - (y - a.cy) * (y - a.cy);
           if (dyh > 0) {
             const int h = isqrt_below(dyh);
@@ -209,50 +251,27 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
         // distances loop invariants, so a cell costs a compare and a select per sphere. Cheaper variants measured
         // slower (an x interval per row, tests only on the chunk the sphere reaches; profiles/r5/ai, aj, ap); the
         // blocks of sphere-crossing rows are evened out by sphere-weighted z parts (x3sphw, profiles/r5/ao)
-        auto sph_fix = [&](const RowSph &rs, int x, T v) -> T {
-          const bool hot = (x - a.hx) * (x - a.hx) < a.r1sq - rs.dh;
-          const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - rs.dc;
+        auto sph_fix = [&](int dh, int dc, int x, T v) -> T {
+          const bool hot = (x - a.hx) * (x - a.hx) < a.r1sq - dh;
+          const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - dc;
           return hot ? T(1) : (cold ? T(0) : v);
         };
         auto sphere_row = [&](const RowSph &rs, NV(&o)[H]) {
           if (KIND == 0 && rs.hit) {
-            // XH: the cell coordinates through an opaque copy, so the per-cell squared distances are recomputed on
-            // the sphere rows instead of held in 16 VGPRs over the march (the XH edges need them: 44 spilled)
-            int x0 = xb;
-            if constexpr (XH) asm volatile("v_mov_b32 %0, %1" : "=v"(x0) : "v"(xb));
-#ifdef X3_EXP_SPH2
-            // interval form: per row-plane x ranges [lo, lo + len) of the two spheres (uniform), per cell one
-            // unsigned compare per sphere
             const int Dh = a.r1sq - rs.dh, Dc = a.r1sq - rs.dc;
-            auto rng = [&](int D, int c, int &lo, unsigned &len) {
-              if (D <= 0) { lo = 0; len = 0; return; }
-              int h = int(__builtin_sqrtf(float(D - 1)));
-              while (h > 0 && h * h > D - 1) --h;
-              while ((h + 1) * (h + 1) <= D - 1) ++h;
-              lo = c - h; len = unsigned(2 * h + 1);
-            };
-            int lh, lc; unsigned nh, nc;
-            rng(Dh, a.hx, lh, nh);
-            rng(Dc, a.cx, lc, nc);
-            lh = __builtin_amdgcn_readfirstlane(lh); lc = __builtin_amdgcn_readfirstlane(lc);
-            nh = __builtin_amdgcn_readfirstlane(nh); nc = __builtin_amdgcn_readfirstlane(nc);
 #pragma unroll
             for (int h = 0; h < H; ++h)
 #pragma unroll
               for (int k = 0; k < V; ++k) {
-                const int x = x0 + h * CS + k;
-                o[h][k] = unsigned(x - lh) < nh ? T(1) : (unsigned(x - lc) < nc ? T(0) : o[h][k]);
+                const int x = xb + h * CS + k;
+                const bool hot = (x - a.hx) * (x - a.hx) < Dh;
+                const bool cold = (x - a.cx) * (x - a.cx) < Dc;
+                o[h][k] = hot ? T(1) : (cold ? T(0) : o[h][k]);
               }
-#else
-#pragma unroll
-            for (int h = 0; h < H; ++h)
-#pragma unroll
-              for (int k = 0; k < V; ++k) o[h][k] = sph_fix(rs, x0 + h * CS + k, o[h][k]);
-#endif
           }
         };
         // S of the wave's row (both chunks), x-neighbours by lane rotates; at the row / column ends lane 0 and lane
-        // 63 take the periodic wrap (whole rows) or e, their own end's cell beyond the column (XH). Exact /6 (div6v)
+        // 63 take the periodic wrap (whole rows) or ev, their end's cell beyond the column (XH). Exact /6 (div6v)
         auto row_update = [&](const NV(&cm)[H], const NV(&up)[H], const NV(&dn)[H], const NV(&zp)[H], const NV(&zm)[H],
                               T ev, NV(&o)[H]) {
           static_assert(H == 2, "two chunks per lane");
@@ -279,49 +298,49 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
           constexpr int dz = DOWN ? -1 : 1;
           const int z0 = DOWN ? ze - 1 : zs;
           NV C[NC][H];
-          E4 E[NC];                  // XH: the column-end cells of the src window planes
           NV U1a[H], U1b[H], U1c[H]; // u1 at planes z+2dz (new), z, z+dz
           NV U2a[H], U2b[H], U2c[H]; // u2 at planes z+dz (new), z-dz, z
-          P2 U1Ea, U1Eb, U1Ec;       // XH: u1 at (e[1], e[2]) of the end, planes as U1
-          T U2Ea, U2Eb, U2Ec;        // XH: u2 at the end's adjacent cell, planes as U2
-          // buffer loads: the plane offset in an SGPR (soffset), the row offset a per-segment constant VGPR. With
-          // 64-bit VGPR addresses recomputed every step, the address write landed on registers of the slot's
-          // previous load and the compiler waited for every outstanding memory op (s_waitcnt vmcnt(0)) before each
-          // step's loads, the previous step's stores included
+          E4 E[NC];                  // edge waves: the column-end cells of the src window planes
+          P2 U1Ea, U1Eb, U1Ec;       // edge waves: u1 at (e[1], e[2]), planes as U1
+          // buffer loads: the plane in the resource (SGPRs), the row offset a per-segment constant VGPR. With 64-bit
+          // VGPR addresses recomputed every step, the address write landed on registers of the slot's previous load
+          // and the compiler waited for every outstanding memory op (s_waitcnt vmcnt(0)) before each step's loads,
+          // the previous step's stores included
           auto load_row = [&](int zz, int k) {
-            const uint32_t po = uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
+            // a raw buffer over the plane (its base in SGPRs: fields beyond 4 GiB, fp64 1024^3), the row offset a
+            // per-segment constant VGPR
+            // (whole rows: one resource over the field, the plane offset in soffset - fields below 4 GiB)
+            const uint32_t po = XH ? 0u : uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<T *>(XH ? a.src + int64_t(zcl(zz)) * a.pxy : a.src), 0, -1, 0x00020000);
 #pragma unroll
-            for (int h = 0; h < H; ++h)
-              C[k][h] = x3_load16<NV>(srcRsrc, rowoff + uint32_t(h * CS * int(sizeof(T))), po);
-            if constexpr (XH) {
+            for (int h = 0; h < H; ++h) C[k][h] = x3_load16<NV>(rs, rowoff + uint32_t(h * CS * int(sizeof(T))), po);
+            if constexpr (EDGE) {
               if constexpr (sizeof(T) == 4) {
-                E[k] = x3_load16<E4>(srcRsrc, edgeoff, po);
+                E[k] = x3_load16<E4>(rs, edgeoff, 0);
               } else {
-                const NV lo = x3_load16<NV>(srcRsrc, edgeoff, po), hi = x3_load16<NV>(srcRsrc, edgeoff + 16, po);
+                const NV lo = x3_load16<NV>(rs, edgeoff, 0), hi = x3_load16<NV>(rs, edgeoff + 16, 0);
                 E[k] = E4{lo[0], lo[1], hi[0], hi[1]};
               }
             }
           };
-          auto publish_src = [&](int bi, int k) {
-#pragma unroll
-            for (int h = 0; h < H; ++h) cs[bi][w][h][lane] = C[k][h];
-            if constexpr (XH)
-              if (edgeLane) ce[bi][w][side] = P2{E[k][1], E[k][2]};
-          };
-          // the end's cell adjacent to the column: x-1 (left, e[2] / the pair's [1]) or x+CW (right, e[1] / [0])
-          auto adj = [&](const P2 &p) -> T { return isR ? p[0] : p[1]; };
+          // the end's cell adjacent to the column in a pair of end cells: x-1 ([1]) or x+CW ([0])
+          auto adj = [&](const P2 &p) -> T { return eside ? p[0] : p[1]; };
           // step t = -4 starts with src planes z+dz .. z+3dz, z = z0 - 4dz, and the src row of its u1 plane
           // (z+2dz: slot 1) published
           {
             const int zw = z0 - 3 * dz;
 #pragma unroll
             for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, k);
-            publish_src(0, 1);
 #pragma unroll
-            for (int h = 0; h < H; ++h)
+            for (int h = 0; h < H; ++h) {
+              cs[0][w][h][lane] = C[1][h];
               U1a[h] = U1b[h] = U1c[h] = U2a[h] = U2b[h] = U2c[h] = C[1][h]; // overwritten before any use
-            U1Ea = U1Eb = U1Ec = P2{T(0), T(0)};
-            U2Ea = U2Eb = U2Ec = T(0);
+            }
+            if constexpr (EDGE) {
+              if (lane < NW) es[0][er][eside] = eside ? E[1][1] : E[1][2];
+              U1Ea = U1Eb = U1Ec = P2{T(0), T(0)};
+            }
             __syncthreads();
           }
           int buf = 0;
@@ -346,28 +365,13 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
                 A[h] = cs[buf][wA][h][lane];
                 B[h] = cs[buf][wB][h][lane];
               }
-              const RowSph rs = row_sph(z + 2 * dz);
-              row_update(C[s1], A, B, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0],
-                         XH ? (isR ? E[s1][1] : E[s1][2]) : T(0), U1a);
-              sphere_row(rs, U1a);
-              if constexpr (XH && R >= 2) {
-                // u1 at the end's cells (e[1], e[2]): x-neighbours in the lane's own load, y from LDS, z from the
-                // window's other planes
-                const P2 ya = ce[buf][wA][side], yb = ce[buf][wB][side];
-                const E4 &ec = E[s1], &ep = DOWN ? E[s0] : E[s2], &em = DOWN ? E[s2] : E[s0];
-                U1Ea = div6v<T, P2, 2>(sum6v<T, KIND>(P2{ec[2], ec[3]}, P2{ec[0], ec[1]}, yb, ya, P2{ep[1], ep[2]},
-                                                       P2{em[1], em[2]}));
-                if (KIND == 0 && rs.hit) {
-                  const int x1 = isR ? xcol + CW : xcol - 2;
-                  U1Ea[0] = sph_fix(rs, x1, U1Ea[0]);
-                  U1Ea[1] = sph_fix(rs, x1 + 1, U1Ea[1]);
-                }
-                if (edgeLane) ue[nbuf][w][side] = adj(U1Ea);
-              }
-              publish_src(nbuf, s2);
-              if constexpr (R >= 1)
+              row_update(C[s1], A, B, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], XH ? es[buf][w][side] : T(0), U1a);
+              sphere_row(row_sph(z + 2 * dz), U1a);
 #pragma unroll
-                for (int h = 0; h < H; ++h) us[nbuf][w][h][lane] = U1a[h];
+              for (int h = 0; h < H; ++h) {
+                cs[nbuf][w][h][lane] = C[s2][h];
+                us[nbuf][w][h][lane] = U1a[h];
+              }
             }
             if constexpr (LV >= 2) {
               NV A[H], B[H];
@@ -376,25 +380,10 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
                 A[h] = us[buf][wA][h][lane];
                 B[h] = us[buf][wB][h][lane];
               }
-              const RowSph rs = row_sph(z + dz);
-              row_update(U1c, A, B, DOWN ? U1b : U1a, DOWN ? U1a : U1b, XH ? adj(U1Ec) : T(0), U2a);
-              sphere_row(rs, U2a);
-              if constexpr (XH && R == 3) {
-                // u2 at the end's adjacent cell: x-neighbours the end's far u1 cell and the row's own first / last
-                // u1 cell, y from LDS, z the adjacent u1 cells of the planes before / after
-                const T far = isR ? U1Ec[1] : U1Ec[0];
-                const T inner = isR ? U1c[H - 1][V - 1] : U1c[0][0];
-                const T vmx = isR ? inner : far, vpx = isR ? far : inner;
-                const T ya = ue[buf][wA][side], yb = ue[buf][wB][side];
-                const T za = adj(U1Ea), zb = adj(U1Eb);
-                // (a pair: sum6v / div6v map an all -0 sum to +0 exactly as the single step's 0-started sum does)
-                U2Ea = div6v<T, P2, 2>(sum6v<T, KIND>(P2{vpx, vpx}, P2{vmx, vmx}, P2{yb, yb}, P2{ya, ya},
-                                                       DOWN ? P2{zb, zb} : P2{za, za}, DOWN ? P2{za, za} : P2{zb, zb}))[0];
-                if (KIND == 0 && rs.hit) U2Ea = sph_fix(rs, isR ? xcol + CW : xcol - 1, U2Ea);
-              }
-              if constexpr (R >= 2)
+              row_update(U1c, A, B, DOWN ? U1b : U1a, DOWN ? U1a : U1b, XH ? eu[buf][w][side] : T(0), U2a);
+              sphere_row(row_sph(z + dz), U2a);
 #pragma unroll
-                for (int h = 0; h < H; ++h) vs[nbuf][w][h][lane] = U2a[h];
+              for (int h = 0; h < H; ++h) vs[nbuf][w][h][lane] = U2a[h];
             }
             if constexpr (LV >= 3) {
               NV A[H], B[H];
@@ -403,7 +392,7 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
                 A[h] = vs[buf][wA][h][lane];
                 B[h] = vs[buf][wB][h][lane];
               }
-              row_update(U2c, A, B, DOWN ? U2b : U2a, DOWN ? U2a : U2b, XH ? U2Ec : T(0), o);
+              row_update(U2c, A, B, DOWN ? U2b : U2a, DOWN ? U2a : U2b, XH ? ev[buf][w][side] : T(0), o);
               sphere_row(row_sph(z), o);
               // unconditional: a row past the region's y end (the last row group) stores into a per-device sink, so
               // every path has the same vector-memory ops and the next step's load wait counts past these stores
@@ -418,7 +407,46 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
                   *q = o[h];
               }
             }
-            if constexpr (LV < 1) publish_src(nbuf, s2);
+            if constexpr (LV < 1)
+#pragma unroll
+              for (int h = 0; h < H; ++h) cs[nbuf][w][h][lane] = C[s2][h];
+            if constexpr (EDGE) {
+              // u1 at the end cells (e[1], e[2]) of plane z+2dz for every row: x-neighbours in the lane's own load, y
+              // the neighbour rows' lanes (row shifts), z the window's other planes
+              const E4 &ec = E[s1], &ep = DOWN ? E[s0] : E[s2], &em = DOWN ? E[s2] : E[s0];
+              const P2 yb = {x3_row_next(ec[1]), x3_row_next(ec[2])}, ya = {x3_row_prev(ec[1]), x3_row_prev(ec[2])};
+              U1Ea = div6v<T, P2, 2>(sum6v<T, KIND>(P2{ec[2], ec[3]}, P2{ec[0], ec[1]}, yb, ya, P2{ep[1], ep[2]},
+                                                     P2{em[1], em[2]}));
+              // u2 at the adjacent cell of plane z+dz: x-neighbours the far u1 end cell and the row's own first / last
+              // u1 cell (published by its wave last step), y the neighbour rows' lanes, z the adjacent u1 cells of the
+              // planes before / after
+              const T far = eside ? U1Ec[1] : U1Ec[0];
+              const T inner = eside ? us[buf][er][H - 1][63][V - 1] : us[buf][er][0][0][0];
+              const T vmx = eside ? inner : far, vpx = eside ? far : inner;
+              const T ca = adj(U1Ec);
+              const T ya2 = x3_row_prev(ca), yb2 = x3_row_next(ca);
+              const T za = adj(U1Ea), zb = adj(U1Eb);
+              // (a pair: sum6v / div6v map an all -0 sum to +0 exactly as the single step's 0-started sum does)
+              T U2E = div6v<T, P2, 2>(sum6v<T, KIND>(P2{vpx, vpx}, P2{vmx, vmx}, P2{yb2, yb2}, P2{ya2, ya2},
+                                                      DOWN ? P2{zb, zb} : P2{za, za}, DOWN ? P2{za, za} : P2{zb, zb}))[0];
+              if (KIND == 0 && a.r1sq > 0) {
+                // spheres at the lane's row (per lane), tested only when some row of the block reaches one
+                const int P1 = z + 2 * dz, P2p = z + dz;
+                const int dh1 = eyh + (P1 - a.hz) * (P1 - a.hz), dc1 = eyc + (P1 - a.cz) * (P1 - a.cz);
+                const int dh2 = eyh + (P2p - a.hz) * (P2p - a.hz), dc2 = eyc + (P2p - a.cz) * (P2p - a.cz);
+                if (__builtin_amdgcn_ballot_w64(min(min(dh1, dc1), min(dh2, dc2)) < a.r1sq) != 0) {
+                  const int x1 = eside ? xcol + CW : xcol - 2;
+                  U1Ea[0] = sph_fix(dh1, dc1, x1, U1Ea[0]);
+                  U1Ea[1] = sph_fix(dh1, dc1, x1 + 1, U1Ea[1]);
+                  U2E = sph_fix(dh2, dc2, eside ? xcol + CW : xcol - 1, U2E);
+                }
+              }
+              if (lane < NW) {
+                es[nbuf][er][eside] = eside ? E[s2][1] : E[s2][2];
+                eu[nbuf][er][eside] = adj(U1Ea);
+                ev[nbuf][er][eside] = U2E;
+              }
+            }
             // boundary-plane publication (block-uniform, as the pairs): every wave's stores of output plane z
             // complete before the barrier, then one thread writes the L2 back (release) and counts the block's cells
             const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
@@ -438,10 +466,10 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
               U2b[h] = U2c[h];
               U2c[h] = U2a[h];
             }
-            U1Eb = U1Ec;
-            U1Ec = U1Ea;
-            U2Eb = U2Ec;
-            U2Ec = U2Ea;
+            if constexpr (EDGE) {
+              U1Eb = U1Ec;
+              U1Ec = U1Ea;
+            }
             ++t;
             return true;
           };
@@ -449,9 +477,9 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
           using I1 = std::integral_constant<int, 1>;
           using I2 = std::integral_constant<int, 2>;
           using I3 = std::integral_constant<int, 3>;
-          using L1 = std::integral_constant<int, (R < 1 ? R : 1)>;
-          using L2 = std::integral_constant<int, (R < 2 ? R : 2)>;
-          using LR = std::integral_constant<int, R>;
+          using L1 = std::integral_constant<int, (RM < 1 ? RM : 1)>;
+          using L2 = std::integral_constant<int, (RM < 2 ? RM : 2)>;
+          using LR = std::integral_constant<int, RM>;
           // warm-up: t = -4, -3 compute u1 only, t = -2, -1 u1 and u2 (one cycle of the slot rotation)
           step(I0{}, L1{});
           step(I1{}, L1{});
@@ -475,6 +503,8 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
     body(std::integral_constant<int, 2>{});
   else if (role == 1)
     body(std::integral_constant<int, 1>{});
+  else if (XH)
+    body(std::integral_constant<int, 4>{});
   else
     body(std::integral_constant<int, 0>{});
   if (a.clk) { // measurement only (StencilTune::blockClock): every wave done, one lane stores the block's interval
@@ -554,7 +584,9 @@ bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   const Rect3 cr = dom.get_compute_region();
   if (!(region.lo == cr.lo && region.hi == cr.hi)) return false; // the kernel sweeps whole sub-domains
   if (n.y < 3 || n.z < 16) return false;
-  if (dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096) return false; // 32-bit buffer-load offsets
+  // 32-bit buffer offsets: within a plane (XH: a resource per plane), within the field (whole rows)
+  if (dom.pitch(qi).x * dom.pitch(qi).y * es >= (int64_t(1) << 31)) return false;
+  if ((wrapm & 1) && dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096) return false;
   (void)x3_sink(dom.gpu(), true);
   const int64_t lox = rad.x(-1);
   return (reinterpret_cast<uintptr_t>(static_cast<const char *>(dom.curr_data(qi)) + lox * es) % 16 == 0) &&
@@ -615,9 +647,30 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
       }
     }
   }
-  if (tune.x2lockstep && ls.parts > 0 && ls.rounds == 1) {
-    a.seg = 2;
+  if (tune.x3sched == 1 && cols > slots && !tune.publish) {
+    // more row groups than resident blocks (fp64 1024^3 as 4 x 171 groups of 256-cell columns): rounds R of P z
+    // parts over cm = ceil(cols / R) groups, every block in step with its y-neighbours in every round; leftover
+    // groups as unsynchronised second segments re-fetch their halo rows (fp64 1024^3: 5.1 ms per triple and
+    // quantity, profiles/r6/j)
+    ls = X2Schedule();
+    double best = 1e30;
+    for (int64_t R = (cols + slots - 1) / slots; R <= 4 * ((cols + slots - 1) / slots); ++R)
+      for (int64_t P = 1; P <= 4; ++P) {
+        const int64_t cm = (cols + R - 1) / R;
+        if (P * cm > slots || nz / P < 16) continue;
+        const double cost = double(R) * (double(nz) / double(P) + 4);
+        if (cost < best - 1e-9) {
+          best = cost;
+          ls.parts = int(P);
+          ls.blocks = P * cm;
+          ls.rounds = int(R);
+        }
+      }
+  }
+  if (tune.x2lockstep && ls.parts > 0) {
+    a.seg = ls.rounds > 1 ? 3 : 2;
     a.zparts = ls.parts;
+    a.zrounds = ls.rounds;
     blocks = uint32_t(ls.blocks);
   }
   ZPartBounds zb{};

@@ -139,6 +139,21 @@ void StencilModel::init() {
       const auto &d = doms0[di];
       for (int64_t q = 0; q < d.num_data(); ++q) w &= stencil7x2_wrappable_axes(d, q, cfg_.tune.x2row);
     }
+    // fused triples where the whole-row kernel cannot wrap x (rows other than 512 fp32 cells: the 1024-wide cbrt
+    // shape, fp64): read x from halos (the XH form) and leave the x self copies in the exchange, one per three steps,
+    // instead of falling back to pairs that wrap x
+    if (cfg_.temporal >= 3 && (w & 1) && doms0[0].backend() == Backend::Device) {
+      StencilTune tw = cfg_.tune, th = cfg_.tune;
+      tw.wrap = w;
+      th.wrap = w & ~1;
+      bool withWrap = true, withHalo = true;
+      for (const auto &d : doms0)
+        for (int64_t q = 0; q < d.num_data(); ++q) {
+          withWrap = withWrap && stencil7x3_supported(d, q, d.get_compute_region(), tw);
+          withHalo = withHalo && stencil7x3_supported(d, q, d.get_compute_region(), th);
+        }
+      if (!withWrap && withHalo) w &= ~1;
+    }
     int wOn = w;
     for (size_t di = 0; di < doms0.size() && !pairInteriors_.empty(); ++di) {
       // the swept regions must span every wrapped axis (a forced full split cuts all of them)

@@ -344,7 +344,7 @@ def _set_field(m, u, quantities=1):
     torch.cuda.synchronize()
 
 
-# x cut by cost (1, 4, 4); (4, 3, 2) keeps x whole (z, then y cut)
+# x cut by cost (1, 4, 4); (100, 3, 2) / (100, 2, 3) keep x whole
 @pytest.mark.parametrize("kind,size,fp64,gpus,cost,scale", [
     ("jacobi", (512, 120, 116), False, [0], None, 1.0), ("jacobi", (1024, 240, 232), False, [0], None, 1.0),
     ("astaroth", (512, 36, 28), False, [0], None, 1.0), ("astaroth", (1536, 13, 17), False, [0], None, 1.0),
@@ -352,7 +352,7 @@ def _set_field(m, u, quantities=1):
     ("jacobi", (256, 64, 64), True, [0], None, 1.0), ("astaroth", (512, 20, 24), True, [0], None, 1.0),
     ("astaroth", (256, 12, 16), True, [0], None, 1e-300),
     ("jacobi", (1024, 240, 232), False, [0, 0], (1, 4, 4), 1.0), ("astaroth", (2048, 30, 20), False, [0, 0, 0, 0], (1, 4, 4), 1.0),
-    ("astaroth", (512, 40, 64), False, [0, 0, 0, 0], (4, 3, 2), 1.0), ("jacobi", (512, 240, 232), False, [0, 0], (4, 2, 3), 1.0),
+    ("astaroth", (512, 40, 64), False, [0, 0, 0, 0], (100, 3, 2), 1.0), ("jacobi", (512, 240, 232), False, [0, 0], (100, 2, 3), 1.0),
     ("astaroth", (512, 24, 40), True, [0, 0], (1, 4, 4), 1.0)])
 def test_temporal3_x_halos(st, kind, size, fp64, gpus, cost, scale):
     """Fused triples reading x from 3-deep halos (stencil7x3 XH form: 512-cell fp32 / 256-cell fp64 columns, the 3
@@ -383,6 +383,50 @@ def test_temporal3_x_halos(st, kind, size, fp64, gpus, cost, scale):
             got = _gather(m, q).to(u.device)
             bad = int((got != u).sum())
             assert bad == 0, f"run({n}) q{q}: {bad} cells differ, max {(got - u).abs().max().item()}"
+
+
+@pytest.mark.parametrize("kind,size,fp64", [("astaroth", (1024, 36, 28), False), ("jacobi", (1024, 240, 232), False),
+                                            ("astaroth", (512, 20, 24), True), ("jacobi", (512, 120, 116), True)])
+def test_temporal3_x_halos_where_x_cannot_wrap(st, kind, size, fp64):
+    """One GPU, wrap_self=True, rows the whole-row triple cannot wrap (1024 fp32 cells, fp64): the model keeps fused
+    triples by reading x from halos (the x self copies stay in the depth-3 exchange) and wraps only y and z; bitwise
+    equal to single steps of the torch oracle."""
+    from stencil2_amd.ops import astaroth_step_reference
+    cls, ref, kw = ((st.Jacobi3D, jacobi_step_reference, {}) if kind == "jacobi"
+                    else (st.AstarothSim, astaroth_step_reference, {"quantities": 1}))
+    m = cls(size, gpus=[0], temporal=3, fp64=fp64, **kw)
+    m.init()
+    assert m.temporal_triples() and m.wrap_axes() == 6, f"triples {m.temporal_triples()} wrap {m.wrap_axes()}"
+    dt = torch.float64 if fp64 else torch.float32
+    u = torch.rand((size[2], size[1], size[0]), device="cuda", dtype=dt, generator=torch.Generator(device="cuda").manual_seed(9))
+    _set_field(m, u)
+    for n in (3, 20, 4):
+        m.run(n)
+        for _ in range(n):
+            u = ref(u)
+        m.synchronize()
+        got = _gather(m).to(u.device)
+        assert torch.equal(got, u), f"run({n}): {int((got != u).sum())} cells differ"
+
+
+def test_temporal3_field_beyond_4gib(st):
+    """A 1024 x 1024 x 1040 fp32 field (4.4 GB per buffer): the triple's buffer loads address one plane at a time
+    (resource base per plane), so fields past 4 GiB (config 5: 1024^3 fp64, 8.6 GB per quantity) keep the triples"""
+    from stencil2_amd.ops import astaroth_step_reference
+    size = (1024, 1024, 1040)
+    m = st.AstarothSim(size, quantities=1, gpus=[0], temporal=3)
+    m.init()
+    assert m.temporal_triples() and m.domain.domain(0).buffer_bytes(0) > (1 << 32)
+    u = torch.rand((size[2], size[1], size[0]), device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+    _set_field(m, u)
+    m.run(3)
+    m.run(1)
+    m.synchronize()
+    for _ in range(4):
+        u = astaroth_step_reference(u)
+    got = m.interior(0)
+    assert torch.equal(got, u), f"{int((got != u).sum())} cells differ"
+    del m
 
 
 # cuts follow the interface cost (NodePartition): 4*Y*Z for an x cut against 2*X*Z (y, cost 4,2,3) / 2*X*Y (z, 4,3,2)
