@@ -147,6 +147,7 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
     zz -= zz >= zwhi ? zwn : 0;
     return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
   };
+  const __amdgpu_buffer_rsrc_t srcRsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(a.src), 0, -1, 0x00020000);
   auto ywrap = [&](int yy) {
     yy = yy < a.wlo[1] ? yy + a.wn[1] : (yy >= a.wlo[1] + a.wn[1] ? yy - a.wn[1] : yy);
     return yy < 0 ? 0 : (yy > a.rawYm1 ? a.rawYm1 : yy);
@@ -311,8 +312,10 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
             // per-segment constant VGPR
             // (whole rows: one resource over the field, the plane offset in soffset - fields below 4 GiB)
             const uint32_t po = XH ? 0u : uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<T *>(XH ? a.src + int64_t(zcl(zz)) * a.pxy : a.src), 0, -1, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs =
+                XH ? __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(a.src + int64_t(zcl(zz)) * a.pxy), 0, -1,
+                                                       0x00020000)
+                   : srcRsrc;
 #pragma unroll
             for (int h = 0; h < H; ++h) C[k][h] = x3_load16<NV>(rs, rowoff + uint32_t(h * CS * int(sizeof(T))), po);
             if constexpr (EDGE) {

@@ -34,7 +34,7 @@ def main():
     ev = [("K " + n.split("(")[0][-40:], s, e, st) for n, s, e, st in ks] + \
          [(f"C {n[12:]} {sz}", s, e, st) for n, s, e, st, sz in cs]
     ev.sort(key=lambda x: x[1])
-    tail = ev[-a.tail:]
+    tail = ev[-a.tail:] if a.tail > 0 else []
     if tail:
         t0 = tail[0][1]
         print(f"\nlast {len(tail)} events (us from the first shown)")

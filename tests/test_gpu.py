@@ -994,6 +994,21 @@ def test_triples_across_ranks(kind, size, cost, ranks, mode):
         assert "jacobi bad 0" in out, out[-2000:]
 
 
+@pytest.mark.parametrize("kind,size,ranks", [("astaroth", "1024,36,40", 2), ("jacobi", "1024,240,232", 2),
+                                             ("astaroth", "2048,24,20", 4)])
+def test_x_halo_triples_across_ranks(kind, size, ranks):
+    """x cut between ranks sharing one GPU over HIP IPC (cost 1,4,4): the fused triples read x from the 3-deep halos
+    another rank sends (XH columns, faces / edges / corners through one depth-3 exchange per three steps), y / z
+    wrapped in-kernel. Bitwise vs the oracle through single steps and triples."""
+    outs = run_ranks(ranks, WORKER, ["jacobi", size],
+                     env_extra={"MP_DEVICE": "1", "MP_METHODS": "All", "STENCIL_WAIT_TIMEOUT": "20",
+                                "MP_TEMPORAL": "3", "MP_KIND": kind, "MP_RANDOM": "1", "MP_AXIS_COST": "1,4,4",
+                                "MP_RUN_STEPS": "9", "MP_EXPECT_TRIPLES": "1", "MP_EXPECT_WRAP": "6"})
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        assert "jacobi bad 0" in out, out[-2000:]
+
+
 @pytest.mark.parametrize("size,cost", [("512,264,16", "4,2,3"), ("1024,520,12", "4,2,3"), ("645,520,12", "4,2,3"),
                                        ("512,16,300", "4,3,2"), ("645,12,520", "4,3,2")])  # y cut / z cut
 def test_colocated_ipc_wide_rows_two_ranks(size, cost):
