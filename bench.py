@@ -455,8 +455,8 @@ def make_tune(st, args):
 
 
 def tune_record(tune) -> dict:
-    return {k: getattr(tune, k) for k in ("x3sched", "x3parts", "x3sphw", "x2sphw", "x2early", "x2row", "x2pf",
-                                          "x2nw", "nontemporal", "alternate_z", "xcd_remap", "variant")}
+    return {k: getattr(tune, k) for k in ("x3sched", "x3parts", "x3sphw", "x2sphw", "x2early", "x2row",
+                                          "nontemporal", "alternate_z", "xcd_remap", "variant")}
 
 
 def make_transport(st, args, inbox=None):

@@ -343,24 +343,20 @@ int main(int argc, char **argv) {
     jacobi_init(l2, 0, l2.get_full_region(), s);
     fill_value(l2, 0, 0.5, false, s);
     s.sync();
-    for (int nw : {12, 16})
-      for (int pf : {1, 2, 3})
-        for (int zc : {-1, 0, 64, 128}) { // -1: fixed auto z-chunks (x2sched 0); 0: balanced segments
-          const int nt = 1, alt = 1;
-          StencilTune t;
-          t.nontemporal = nt;
-          t.alternateZ = alt;
-          t.zchunk = zc < 0 ? 0 : zc;
-          t.x2sched = zc < 0 ? 0 : 1;
-          t.x2nw = nw;
-          t.x2pf = pf;
-          const double us = timeit([&] {
-            stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t);
-            l2.swap();
-          }) / 2;
-          std::printf("x2pp_nt%d_alt%d,%d,1,%d,%.2f,%.1f,%.3f,nw%d\n", nt, alt, t.x2pf, zc, us, cells / us / 1e3,
-                      cells * 8 / us / 1e6, t.x2nw);
-        }
+    for (int zc : {-1, 0, 64, 128}) { // -1: fixed auto z-chunks (x2sched 0); 0: balanced segments
+      const int nt = 1, alt = 1;
+      StencilTune t;
+      t.nontemporal = nt;
+      t.alternateZ = alt;
+      t.zchunk = zc < 0 ? 0 : zc;
+      t.x2sched = zc < 0 ? 0 : 1;
+      const double us = timeit([&] {
+        stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t);
+        l2.swap();
+      }) / 2;
+      std::printf("x2pp_nt%d_alt%d,1,1,%d,%.2f,%.1f,%.3f,nw12\n", nt, alt, zc, us, cells / us / 1e3,
+                  cells * 8 / us / 1e6);
+    }
   }
   for (int rep = 0; rep < reps; ++rep)
   if (only.empty() || only == "x2") {
@@ -372,17 +368,12 @@ int main(int argc, char **argv) {
     const Rect3 reg2 = l2.get_compute_region();
     jacobi_init(l2, 0, l2.get_full_region(), s);
     s.sync();
-    for (int nw : {12, 16})
-      for (int pf : {1, 2, 3})
-        for (int zc : {0, 43, 64, 128}) {
-          StencilTune t;
-          t.x2nw = nw;
-          t.x2pf = pf;
-          t.zchunk = zc;
-          const double us = timeit([&] { stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t); }) / 2;
-          std::printf("stencil7x2,%d,%d,%d,%.2f,%.1f,%.3f,nw%d\n", pf, 1, zc, us, cells / us / 1e3, cells * 8 / us / 1e6,
-                      nw);
-        }
+    for (int zc : {0, 43, 64, 128}) {
+      StencilTune t;
+      t.zchunk = zc;
+      const double us = timeit([&] { stencil7x2_apply(l2, 0, reg2, StencilKind::Jacobi, sph, s, t); }) / 2;
+      std::printf("stencil7x2,1,1,%d,%.2f,%.1f,%.3f,nw12\n", zc, us, cells / us / 1e3, cells * 8 / us / 1e6);
+    }
   }
   for (int rep = 0; rep < reps; ++rep)
   for (const Cfg &c : cfgs) {

@@ -46,10 +46,6 @@ struct StencilTune {
   int ty = 2;     // rows per lane (variant 0: 2/4/8, variant 1: 4/8)
   int zchunk = 0; // planes per block (0 = auto: exactly one round of resident blocks)
   int nw = 8;     // waves per block stacked in y (deep-lookahead variants: 4/8/16)
-  // fused-pair kernel (stencil7x2): waves per block (8/12/16, one src row each, NW-4 output rows) and planes of
-  // z lookahead (1/2/3). 12 waves get 3 waves/SIMD and up to 168 VGPRs (no spills at any lookahead, fp32 or fp64);
-  // one MI355X, 512^3, bench.py: 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s
-  int x2nw = 12, x2pf = 1; // one plane of lookahead: best for the whole-row kernel once its edge waves skip u1/u2
   int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
   float x3sphw = 0.3f;    // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z

@@ -732,7 +732,6 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("nontemporal", &StencilTune::nontemporal)
       .def_readwrite("alternate_z", &StencilTune::alternateZ)
       .def_readwrite("nw", &StencilTune::nw)
-      .def_readwrite("x2pf", &StencilTune::x2pf)
       .def_readwrite("x3sched", &StencilTune::x3sched)
       .def_readwrite("x2early", &StencilTune::x2early)
       .def_readwrite("x3parts", &StencilTune::x3parts)
@@ -741,7 +740,6 @@ PYBIND11_MODULE(_C, m) {
       .def_property(
           "block_clock", [](const StencilTune &t) { return reinterpret_cast<uintptr_t>(t.blockClock); },
           [](StencilTune &t, uintptr_t p) { t.blockClock = reinterpret_cast<uint64_t *>(p); })
-      .def_readwrite("x2nw", &StencilTune::x2nw)
       .def_readwrite("x2row", &StencilTune::x2row)
       .def_readwrite("x2sched", &StencilTune::x2sched)
       .def_readwrite("x2reserve", &StencilTune::x2reserve)

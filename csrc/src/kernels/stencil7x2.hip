@@ -1387,16 +1387,9 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   const bool f32 = dom.elem_size(qi) == 4;
   const bool jac = kind == StencilKind::Jacobi;
   if (f32 && tune.x2row) { // whole rows of 512 cells in one wave (x wrapped in-kernel)
-    const int pf = tune.x2pf <= 1 ? 1 : (tune.x2pf == 2 ? 2 : 3);
-    bool done;
-    if (jac)
-      done = pf == 1 ? apply_x2row_t<0, 1>(dom, qi, region, sph, stream, tune)
-                     : (pf == 2 ? apply_x2row_t<0, 2>(dom, qi, region, sph, stream, tune)
-                                : apply_x2row_t<0, 3>(dom, qi, region, sph, stream, tune));
-    else
-      done = pf == 1 ? apply_x2row_t<1, 1>(dom, qi, region, sph, stream, tune)
-                     : (pf == 2 ? apply_x2row_t<1, 2>(dom, qi, region, sph, stream, tune)
-                                : apply_x2row_t<1, 3>(dom, qi, region, sph, stream, tune));
+    // one plane of lookahead (1-3 measured within noise once the edge waves skip u1 / u2, r2s3; 2 / 3 removed in r6)
+    bool done = jac ? apply_x2row_t<0, 1>(dom, qi, region, sph, stream, tune)
+                    : apply_x2row_t<1, 1>(dom, qi, region, sph, stream, tune);
     if (done) return;
     const Rect3 rr(region.lo - dom.accessor_origin(), region.hi - dom.accessor_origin());
     const int64_t nx = rr.hi.x - rr.lo.x;
@@ -1443,36 +1436,15 @@ void stencil7x2_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, S
   // the column kernels wrap x only for whole chunks (ragged periodic rows are the whole-row kernel's)
   STENCIL_REQUIRE(!(tune.wrap & 1) || (stencil7x2_wrappable_axes(dom, qi, 0) & 1),
                   "in-kernel x wrap of a ragged row needs the whole-row kernel (fp32, x2row, 256 < nx < 1024)");
-  // shapes (rows per lane, waves per block, min waves/SIMD): 1x8 keeps everything in registers at 6 waves/SIMD;
-  // 2x4 at 3 waves/SIMD; 2x8 at 4 (spills)
-  // shape = waves per block (one src row each; NW-4 output rows) x planes of z lookahead
-  const int shape = (tune.x2nw == 8 ? 0 : (tune.x2nw == 12 ? 3 : 6)) + (tune.x2pf <= 1 ? 0 : (tune.x2pf == 2 ? 1 : 2));
-#define X2_LAUNCH(TT, K)                                                                                           \
-  do {                                                                                                             \
-    switch (shape) {                                                                                               \
-    case 0: apply_x2_t<TT, K, 8, 1>(dom, qi, region, sph, stream, tune); break;                                    \
-    case 1: apply_x2_t<TT, K, 8, 2>(dom, qi, region, sph, stream, tune); break;                                    \
-    case 2: apply_x2_t<TT, K, 8, 3>(dom, qi, region, sph, stream, tune); break;                                    \
-    case 3: apply_x2_t<TT, K, 12, 1>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 4: apply_x2_t<TT, K, 12, 2>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 5: apply_x2_t<TT, K, 12, 3>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 6: apply_x2_t<TT, K, 16, 1>(dom, qi, region, sph, stream, tune); break;                                   \
-    case 7: apply_x2_t<TT, K, 16, 2>(dom, qi, region, sph, stream, tune); break;                                   \
-    default: apply_x2_t<TT, K, 16, 3>(dom, qi, region, sph, stream, tune); break;                                  \
-    }                                                                                                              \
-  } while (0)
-  if (f32) {
-    if (jac)
-      X2_LAUNCH(float, 0);
-    else
-      X2_LAUNCH(float, 1);
-  } else {
-    if (jac)
-      X2_LAUNCH(double, 0);
-    else
-      X2_LAUNCH(double, 1);
-  }
-#undef X2_LAUNCH
+  // one-chunk column kernel: 12 waves (one src row each, 8 output rows) and one plane of z lookahead, the measured best
+  // (bench.py 12x3 883-888, 12x1 881-883, 16x2 797-804, 8x2 759-772 Gcells/s, profiles/r1s4_bench_block_shapes.txt;
+  // the other shapes were removed in r6)
+  if (f32)
+    jac ? apply_x2_t<float, 0, 12, 1>(dom, qi, region, sph, stream, tune)
+        : apply_x2_t<float, 1, 12, 1>(dom, qi, region, sph, stream, tune);
+  else
+    jac ? apply_x2_t<double, 0, 12, 1>(dom, qi, region, sph, stream, tune)
+        : apply_x2_t<double, 1, 12, 1>(dom, qi, region, sph, stream, tune);
 }
 
 template <typename T, int KIND>
