@@ -257,18 +257,35 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
           const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - dc;
           return hot ? T(1) : (cold ? T(0) : v);
         };
+        // the chunks (cells xcol + h CS .. + CS - 1 over the wave) a sphere's x range can reach (block-uniform): the
+        // 512^3 hot sphere (x 119-221) only touches chunk 0, the cold one (290-392) only chunk 1, so a sphere row tests
+        // half the cells (StencilTune.x3sphchunk; 0: every chunk for both spheres)
+        bool hotc[H], coldc[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const int lo = xcol + h * CS, hi = lo + CS - 1;
+          hotc[h] = !a.sphchunk || (a.hx - a.sphr <= hi && a.hx + a.sphr >= lo);
+          coldc[h] = !a.sphchunk || (a.cx - a.sphr <= hi && a.cx + a.sphr >= lo);
+        }
         auto sphere_row = [&](const RowSph &rs, NV(&o)[H]) {
           if (KIND == 0 && rs.hit) {
             const int Dh = a.r1sq - rs.dh, Dc = a.r1sq - rs.dc;
+            // cold first, then hot: the hot sphere wins where both hold, as in the single step
 #pragma unroll
-            for (int h = 0; h < H; ++h)
+            for (int h = 0; h < H; ++h) {
+              if (coldc[h])
 #pragma unroll
-              for (int k = 0; k < V; ++k) {
-                const int x = xb + h * CS + k;
-                const bool hot = (x - a.hx) * (x - a.hx) < Dh;
-                const bool cold = (x - a.cx) * (x - a.cx) < Dc;
-                o[h][k] = hot ? T(1) : (cold ? T(0) : o[h][k]);
-              }
+                for (int k = 0; k < V; ++k) {
+                  const int x = xb + h * CS + k;
+                  o[h][k] = (x - a.cx) * (x - a.cx) < Dc ? T(0) : o[h][k];
+                }
+              if (hotc[h])
+#pragma unroll
+                for (int k = 0; k < V; ++k) {
+                  const int x = xb + h * CS + k;
+                  o[h][k] = (x - a.hx) * (x - a.hx) < Dh ? T(1) : o[h][k];
+                }
+            }
           }
         };
         // S of the wave's row (both chunks), x-neighbours by lane rotates; at the row / column ends lane 0 and lane
@@ -610,6 +627,8 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   if (!(a.wrapm & 4)) a.wn[2] = 0;
   a.x0 = a.lox;
   a.remap = tune.xcdRemap ? 1 : 0;
+  a.sphchunk = tune.x3sphchunk ? 1 : 0;
+  a.sphr = int(sph.radius);
   const int nx = a.hix - a.lox, ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = XH ? int(nx / x3_column_cells(int64_t(sizeof(T)))) : 1;
   a.gy = (ny + YO - 1) / YO;

@@ -60,6 +60,8 @@ template <typename T> struct StencilArgs {
   // spheres, raw coordinates
   int hx, hy, hz, cx, cy, cz;
   int r1sq; // (radius+1)^2, 0 = disabled
+  int sphr;  // the sphere radius (stencil7x3: which chunks a sphere can reach)
+  int sphchunk; // stencil7x3: test each sphere only on the chunks it can reach
   // halo forwarding (FWD kernels): cells within fwm[a] of the low face send along -a, within fwp[a] of the high
   // face along +a; the receiving halo cell of direction k = (dx+1) + 3(dy+1) + 9(dz+1) is at (own output address +
   // fd[k]) for every k set in fmask (receivers with our pitches; the rest is copied after the kernel)
