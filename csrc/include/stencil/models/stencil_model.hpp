@@ -127,7 +127,8 @@ public:
   bool local_interior_steps() const { return localSteps_; } // overlapped single steps on get_local_interior
   bool forwarding() const { return forward_; }
   bool temporal_blocking() const { return pairs_; }
-  // three steps per sweep (stencil7x3_row_kernel): temporal >= 3, one device, every axis wrapped in-kernel
+  // three steps per sweep (stencil7x3): temporal >= 3, device sub-domains of 512-cell fp32 rows wrapped in-kernel or of
+  // 512-cell fp32 / 256-cell fp64 columns with x halos
   bool temporal_triples() const { return triples_; }
   int wrap_axes() const { return pairTune_.wrap; } // axes the fused pairs wrap in-kernel (mask 1=x 2=y 4=z)
   int step_wrap_axes() const { return stepTune_.wrap; } // same for single steps (stencil7_apply)

@@ -1,14 +1,16 @@
 // Three fused 7-point steps per sweep (deeper temporal blocking): dst = S(S(S(src))) on a whole sub-domain, for
-// gfx950. Two forms of one kernel:
-//   * whole periodic rows (x wrapped in-kernel, fp32 rows of exactly 512 cells): the x-neighbours and the wrap are DPP
-//     lane rotates of the wave's own registers, nothing is read beyond the row;
-//   * columns with x halos (XH: fp32 x a multiple of 512, fp64 of 256): the same two-chunk lane layout per column of
-//     CW cells, and only the 3 cells beyond each column end come from outside the wave - one 16-B load per lane half
-//     (cells x-3 .. x of the left end into lanes 0-31, x+CW-1 .. x+CW+2 of the right end into lanes 32-63; lanes 0
-//     and 63 use them). The intermediate levels are computed on the cells the next level needs there: u1 at x-2, x-1
-//     and x+CW, x+CW+1, u2 at x-1 and x+CW, with the neighbour rows' edge values through LDS. So a sub-domain whose
-//     x faces come from an exchange (the reference's every-iteration exchange on one GPU, x cut across GPUs, fp64)
-//     runs one depth-3 exchange and one read + write of the field per three steps.
+// gfx950. Two kernels share the design below:
+//   * stencil7x3_wrap_kernel - whole periodic rows (x wrapped in-kernel, fp32 rows of exactly 512 cells): the
+//     x-neighbours and the wrap are DPP lane rotates of the wave's own registers, nothing is read beyond the row (the
+//     one-GPU headline);
+//   * stencil7x3_xh_kernel - columns with x halos (fp32 x a multiple of 512, fp64 of 256): the same two-chunk lane
+//     layout per column of CW cells; only the 3 cells beyond each column end come from outside the wave. The two edge
+//     waves (rows 0 and 11, which otherwise only load and publish their source row) carry the column ends of all 12
+//     rows - wave 0 the left end, wave 11 the right, lane r = row r: one 16-B load per row and plane (cells x-3 .. x /
+//     x+CW-1 .. x+CW+2), u1 at the two cells beyond the end, u2 at the adjacent one, y-neighbours by DPP row shifts -
+//     and publish each row's adjacent cell per level through LDS; the output waves read one value per level on lanes
+//     0 / 63. So a sub-domain whose x faces come from an exchange (the reference's every-iteration exchange on one
+//     GPU, x cut across GPUs, fp64) runs one depth-3 exchange and one read + write of the field per three steps.
 //
 // The fused pair (stencil7x2_row_kernel) streams the field once per two steps at ~95 % of a plain copy of its access
 // shape (205 us per 512^3 pair, profiles/r4/j); a triple reads and writes the field once per THREE steps. What it
@@ -111,9 +113,11 @@ __device__ __forceinline__ double x3_row_prev(double v) {
   return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
 }
 
-template <typename T, int KIND, bool XH>
+// Columns with x halos (the XH form): every x-neighbour beyond a column end comes from the exchanged halos
+template <typename T, int KIND>
 __global__ __launch_bounds__(64 * 12, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
-stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
+stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
+  constexpr bool XH = true;
   using NV = typename Vec16<T>::native;
   using P2 = typename Pk<T>::t;
   typedef T E4 __attribute__((ext_vector_type(4)));
@@ -123,7 +127,6 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
   constexpr int CW = H * CS;          // cells per column (the whole row when x wraps in-kernel)
   constexpr int YO = NW - 6;          // output rows per block
   constexpr int NC = 4;               // src planes in registers (one plane of lookahead)
-  static_assert(XH || sizeof(T) == 4, "whole periodic rows: fp32 (512 cells)");
   __shared__ NV cs[2][NW][H][64]; // src rows  (plane z+3dz at publish)
   __shared__ NV us[2][NW][H][64]; // u1 rows   (plane z+2dz at publish)
   __shared__ NV vs[2][NW][H][64]; // u2 rows   (plane z+dz at publish)
@@ -523,8 +526,315 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
     body(std::integral_constant<int, 2>{});
   else if (role == 1)
     body(std::integral_constant<int, 1>{});
-  else if (XH)
+  else
     body(std::integral_constant<int, 4>{});
+  if (a.clk) { // measurement only (StencilTune::blockClock): every wave done, one lane stores the block's interval
+    __syncthreads();
+    if (lane == 0 && w == 0) {
+      a.clk[2 * lb] = clk0;
+      a.clk[2 * lb + 1] = wall_clock64();
+    }
+  }
+}
+
+// Whole periodic rows (fp32, 512 cells, x wrapped in-kernel): x-neighbours and the wrap by DPP lane rotates of the
+// wave's own registers; the headline kernel (bench.py, one GPU). Kept apart from the XH form: sharing one body cost
+// the whole-row instance ~3 % more VALU (window register moves) and 1.2 % of steady-state time (profiles/r6/r6n)
+template <int KIND>
+__global__ __launch_bounds__(64 * 12, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
+stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
+  constexpr int NW = 12;     // 3 waves per SIMD (168 VGPRs), 3 x 48 KiB of LDS
+  using T = float;
+  using NV = nf4;
+  constexpr int V = 4, H = 2;
+  constexpr int CS = 64 * V; // cells between a lane's chunks (chunk h = cells 256 h + 4 lane ..)
+  constexpr int LS = V;      // cells between adjacent lanes
+  constexpr int YO = NW - 6; // output rows per block
+  constexpr int NC = 4;      // src planes in registers (one plane of lookahead)
+  __shared__ NV cs[2][NW][H][64]; // src rows  (plane z+3dz at publish)
+  __shared__ NV us[2][NW][H][64]; // u1 rows   (plane z+2dz at publish)
+  __shared__ NV vs[2][NW][H][64]; // u2 rows   (plane z+dz at publish)
+
+  const uint32_t nb = gridDim.x;
+  const uint32_t lb = a.remap ? xcd_remap(blockIdx.x, nb) : blockIdx.x;
+  const int lane = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.y)); // the wave's block row (wave-uniform: SGPR)
+  const uint32_t nzt = uint32_t(a.hiz - a.loz);
+  const X3Seg sg = x3_segments(a, zbounds, lb, nb, uint32_t(a.gy), uint32_t(a.gy), nzt);
+  const bool lane0 = lane == 0, lane63 = lane == 63;
+  const int wA = w > 0 ? w - 1 : 0, wB = w < NW - 1 ? w + 1 : NW - 1;
+  const int xb = a.lox + lane * LS; // chunk h at xb + h * CS
+  const int zwn = a.wn[2], zwlo = a.wlo[2], zwhi = a.wlo[2] + a.wn[2];
+  // raw buffer over the source field (offsets from raw [0,0,0] are non-negative and below 4 GiB: checked by the host)
+  const __amdgpu_buffer_rsrc_t srcRsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.src), 0, -1, 0x00020000);
+  auto zcl = [&](int zz) {
+    zz += zz < zwlo ? zwn : 0;
+    zz -= zz >= zwhi ? zwn : 0;
+    return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
+  };
+  // The wave's role = the levels its row computes (wave-uniform): 0 on rows 0 / 11 (source rows only), 1 (u1) on 1 /
+  // 10, 2 (u1, u2) on 2 / 9, 3 (u1, u2, u3 = output) on 3..8. The whole march is instantiated per role, and the
+  // warm-up steps (fewer valid levels) are unrolled separately, so the steady-state step has no role or level
+  // branches: per step one tiny-sum test (ballot) and, for Jacobi, one sphere test per level.
+  auto body = [&](auto roleTag) {
+    constexpr int R = decltype(roleTag)::value;
+    bool odd = sg.odd;
+    const bool pubOrder = a.pub != nullptr;
+    for (int pp = 0; pp < 2; ++pp) {
+      // publishing: the leftover row groups' short second segments first (their face planes would otherwise come
+      // out last), the main lockstep segment in its fixed direction
+      const int pass = pubOrder ? 1 - pp : pp;
+      uint32_t s = pass == 0 ? sg.s : sg.s2;
+      const uint32_t e = pass == 0 ? sg.e : sg.e2;
+      while (s < e) { // block-uniform
+        const uint32_t by = s / nzt;
+        const int zo = int(s - by * nzt);
+        const int nzs = int(min(nzt - uint32_t(zo), e - s));
+        s += uint32_t(nzs);
+        const int zs = a.loz + zo;
+        const int ze = zs + nzs;
+        bool down = pass == 0 && sg.odd;
+        if (!pubOrder) {
+          down = odd != (a.flip != 0);
+          odd = !odd;
+        }
+        const int yblk = a.loy + YO * int(by);
+        const int y = yblk - 3 + w;
+        if (yblk >= a.hiy) continue;
+        const bool outRow = R == 3 && y < a.hiy;
+        int yw = y < a.wlo[1] ? y + a.wn[1] : (y >= a.wlo[1] + a.wn[1] ? y - a.wn[1] : y);
+        yw = yw < 0 ? 0 : (yw > a.rawYm1 ? a.rawYm1 : yw);
+        const uint32_t rowoff = uint32_t((yw * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+        const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
+
+        // spheres (Jacobi): the planes P of this row that cross the hot / cold sphere form two intervals
+        // |P - c.z| <= h (h * h < r1sq - dy^2), computed once per segment; per-cell tests only on those planes
+        struct RowSph {
+          int dh, dc;
+          bool hit;
+        };
+        auto isqrt_below = [](int d) -> int { // largest h >= 0 with h * h < d (d > 0), exact
+          int h = int(__builtin_sqrtf(float(d - 1)));
+          while (h > 0 && h * h > d - 1) --h;
+          while ((h + 1) * (h + 1) <= d - 1) ++h;
+          return h;
+        };
+        int hzlo = 1, hzhi = 0, czlo = 1, czhi = 0; // empty intervals
+        if (KIND == 0 && a.r1sq > 0) {
+          const int dyh = a.r1sq - (y - a.hy) * (y - a.hy), dyc = a.r1sq - (y - a.cy) * (y - a.cy);
+          if (dyh > 0) {
+            const int h = isqrt_below(dyh);
+            hzlo = a.hz - h;
+            hzhi = a.hz + h;
+          }
+          if (dyc > 0) {
+            const int h = isqrt_below(dyc);
+            czlo = a.cz - h;
+            czhi = a.cz + h;
+          }
+        }
+        auto row_sph = [&](int P) -> RowSph {
+          RowSph r{0, 0, false};
+          if (KIND == 0) {
+            r.hit = (P >= hzlo && P <= hzhi) || (P >= czlo && P <= czhi);
+            r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
+            r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
+          }
+          return r;
+        };
+        // per-cell tests on the rows that cross a sphere (cheaper variants measured slower: an x interval per row,
+        // tests only on the chunk the sphere reaches; profiles/r5/ai, aj, ap). Those rows make their blocks the
+        // sweep's longest, which the host evens out with sphere-weighted z parts (x3sphw, profiles/r5/ao)
+        auto sphere_row = [&](const RowSph &rs, NV(&o)[H]) {
+          if (KIND == 0 && rs.hit) {
+            // (x - c)^2 + d < r1sq <=> (x - c)^2 < r1sq - d: the row's bound is one scalar per sphere, the per-cell
+            // squared distances loop invariants, so a cell costs a compare and a select per sphere
+            const int Dh = a.r1sq - rs.dh, Dc = a.r1sq - rs.dc;
+#pragma unroll
+            for (int h = 0; h < H; ++h)
+#pragma unroll
+              for (int k = 0; k < V; ++k) {
+                const int x = xb + h * CS + k;
+                const bool hot = (x - a.hx) * (x - a.hx) < Dh;
+                const bool cold = (x - a.cx) * (x - a.cx) < Dc;
+                o[h][k] = hot ? T(1) : (cold ? T(0) : o[h][k]);
+              }
+          }
+        };
+        // S of the wave's row (both chunks), x-neighbours and the periodic x wrap by lane rotates; exact /6 (div6v)
+        auto row_update = [&](const NV(&cm)[H], const NV(&up)[H], const NV(&dn)[H], const NV(&zp)[H], const NV(&zm)[H],
+                              NV(&o)[H]) -> T {
+          static_assert(H == 2, "two chunks per lane");
+          // named scalars, not arrays: a select between two array elements became a dynamically indexed private
+          // array (scratch stores + loads on every row update, 449 vs 304 us per triple)
+          const T r30 = rot_prev(cm[0][V - 1]), r31 = rot_prev(cm[1][V - 1]);
+          const T l00 = rot_next(cm[0][0]), l01 = rot_next(cm[1][0]);
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            const T left = h == 0 ? (lane0 ? r31 : r30) : (lane0 ? r30 : r31);
+            const T right = h == 0 ? (lane63 ? l01 : l00) : (lane63 ? l00 : l01);
+            NV vpx, vmx;
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+              vpx[k] = k < V - 1 ? cm[h][k + 1] : right;
+              vmx[k] = k > 0 ? cm[h][k - 1] : left;
+            }
+            o[h] = div6v<T, NV, V>(sum6v<T, KIND>(vpx, vmx, dn[h], up[h], zp[h], zm[h]));
+          }
+          return T(1);
+        };
+
+        auto march = [&](auto downTag) {
+          constexpr bool DOWN = decltype(downTag)::value;
+          constexpr int dz = DOWN ? -1 : 1;
+          const int z0 = DOWN ? ze - 1 : zs;
+          NV C[NC][H];
+          NV U1a[H], U1b[H], U1c[H]; // u1 at planes z+2dz (new), z, z+dz
+          NV U2a[H], U2b[H], U2c[H]; // u2 at planes z+dz (new), z-dz, z
+          // buffer loads: the plane offset in an SGPR (soffset), the row offset a per-segment constant VGPR. With
+          // 64-bit VGPR addresses recomputed every step, the address write landed on registers of the slot's
+          // previous load and the compiler waited for every outstanding memory op (s_waitcnt vmcnt(0)) before each
+          // step's loads, the previous step's stores included
+          auto load_row = [&](int zz, int k) {
+            const uint32_t po = uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
+#pragma unroll
+            for (int h = 0; h < H; ++h)
+              C[k][h] = __builtin_bit_cast(
+                  NV, __builtin_amdgcn_raw_buffer_load_b128(srcRsrc, rowoff + uint32_t(h * CS * int(sizeof(T))), po, 0));
+          };
+          // step t = -4 starts with src planes z+dz .. z+(NC-1)dz, z = z0 - 4dz, and the src row of its u1 plane
+          // (z+2dz: slot 1) published
+          {
+            const int zw = z0 - 3 * dz;
+#pragma unroll
+            for (int k = 0; k < NC - 1; ++k) load_row(zw + k * dz, k);
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+              cs[0][w][h][lane] = C[1][h];
+              U1a[h] = U1b[h] = U1c[h] = U2a[h] = U2b[h] = U2c[h] = C[1][h]; // overwritten before any use
+            }
+            __syncthreads();
+          }
+          int buf = 0;
+          int t = -4;
+          // one z step with LV = min(role, levels valid at this step) levels
+          auto step = [&](auto phase, auto lvTag) -> bool {
+            constexpr int k = decltype(phase)::value;
+            constexpr int LV = decltype(lvTag)::value;
+            // slots: s0 = plane z+dz, s1 = z+2dz, s2 = z+3dz; sn receives z + NC dz (it held plane z)
+            constexpr int s0 = k % NC, s1 = (k + 1) % NC, s2 = (k + 2) % NC, sn = (k + NC - 1) % NC;
+            if (t >= nzs) return false;
+            const int z = z0 + t * dz;
+            load_row(z + NC * dz, sn);
+            NV o[H];
+            // every level reads the previous step's rows (buf): no level waits for another's LDS writes; each
+            // level's row goes into the other buffer (its readers finished last step) right after its update, the src
+            // row right after u1 (its load was waited for there): the step is bound by LDS write -> barrier -> LDS read
+            // -> update three times, with only 2-3 waves per SIMD to overlap it (r5: 1381-1392 -> 1431-1443 Gcells/s
+            // against publishing everything before the barrier, profiles/r5/v)
+            auto levels = [&]() {
+              NV A1[H], B1[H], A2[H], B2[H], A3[H], B3[H];
+              auto rd = [&](NV(&sh)[2][NW][H][64], NV(&A)[H], NV(&B)[H]) {
+#pragma unroll
+                for (int h = 0; h < H; ++h) {
+                  A[h] = sh[buf][wA][h][lane];
+                  B[h] = sh[buf][wB][h][lane];
+                }
+              };
+              if constexpr (LV >= 1) {
+                rd(cs, A1, B1);
+                (void)row_update(C[s1], A1, B1, DOWN ? C[s0] : C[s2], DOWN ? C[s2] : C[s0], U1a);
+                sphere_row(row_sph(z + 2 * dz), U1a);
+#pragma unroll
+                for (int h = 0; h < H; ++h) cs[buf ^ 1][w][h][lane] = C[s2][h];
+#pragma unroll
+                for (int h = 0; h < H; ++h) us[buf ^ 1][w][h][lane] = U1a[h];
+              }
+              if constexpr (LV >= 2) {
+                rd(us, A2, B2);
+                (void)row_update(U1c, A2, B2, DOWN ? U1b : U1a, DOWN ? U1a : U1b, U2a);
+                sphere_row(row_sph(z + dz), U2a);
+#pragma unroll
+                for (int h = 0; h < H; ++h) vs[buf ^ 1][w][h][lane] = U2a[h];
+              }
+              if constexpr (LV >= 3) {
+                rd(vs, A3, B3);
+                (void)row_update(U2c, A3, B3, DOWN ? U2b : U2a, DOWN ? U2a : U2b, o);
+                sphere_row(row_sph(z), o);
+              }
+            };
+            levels();
+            if constexpr (LV >= 3) {
+              // unconditional: a row past the region's y end (the last row group) stores into a per-device sink, so
+              // every path has the same vector-memory ops and the next step's load wait counts past these stores
+              char *dp = outRow ? reinterpret_cast<char *>(a.dst + int64_t(z) * a.pxy) + outoff
+                                : a.sink + lane * LS * int(sizeof(T));
+#pragma unroll
+              for (int h = 0; h < H; ++h) {
+                NV *q = reinterpret_cast<NV *>(dp + h * CS * int(sizeof(T)));
+                if (a.nt)
+                  __builtin_nontemporal_store(o[h], q);
+                else
+                  *q = o[h];
+              }
+            }
+            const int nbuf = buf ^ 1;
+            if constexpr (LV < 1)
+#pragma unroll
+              for (int h = 0; h < H; ++h) cs[nbuf][w][h][lane] = C[s2][h];
+            // boundary-plane publication (block-uniform, as the pairs): every wave's stores of output plane z
+            // complete before the barrier, then one thread writes the L2 back (release) and counts the block's cells
+            const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
+            if (pubStep) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (pubStep && lane == 0 && w == 0) {
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+              const unsigned long long cells =
+                  (unsigned long long)(min(YO, a.hiy - yblk)) * (unsigned long long)(a.hix - a.lox);
+              __hip_atomic_fetch_add(a.pub, cells, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            buf = nbuf;
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+              U1b[h] = U1c[h];
+              U1c[h] = U1a[h];
+              U2b[h] = U2c[h];
+              U2c[h] = U2a[h];
+            }
+            ++t;
+            return true;
+          };
+          using I0 = std::integral_constant<int, 0>;
+          using I1 = std::integral_constant<int, 1>;
+          using I2 = std::integral_constant<int, 2>;
+          using I3 = std::integral_constant<int, 3>;
+          using L1 = std::integral_constant<int, (R < 1 ? R : 1)>;
+          using L2 = std::integral_constant<int, (R < 2 ? R : 2)>;
+          using LR = std::integral_constant<int, R>;
+          // warm-up: t = -4, -3 compute u1 only, t = -2, -1 u1 and u2 (one cycle of the slot rotation)
+          step(I0{}, L1{});
+          step(I1{}, L1{});
+          step(I2{}, L2{});
+          step(I3{}, L2{});
+          while (step(I0{}, LR{}) && step(I1{}, LR{}) && step(I2{}, LR{}) && step(I3{}, LR{})) {
+          }
+        };
+        if (down)
+          march(std::true_type{});
+        else
+          march(std::false_type{});
+      } // segments
+    }   // passes
+  };
+  const unsigned long long clk0 = a.clk ? wall_clock64() : 0;
+  const int role = (w >= 3 && w < NW - 3) ? 3 : ((w >= 2 && w < NW - 2) ? 2 : ((w >= 1 && w < NW - 1) ? 1 : 0));
+  if (role == 3)
+    body(std::integral_constant<int, 3>{});
+  else if (role == 2)
+    body(std::integral_constant<int, 2>{});
+  else if (role == 1)
+    body(std::integral_constant<int, 1>{});
   else
     body(std::integral_constant<int, 0>{});
   if (a.clk) { // measurement only (StencilTune::blockClock): every wave done, one lane stores the block's interval
@@ -538,6 +848,13 @@ stencil7x3_row_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
 
 // ---------------------------------------------------------------------------------------------------------
 // host side
+template <typename T, int KIND> static const void *x3_wrap_kernel_ptr() {
+  if constexpr (std::is_same<T, float>::value)
+    return (const void *)stencil7x3_wrap_kernel<KIND>;
+  else
+    return nullptr;
+}
+
 // ---------------------------------------------------------------------------------------------------------
 static int64_t x3_resident_blocks(const void *kernel, int threads) {
   static std::map<const void *, int64_t> cache;
@@ -632,7 +949,7 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   const int nx = a.hix - a.lox, ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = XH ? int(nx / x3_column_cells(int64_t(sizeof(T)))) : 1;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = (const void *)stencil7x3_row_kernel<T, KIND, XH>;
+  const void *kern = XH ? (const void *)stencil7x3_xh_kernel<T, KIND> : x3_wrap_kernel_ptr<T, KIND>();
   const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x3_resident_blocks(kern, 64 * NW);
   // CUs left to the transport kernels running beside the sweep (pipelined triples: the gated exchange)
@@ -703,7 +1020,10 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.sink = x3_sink(dom.gpu(), false);
   a.clk = reinterpret_cast<unsigned long long *>(tune.blockClock);
   STENCIL_REQUIRE(a.sink, "stencil7x3: no store sink on device " << dom.gpu() << " (stencil7x3_supported first)");
-  hipLaunchKernelGGL((stencil7x3_row_kernel<T, KIND, XH>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+  if constexpr (XH || !std::is_same<T, float>::value)
+    hipLaunchKernelGGL((stencil7x3_xh_kernel<T, KIND>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+  else
+    hipLaunchKernelGGL((stencil7x3_wrap_kernel<KIND>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   HIP_CHECK(hipGetLastError());
 }
 

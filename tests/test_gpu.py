@@ -305,7 +305,7 @@ def test_temporal2_in_kernel_wrap(st, size, fp64, gpus, kind):
                                        ("jacobi", (512, 512, 112)), ("astaroth", (512, 36, 28)),
                                        ("astaroth", (512, 13, 17)), ("astaroth", (512, 3, 16))])
 def test_temporal3_matches_three_single_steps(st, kind, size, sched, scale):
-    """Fused triples (stencil7x3_row_kernel, temporal=3, one GPU, every axis wrapped in-kernel): S(S(S(u))) bitwise
+    """Fused triples (stencil7x3_wrap_kernel, temporal=3, one GPU, every axis wrapped in-kernel): S(S(S(u))) bitwise
     equal to three single steps of the torch oracle; run(n) covers whole hipGraph blocks (18 steps), triples and the
     pair / single-step remainders; y extents that are not a multiple of the block's 6 output rows and a 3-row grid
     (every block row wraps onto itself twice). scale 1e-33 puts every sum below 2^-100, where the quotient is the
