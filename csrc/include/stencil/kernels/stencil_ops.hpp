@@ -52,6 +52,9 @@ struct StencilTune {
                           // parts are cut per row group (0: equal parts)
   float x2sphw = 0.15f;   // fused pairs (Jacobi, row / col2 kernels): sphere weight of the z parts (r5/at, r5/au)
   bool x3sphchunk = true; // fused triples (Jacobi): test each sphere only on the lane chunks its x range reaches
+  // fused triples, lockstep parts: each block's slice of the leftover row groups levels it against the blocks whose
+  // parts cost more (sphere-crossing groups); false = equal slices
+  bool x3balance = true;
   bool x2early = true;    // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
                           // (row kernel 208.6 vs 216.6 us per pair, col2 226.9 vs 234.1)
   // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells

@@ -38,6 +38,7 @@
 #include <utility>
 #include <vector>
 #include <cmath>
+#include <cstring>
 
 #include "stencil/kernels/stencil_ops.hpp"
 #include "stencil/rt/hip_check.hpp"
@@ -74,9 +75,14 @@ __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<T> &a, const ZPar
     // publishing boundary planes (a.pub): the first part marches up from the low z face and the last one down
     // from the high face, so both faces' planes come out in the first steps of the sweep
     r.odd = a.pub != nullptr ? (qq + 1 == P || (qq != 0 && (qq & 1) != 0)) : (qq & 1) != 0;
-    const uint64_t LW = uint64_t(ncols - cm) * nzt;
-    r.s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
-    r.e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
+    if (B.lon) { // levelled against the parts (balance_leftover)
+      r.s2 = cm * nzt + B.s2[lb];
+      r.e2 = cm * nzt + B.s2[lb + 1];
+    } else {
+      const uint64_t LW = uint64_t(ncols - cm) * nzt;
+      r.s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
+      r.e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
+    }
   } else {
     const uint64_t W = uint64_t(ncols) * nzt;
     r.s = uint32_t(uint64_t(lb) * W / nb);
@@ -1012,10 +1018,29 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     a.zrounds = ls.rounds;
     blocks = uint32_t(ls.blocks);
   }
+  // z-part bounds and leftover slices depend on the geometry only: computed once per shape (host work of a few ms
+  // would otherwise precede every un-captured launch)
   ZPartBounds zb{};
-  zb.on = 0;
-  if (KIND == 0 && a.seg == 2)
-    sphere_part_bounds(zb, a, std::min<int64_t>(int64_t(blocks) / a.zparts, a.gy), a.zparts, NW, YO, 3, tune.x3sphw);
+  if (a.seg == 2) {
+    static std::map<std::vector<int64_t>, ZPartBounds> cache;
+    static std::mutex mu;
+    const float w = KIND == 0 ? tune.x3sphw : 0.f;
+    int32_t wbits = 0;
+    std::memcpy(&wbits, &w, sizeof(w));
+    const std::vector<int64_t> key{KIND,  a.loy, a.hiy,  a.loz,     a.hiz,     a.hy,          a.cy,
+                                   a.hz,  a.cz,  a.r1sq, int64_t(blocks), a.zparts, cols, a.gy,
+                                   wbits, tune.x3balance};
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+      ZPartBounds b{};
+      const int64_t cm = int64_t(blocks) / a.zparts;
+      if (KIND == 0) sphere_part_bounds(b, a, std::min<int64_t>(cm, a.gy), a.zparts, NW, YO, 3, w);
+      if (tune.x3balance) balance_leftover(b, a, int64_t(blocks), cm, a.zparts, cols, a.gy, NW, YO, 3, w, 4, 1.0);
+      it = cache.emplace(key, b).first;
+    }
+    zb = it->second;
+  }
   dom.set_device();
   a.sink = x3_sink(dom.gpu(), false);
   a.clk = reinterpret_cast<unsigned long long *>(tune.blockClock);

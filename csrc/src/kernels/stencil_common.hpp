@@ -210,11 +210,51 @@ __device__ __forceinline__ T sum6(T vpx, T vmx, T vpy, T vmy, T vpz, T vmz) {
 // triples): the Jacobi blocks whose rows cross the hot / cold spheres pay the per-cell sphere tests on those planes
 // and set the sweep's time (profiles/r5/ak), so the host cuts each group's z range by plane weights
 // 1 + w * (the group's rows crossing a sphere at that plane) / rows; on = 0: equal parts
-constexpr int kZPartMaxCols = 256, kZPartMaxParts = 4;
+constexpr int kZPartMaxCols = 256, kZPartMaxParts = 4, kLeftMaxBlocks = 256;
 struct ZPartBounds {
   int on;
   uint16_t zb[kZPartMaxCols][kZPartMaxParts - 1];
+  // lon: block lb's second segment is leftover (column, plane) slice [s2[lb], s2[lb + 1]) (balance_leftover);
+  // 0: equal slices
+  int lon;
+  uint16_t s2[kLeftMaxBlocks + 1];
 };
+
+// plane weights of row group grp (blocks holding rows [yblk - rowOff, yblk - rowOff + rows), yblk = loy + YO grp):
+// 1 + w * (levels of the group's rows crossing a sphere at that plane) / (sum of levels); false: no sphere crossed
+template <typename T>
+inline bool sphere_group_weights(std::vector<double> &wz, const StencilArgs<T> &a, int64_t grp, int rows, int YO,
+                                 int rowOff, float w) {
+  const int nz = a.hiz - a.loz;
+  wz.assign(static_cast<size_t>(nz), 1.0);
+  if (a.r1sq <= 0 || w <= 0) return false;
+  auto isqrt_below = [](int d) { // largest h >= 0 with h * h < d (d > 0)
+    int h = int(std::sqrt(double(d - 1)));
+    while (h > 0 && h * h > d - 1) --h;
+    while ((h + 1) * (h + 1) <= d - 1) ++h;
+    return h;
+  };
+  double levelSum = 0;
+  for (int r = 0; r < rows; ++r) levelSum += std::min(std::min(r, rows - 1 - r), rowOff);
+  bool any = false;
+  const int yblk = a.loy + YO * int(grp);
+  for (int r = 0; r < rows; ++r) {
+    const int y = yblk - rowOff + r;
+    const double lw = w * std::min(std::min(r, rows - 1 - r), rowOff) / levelSum;
+    if (lw <= 0) continue;
+    const int cy[2] = {a.hy, a.cy}, cz[2] = {a.hz, a.cz};
+    for (int sidx = 0; sidx < 2; ++sidx) {
+      const int d = a.r1sq - (y - cy[sidx]) * (y - cy[sidx]);
+      if (d <= 0) continue;
+      const int h = isqrt_below(d);
+      for (int z = std::max(a.loz, cz[sidx] - h); z <= std::min(a.hiz - 1, cz[sidx] + h); ++z) {
+        wz[static_cast<size_t>(z - a.loz)] += lw;
+        any = true;
+      }
+    }
+  }
+  return any;
+}
 // fills b for cm row groups of YO output rows, each block holding rows [yblk - rowOff, yblk - rowOff + rows); a row
 // r that crosses a sphere adds w * levels(r) / (sum of levels) to the plane's weight, levels(r) = the number of
 // updates the row's wave computes per step (min(r, rows - 1 - r, rowOff): the edge rows only load)
@@ -224,34 +264,10 @@ inline void sphere_part_bounds(ZPartBounds &b, const StencilArgs<T> &a, int64_t 
   b.on = 0;
   const int nz = a.hiz - a.loz;
   if (a.r1sq <= 0 || w <= 0 || P < 2 || P > kZPartMaxParts || cm > kZPartMaxCols || nz >= 65536) return;
-  auto isqrt_below = [](int d) { // largest h >= 0 with h * h < d (d > 0)
-    int h = int(std::sqrt(double(d - 1)));
-    while (h > 0 && h * h > d - 1) --h;
-    while ((h + 1) * (h + 1) <= d - 1) ++h;
-    return h;
-  };
-  std::vector<double> wz(static_cast<size_t>(nz));
+  std::vector<double> wz;
   bool any = false;
-  double levelSum = 0;
-  for (int r = 0; r < rows; ++r) levelSum += std::min(std::min(r, rows - 1 - r), rowOff);
   for (int64_t col = 0; col < cm; ++col) {
-    std::fill(wz.begin(), wz.end(), 1.0);
-    const int yblk = a.loy + YO * int(col);
-    for (int r = 0; r < rows; ++r) {
-      const int y = yblk - rowOff + r;
-      const double lw = w * std::min(std::min(r, rows - 1 - r), rowOff) / levelSum;
-      if (lw <= 0) continue;
-      const int cy[2] = {a.hy, a.cy}, cz[2] = {a.hz, a.cz};
-      for (int sidx = 0; sidx < 2; ++sidx) {
-        const int d = a.r1sq - (y - cy[sidx]) * (y - cy[sidx]);
-        if (d <= 0) continue;
-        const int h = isqrt_below(d);
-        for (int z = std::max(a.loz, cz[sidx] - h); z <= std::min(a.hiz - 1, cz[sidx] + h); ++z) {
-          wz[static_cast<size_t>(z - a.loz)] += lw;
-          any = true;
-        }
-      }
-    }
+    any = sphere_group_weights(wz, a, col, rows, YO, rowOff, w) || any;
     double total = 0;
     for (double v : wz) total += v;
     double acc = 0;
@@ -263,6 +279,68 @@ inline void sphere_part_bounds(ZPartBounds &b, const StencilArgs<T> &a, int64_t 
     while (q < P) b.zb[col][(q++) - 1] = uint16_t(nz);
   }
   b.on = any ? 1 : 0;
+}
+
+// Second segments levelled against the lockstep parts (seg 2: block lb = q * cm + col runs part q of column col, then
+// a slice of the leftover columns [cm, ncols)). Equal slices leave every block of a sphere-crossing row group its
+// parts' extra steps on top: at 512^3 (P = 4 parts of 64 groups + 22 leftover groups) those 72 blocks ran ~20 us
+// longer than the rest and set the sweep (profiles/r6/r6r). Here block lb takes leftover planes in order until
+// main(lb) + its slice reaches a common level T, the least T that places every plane (bisection): planes weighted as
+// the parts are (sphere_group_weights; leftover steps cost `leftw`), each segment start `warm` steps. Columns are
+// numbered y-major in x strips (row group = col % gy); b.zb as filled by sphere_part_bounds (b.on), else equal parts.
+template <typename T>
+inline void balance_leftover(ZPartBounds &b, const StencilArgs<T> &a, int64_t nb, int64_t cm, int P, int64_t ncols,
+                             int64_t gy, int rows, int YO, int rowOff, float w, int warm, double leftw) {
+  b.lon = 0;
+  const int64_t nz = a.hiz - a.loz;
+  const int64_t LW = (ncols - cm) * nz;
+  if (LW <= 0 || LW > 65535 || nb > kLeftMaxBlocks || nb != int64_t(P) * cm || cm <= 0 || gy <= 0) return;
+  std::vector<double> wz, mainc(static_cast<size_t>(nb)), lw(static_cast<size_t>(LW));
+  for (int64_t col = 0; col < cm; ++col) {
+    const int64_t grp = col % gy;
+    sphere_group_weights(wz, a, grp, rows, YO, rowOff, w);
+    for (int q = 0; q < P; ++q) {
+      int64_t zlo = int64_t(q) * nz / P, zhi = int64_t(q + 1) * nz / P;
+      if (b.on && grp < kZPartMaxCols) {
+        zlo = q > 0 ? b.zb[grp][q - 1] : 0;
+        zhi = q + 1 < P ? b.zb[grp][q] : nz;
+      }
+      double c = warm;
+      for (int64_t z = zlo; z < zhi; ++z) c += wz[static_cast<size_t>(z)];
+      mainc[static_cast<size_t>(q * cm + col)] = c;
+    }
+  }
+  double total = 0;
+  for (int64_t col = cm; col < ncols; ++col) {
+    sphere_group_weights(wz, a, col % gy, rows, YO, rowOff, w);
+    for (int64_t z = 0; z < nz; ++z) {
+      lw[static_cast<size_t>((col - cm) * nz + z)] = leftw * wz[static_cast<size_t>(z)];
+      total += leftw * wz[static_cast<size_t>(z)];
+    }
+  }
+  // greedy fill at level T; true when every leftover plane found a block
+  auto fill = [&](double lvl, uint16_t *out) {
+    int64_t i = 0;
+    for (int64_t lb = 0; lb < nb; ++lb) {
+      if (out) out[lb] = uint16_t(i);
+      double c = mainc[static_cast<size_t>(lb)];
+      for (bool started = false; i < LW; started = true, ++i) {
+        const double add = lw[static_cast<size_t>(i)] + ((!started || i % nz == 0) ? warm : 0);
+        if (c + add > lvl) break;
+        c += add;
+      }
+    }
+    if (out) out[nb] = uint16_t(i);
+    return i >= LW;
+  };
+  double lo = *std::max_element(mainc.begin(), mainc.end()), hi = lo + total + double(warm) * double(ncols - cm + 1);
+  if (!fill(hi, nullptr)) return;
+  for (int it = 0; it < 48 && hi - lo > 1e-3; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    (fill(mid, nullptr) ? hi : lo) = mid;
+  }
+  fill(hi, b.s2);
+  b.lon = 1;
 }
 
 // hot/cold sphere override of the Jacobi app at raw (x, y, z)
