@@ -598,7 +598,9 @@ def main(argv=None):
                             interior_align=args.interior_align, backend=st.Backend.Host if args.cpu else None,
                             shared_halo_line=bool(args.shared_halo_line == 1 if shared is None else shared))
         model.init()
-        model.prepare()  # hipGraph capture + instantiation (no steps run) outside the timed region
+        # hipGraph capture + instantiation (no steps run) outside the timed region: the 18-step blocks, and one graph of
+        # a whole run(--steps) (the blocks plus the remainder in one launch; the same kernels in the same order)
+        model.prepare([args.steps])
         model.run(args.warmup)
         model.synchronize()
         env.barrier()

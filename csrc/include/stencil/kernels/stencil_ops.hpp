@@ -48,8 +48,10 @@ struct StencilTune {
   int nw = 8;     // waves per block stacked in y (deep-lookahead variants: 4/8/16)
   int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
-  float x3sphw = 0.3f;    // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z
-                          // parts are cut per row group (0: equal parts)
+  // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z parts are cut per row group
+  // and the leftover slices levelled (0: equal parts). 0.3 was best with equal leftover slices; with x3balance 0.6
+  // (512^3 driver command 1581-1584 vs 1551-1581 at 0.45, 1547-1556 at 0.8, profiles/r6/r6z)
+  float x3sphw = 0.6f;
   float x2sphw = 0.15f;   // fused pairs (Jacobi, row / col2 kernels): sphere weight of the z parts (r5/at, r5/au)
   bool x3sphchunk = true; // fused triples (Jacobi): test each sphere only on the lane chunks its x range reaches
   // fused triples, lockstep parts: each block's slice of the leftover row groups levels it against the blocks whose

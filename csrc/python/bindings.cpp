@@ -794,7 +794,8 @@ PYBIND11_MODULE(_C, m) {
       .def("init", &StencilModel::init, py::call_guard<py::gil_scoped_release>())
       .def("step", &StencilModel::step, py::call_guard<py::gil_scoped_release>())
       .def("run", &StencilModel::run, py::call_guard<py::gil_scoped_release>())
-      .def("prepare", &StencilModel::prepare, py::call_guard<py::gil_scoped_release>())
+      .def("prepare", &StencilModel::prepare, py::arg("runs") = std::vector<int>{},
+           py::call_guard<py::gil_scoped_release>())
       .def("synchronize", &StencilModel::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("cells", &StencilModel::cells)
       .def("local_cells", &StencilModel::local_cells)

@@ -62,6 +62,8 @@ StencilModel::~StencilModel() {
     if (g) (void)hipGraphExecDestroy(g);
   for (auto &g : graphBlock_)
     if (g) (void)hipGraphExecDestroy(g);
+  for (auto &kv : runGraph_)
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
   if (pubCounter_) (void)hipFree(pubCounter_);
 }
 
@@ -348,6 +350,15 @@ void StencilModel::step() {
 void StencilModel::run(int iters) {
   TraceRange tr("StencilModel::run");
   auto &doms = dd_->domains();
+  if (graphs_ && iters > 0) { // a whole run recorded by prepare({iters})
+    auto it = runGraph_.find({iters, doms[0].parity()});
+    if (it != runGraph_.end()) {
+      for (int k = 0; k < it->second.sweeps; ++k) dd_->swap();
+      HIP_CHECK(hipGraphLaunch(it->second.exec, compute_[0].get()));
+      steps_ += iters;
+      return;
+    }
+  }
   const int per = steps_per_sweep(), gsteps = graph_steps();
   const int sweeps = gsteps / per; // sweeps per graph block (an even number: the block keeps the parity)
   while (graphs_ && iters >= gsteps) {
@@ -398,12 +409,41 @@ void StencilModel::capture_block() {
   HIP_CHECK(hipGraphDestroy(g));
 }
 
-void StencilModel::prepare() {
+void StencilModel::capture_run(int n) {
+  // the sweeps run(n) enqueues (graph blocks, then triples, pairs, single steps: the same kernels in the same order)
+  // recorded as one graph; the swaps done while recording are undone
+  auto &doms = dd_->domains();
+  const int p = doms[0].parity();
+  hipStream_t s = compute_[0].get();
+  hipGraph_t g = nullptr;
+  int sw = 0;
+  HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  for (int left = n; left > 0;) {
+    const int k = triples_ && left >= 3 ? 3 : (pairs_ && left >= 2 ? 2 : 1);
+    enqueue_step(k);
+    dd_->swap();
+    ++sw;
+    left -= k;
+  }
+  HIP_CHECK(hipStreamEndCapture(s, &g));
+  RunGraph rg;
+  rg.sweeps = sw;
+  HIP_CHECK(hipGraphInstantiate(&rg.exec, g, nullptr, nullptr, 0));
+  HIP_CHECK(hipGraphDestroy(g));
+  if (sw % 2) dd_->swap();
+  runGraph_[{n, p}] = rg;
+}
+
+void StencilModel::prepare(const std::vector<int> &runs) {
   // instantiate the graph blocks of both buffer parities up front, so the first run() of a timed loop does not pay
   // for stream capture + instantiation (the bench's warm-up may be shorter than one block)
   if (!graphs_) return;
   for (int i = 0; i < 2; ++i) {
     if (!graphBlock_[dd_->domains()[0].parity()]) capture_block();
+    for (int n : runs) {
+      STENCIL_REQUIRE(n > 0 && n <= 1024, "prepare: run length " << n << " outside [1, 1024]");
+      if (!runGraph_.count({n, dd_->domains()[0].parity()})) capture_run(n);
+    }
     dd_->swap();
   }
 }

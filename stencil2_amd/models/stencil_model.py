@@ -77,9 +77,10 @@ class StencilModel:
     def run(self, iters: int):
         self._m.run(iters)
 
-    def prepare(self):
-        """Instantiate run()'s hipGraph blocks for both buffer parities (records work, runs nothing)."""
-        self._m.prepare()
+    def prepare(self, runs=()):
+        """Instantiate run()'s hipGraph blocks for both buffer parities (records work, runs nothing); for each length n
+        in `runs` also a graph of a whole run(n), which run(n) then replays as one launch."""
+        self._m.prepare(list(runs))
 
     def synchronize(self):
         self._m.synchronize()

@@ -587,6 +587,26 @@ def test_prepare_graph_blocks(st, temporal):
     assert torch.equal(_gather(m), u)
 
 
+@pytest.mark.parametrize("temporal,size", [(1, (48, 40, 36)), (2, (48, 40, 36)), (3, (512, 120, 116))])
+def test_prepare_whole_run_graphs(st, temporal, size):
+    """prepare(runs) also records one graph per listed run length and parity (blocks plus remainder sweeps): nothing
+    runs while recording, and run(n) replaying it from either parity (odd counts in between) matches the oracle."""
+    m = st.Jacobi3D(size, gpus=[0], temporal=temporal)
+    m.init()
+    if temporal == 3:
+        assert m.temporal_triples()
+    u = _gather(m)
+    m.prepare([20, 7, 1])
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+    for n in (20, 7, 20, 1, 20, 5):
+        m.run(n)
+        for _ in range(n):
+            u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
 def test_temporal2_spheres_at_periodic_face_fall_back(st):
     """Spheres that reach a periodic face (radius x/10 on a thin y/z grid) make the fused pair's halo-ring step
     differ from the neighbour's: the model runs single steps there, still equal to the oracle."""
