@@ -455,7 +455,7 @@ def make_tune(st, args):
 
 
 def tune_record(tune) -> dict:
-    return {k: getattr(tune, k) for k in ("x3sched", "x3parts", "x3sphw", "x3balance", "x2sphw", "x2early", "x2row",
+    return {k: getattr(tune, k) for k in ("x3sched", "x3parts", "x3sphw", "x3left", "x2sphw", "x2early", "x2row",
                                           "nontemporal", "alternate_z", "xcd_remap", "variant")}
 
 

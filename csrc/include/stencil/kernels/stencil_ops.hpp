@@ -49,14 +49,16 @@ struct StencilTune {
   int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
   // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z parts are cut per row group
-  // and the leftover slices levelled (0: equal parts). 0.3 was best with equal leftover slices; with x3balance 0.6
+  // and the leftover slices levelled (0: equal parts). 0.3 was best with equal leftover slices; with x3left 1 0.6
   // (512^3 driver command 1581-1584 vs 1551-1581 at 0.45, 1547-1556 at 0.8, profiles/r6/r6z)
   float x3sphw = 0.6f;
   float x2sphw = 0.15f;   // fused pairs (Jacobi, row / col2 kernels): sphere weight of the z parts (r5/at, r5/au)
   bool x3sphchunk = true; // fused triples (Jacobi): test each sphere only on the lane chunks its x range reaches
-  // fused triples, lockstep parts: each block's slice of the leftover row groups levels it against the blocks whose
-  // parts cost more (sphere-crossing groups); false = equal slices
-  bool x3balance = true;
+  // fused triples, lockstep parts: the row groups beyond the parts' (leftover groups) as second segments. 0 = equal
+  // slices; 1 = slices levelling each block against the blocks whose parts cost more (sphere-crossing groups);
+  // 2 = a second lockstep phase (every leftover group in K parts of common z bounds, blocks binned by their parts'
+  // cost); 3 = whichever of 1 / 2 the host's step estimate prefers, with the number of parts chosen the same way
+  int x3left = 3;
   bool x2early = true;    // fused pairs (row / col2 kernels): publish the src and u1 rows right after the u1 update
                           // (row kernel 208.6 vs 216.6 us per pair, col2 226.9 vs 234.1)
   // fused pairs of fp32 sub-domains: one wave per whole 512-cell periodic row (x wrapped in-kernel and 512 cells

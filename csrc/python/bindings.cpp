@@ -737,7 +737,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("x3parts", &StencilTune::x3parts)
       .def_readwrite("x3sphw", &StencilTune::x3sphw)
       .def_readwrite("x3sphchunk", &StencilTune::x3sphchunk)
-      .def_readwrite("x3balance", &StencilTune::x3balance)
+      .def_readwrite("x3left", &StencilTune::x3left)
       .def_readwrite("x2sphw", &StencilTune::x2sphw)
       .def_property(
           "block_clock", [](const StencilTune &t) { return reinterpret_cast<uintptr_t>(t.blockClock); },

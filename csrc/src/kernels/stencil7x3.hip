@@ -51,14 +51,16 @@ namespace stencil {
 // Columns are numbered y-major inside an x strip (col = bx * gy + by); the z-part bounds are per row group (by)
 struct X3Seg {
   uint32_t s, e, s2, e2;
-  bool odd;
+  bool odd;  // the first segment's march direction (down unless the sweep flips)
+  bool odd2; // the second's
 };
 template <typename T>
 __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<T> &a, const ZPartBounds &B, uint32_t lb, uint32_t nb,
                                              uint32_t ncols, uint32_t gy, uint32_t nzt) {
-  X3Seg r{0, 0, 0, 0, false};
+  X3Seg r{0, 0, 0, 0, false, false};
   if (a.seg == 3) { // rounds of whole column groups (x3_round): parts alternate their z direction as in seg 2
     r.odd = ((lb / (nb / uint32_t(a.zparts))) & 1) != 0;
+    r.odd2 = !r.odd;
     return r;
   }
   if (a.seg == 2) {
@@ -75,19 +77,22 @@ __device__ __forceinline__ X3Seg x3_segments(const StencilArgs<T> &a, const ZPar
     // publishing boundary planes (a.pub): the first part marches up from the low z face and the last one down
     // from the high face, so both faces' planes come out in the first steps of the sweep
     r.odd = a.pub != nullptr ? (qq + 1 == P || (qq != 0 && (qq & 1) != 0)) : (qq & 1) != 0;
-    if (B.lon) { // levelled against the parts (balance_leftover)
-      r.s2 = cm * nzt + B.s2[lb];
-      r.e2 = cm * nzt + B.s2[lb + 1];
+    if (B.lon) { // tabled (balance_leftover / lockstep_leftover)
+      r.s2 = cm * nzt + B.l0[lb];
+      r.e2 = cm * nzt + B.l1[lb];
+      r.odd2 = ((B.ldir[lb >> 5] >> (lb & 31)) & 1) != 0;
     } else {
       const uint64_t LW = uint64_t(ncols - cm) * nzt;
       r.s2 = cm * nzt + uint32_t(uint64_t(lb) * LW / nb);
       r.e2 = cm * nzt + uint32_t(uint64_t(lb + 1) * LW / nb);
+      r.odd2 = !r.odd;
     }
   } else {
     const uint64_t W = uint64_t(ncols) * nzt;
     r.s = uint32_t(uint64_t(lb) * W / nb);
     r.e = uint32_t(uint64_t(lb + 1) * W / nb);
     r.odd = (lb & 1) != 0;
+    r.odd2 = r.odd;
   }
   return r;
 }
@@ -182,6 +187,7 @@ stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
       const int pass = pubOrder ? 1 - pp : pp;
       uint32_t s = pass == 0 ? sg.s : sg.s2;
       uint32_t e = pass == 0 ? sg.e : sg.e2;
+      if (pass == 1 && !pubOrder) odd = sg.odd2;
       if (XH && a.seg == 3) {
         // round pp: column group pp cm + lb % cm, z part lb / cm (every block on y-adjacent columns in step)
         const uint32_t P = uint32_t(a.zparts), cm = nb / P, qq = lb / cm;
@@ -593,6 +599,7 @@ stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
       const int pass = pubOrder ? 1 - pp : pp;
       uint32_t s = pass == 0 ? sg.s : sg.s2;
       const uint32_t e = pass == 0 ? sg.e : sg.e2;
+      if (pass == 1 && !pubOrder) odd = sg.odd2;
       while (s < e) { // block-uniform
         const uint32_t by = s / nzt;
         const int zo = int(s - by * nzt);
@@ -1018,28 +1025,77 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     a.zrounds = ls.rounds;
     blocks = uint32_t(ls.blocks);
   }
-  // z-part bounds and leftover slices depend on the geometry only: computed once per shape (host work of a few ms
-  // would otherwise precede every un-captured launch)
+  // Lockstep parts (seg 2): the z-part bounds (sphere-weighted for Jacobi), the leftover groups' second segments
+  // (StencilTune::x3left) and, with the cost model's P, the number of parts are planned per shape on the host and
+  // cached (host work of a few ms would otherwise precede every un-captured launch). Auto P: the least estimated
+  // steps of the longest block over P = 2 .. 8 and both leftover plans.
   ZPartBounds zb{};
   if (a.seg == 2) {
-    static std::map<std::vector<int64_t>, ZPartBounds> cache;
+    struct Plan {
+      int P;
+      uint32_t blocks;
+      ZPartBounds b;
+    };
+    static std::map<std::vector<int64_t>, Plan> cache;
     static std::mutex mu;
     const float w = KIND == 0 ? tune.x3sphw : 0.f;
     int32_t wbits = 0;
     std::memcpy(&wbits, &w, sizeof(w));
-    const std::vector<int64_t> key{KIND,  a.loy, a.hiy,  a.loz,     a.hiz,     a.hy,          a.cy,
-                                   a.hz,  a.cz,  a.r1sq, int64_t(blocks), a.zparts, cols, a.gy,
-                                   wbits, tune.x3balance};
+    const bool autoP = tune.x3sched == 1 && tune.x3parts <= 0 && tune.x3left != 0;
+    const std::vector<int64_t> key{KIND,  a.loy,    a.hiy, a.loz,        a.hiz,       a.hy,         a.cy,
+                                   a.hz,  a.cz,     a.r1sq, int64_t(blocks), a.zparts, cols,        a.gy,
+                                   wbits, tune.x3left, autoP, slots};
     std::lock_guard<std::mutex> lk(mu);
     auto it = cache.find(key);
     if (it == cache.end()) {
-      ZPartBounds b{};
-      const int64_t cm = int64_t(blocks) / a.zparts;
-      if (KIND == 0) sphere_part_bounds(b, a, std::min<int64_t>(cm, a.gy), a.zparts, NW, YO, 3, w);
-      if (tune.x3balance) balance_leftover(b, a, int64_t(blocks), cm, a.zparts, cols, a.gy, NW, YO, 3, w, 4, 1.0);
-      it = cache.emplace(key, b).first;
+      constexpr double kUnsync = 1.2; // a step of an unsynchronised slice vs a lockstep step (profiles/r6/r6ab)
+      auto plan = [&](int P, int64_t nbP, ZPartBounds &b) -> double {
+        b = ZPartBounds{};
+        const int64_t cm = nbP / P;
+        if (KIND == 0) sphere_part_bounds(b, a, std::min<int64_t>(cm, a.gy), P, NW, YO, 3, w);
+        const int mode = tune.x3left;
+        ZPartBounds bg = b, bl = b;
+        const double tg = mode == 1 || mode == 3
+                              ? balance_leftover(bg, a, nbP, cm, P, cols, a.gy, NW, YO, 3, w, 4, mode == 3 ? kUnsync : 1.0)
+                              : -1;
+        const double tl = mode == 2 || mode == 3 ? lockstep_leftover(bl, a, nbP, cm, P, cols, a.gy, NW, YO, 3, w, 4, 16)
+                                                 : -1;
+        if (tl >= 0 && (tg < 0 || tl <= tg)) {
+          b = bl;
+          return tl;
+        }
+        if (tg >= 0) {
+          b = bg;
+          return tg;
+        }
+        const std::vector<double> mc = lockstep_part_costs(b, a, cm, P, a.gy, NW, YO, 3, w, 4);
+        const double left = cols > cm ? double((cols - cm) * nz) * kUnsync / double(nbP) + 4 : 0;
+        return *std::max_element(mc.begin(), mc.end()) + left;
+      };
+      Plan pl{a.zparts, blocks, ZPartBounds{}};
+      if (autoP) {
+        double best = -1;
+        // spheres: only parts the host can weight (P <= kZPartMaxParts); unweighted parts leave the sphere planes
+        // to one or two parts (P = 7 with a lockstep second phase: 297 vs 228 us per 512^3 triple, profiles/r6/r6ac)
+        const bool sph = KIND == 0 && a.r1sq > 0 && w > 0;
+        for (int P = 2; P <= (sph ? kZPartMaxParts : 8); ++P) {
+          const int64_t cm = std::min<int64_t>(cols, slots / P);
+          if (cm < 1 || nz / P < 16) continue;
+          ZPartBounds b;
+          const double t = plan(P, P * cm, b);
+          if (best < 0 || t < best - 1e-9) {
+            best = t;
+            pl = Plan{P, uint32_t(P * cm), b};
+          }
+        }
+      } else {
+        (void)plan(a.zparts, int64_t(blocks), pl.b);
+      }
+      it = cache.emplace(key, pl).first;
     }
-    zb = it->second;
+    a.zparts = it->second.P;
+    blocks = it->second.blocks;
+    zb = it->second.b;
   }
   dom.set_device();
   a.sink = x3_sink(dom.gpu(), false);

@@ -214,10 +214,11 @@ constexpr int kZPartMaxCols = 256, kZPartMaxParts = 4, kLeftMaxBlocks = 256;
 struct ZPartBounds {
   int on;
   uint16_t zb[kZPartMaxCols][kZPartMaxParts - 1];
-  // lon: block lb's second segment is leftover (column, plane) slice [s2[lb], s2[lb + 1]) (balance_leftover);
-  // 0: equal slices
+  // lon: block lb's second segment is the leftover (column, plane) slice [l0[lb], l1[lb]) (offsets from the first
+  // leftover column), marching down when bit lb of ldir is set (balance_leftover / lockstep_leftover); 0: equal slices
   int lon;
-  uint16_t s2[kLeftMaxBlocks + 1];
+  uint16_t l0[kLeftMaxBlocks], l1[kLeftMaxBlocks];
+  uint32_t ldir[kLeftMaxBlocks / 32];
 };
 
 // plane weights of row group grp (blocks holding rows [yblk - rowOff, yblk - rowOff + rows), yblk = loy + YO grp):
@@ -288,14 +289,12 @@ inline void sphere_part_bounds(ZPartBounds &b, const StencilArgs<T> &a, int64_t 
 // main(lb) + its slice reaches a common level T, the least T that places every plane (bisection): planes weighted as
 // the parts are (sphere_group_weights; leftover steps cost `leftw`), each segment start `warm` steps. Columns are
 // numbered y-major in x strips (row group = col % gy); b.zb as filled by sphere_part_bounds (b.on), else equal parts.
+// block costs (steps) of the lockstep parts: warm + the part's plane weights, block lb = q * cm + col
 template <typename T>
-inline void balance_leftover(ZPartBounds &b, const StencilArgs<T> &a, int64_t nb, int64_t cm, int P, int64_t ncols,
-                             int64_t gy, int rows, int YO, int rowOff, float w, int warm, double leftw) {
-  b.lon = 0;
+inline std::vector<double> lockstep_part_costs(const ZPartBounds &b, const StencilArgs<T> &a, int64_t cm, int P,
+                                               int64_t gy, int rows, int YO, int rowOff, float w, int warm) {
   const int64_t nz = a.hiz - a.loz;
-  const int64_t LW = (ncols - cm) * nz;
-  if (LW <= 0 || LW > 65535 || nb > kLeftMaxBlocks || nb != int64_t(P) * cm || cm <= 0 || gy <= 0) return;
-  std::vector<double> wz, mainc(static_cast<size_t>(nb)), lw(static_cast<size_t>(LW));
+  std::vector<double> wz, mainc(static_cast<size_t>(int64_t(P) * cm));
   for (int64_t col = 0; col < cm; ++col) {
     const int64_t grp = col % gy;
     sphere_group_weights(wz, a, grp, rows, YO, rowOff, w);
@@ -310,6 +309,19 @@ inline void balance_leftover(ZPartBounds &b, const StencilArgs<T> &a, int64_t nb
       mainc[static_cast<size_t>(q * cm + col)] = c;
     }
   }
+  return mainc;
+}
+
+// returns the level (steps of the longest block), or -1 where the slices cannot be tabled (b.lon = 0: equal slices)
+template <typename T>
+inline double balance_leftover(ZPartBounds &b, const StencilArgs<T> &a, int64_t nb, int64_t cm, int P, int64_t ncols,
+                               int64_t gy, int rows, int YO, int rowOff, float w, int warm, double leftw) {
+  b.lon = 0;
+  const int64_t nz = a.hiz - a.loz;
+  const int64_t LW = (ncols - cm) * nz;
+  if (LW <= 0 || LW > 65535 || nb > kLeftMaxBlocks || nb != int64_t(P) * cm || cm <= 0 || gy <= 0) return -1;
+  const std::vector<double> mainc = lockstep_part_costs(b, a, cm, P, gy, rows, YO, rowOff, w, warm);
+  std::vector<double> wz, lw(static_cast<size_t>(LW));
   double total = 0;
   for (int64_t col = cm; col < ncols; ++col) {
     sphere_group_weights(wz, a, col % gy, rows, YO, rowOff, w);
@@ -319,28 +331,126 @@ inline void balance_leftover(ZPartBounds &b, const StencilArgs<T> &a, int64_t nb
     }
   }
   // greedy fill at level T; true when every leftover plane found a block
-  auto fill = [&](double lvl, uint16_t *out) {
+  auto fill = [&](double lvl, bool set) {
     int64_t i = 0;
     for (int64_t lb = 0; lb < nb; ++lb) {
-      if (out) out[lb] = uint16_t(i);
+      const int64_t i0 = i;
       double c = mainc[static_cast<size_t>(lb)];
       for (bool started = false; i < LW; started = true, ++i) {
         const double add = lw[static_cast<size_t>(i)] + ((!started || i % nz == 0) ? warm : 0);
         if (c + add > lvl) break;
         c += add;
       }
+      if (set) {
+        b.l0[lb] = uint16_t(i0);
+        b.l1[lb] = uint16_t(i);
+      }
     }
-    if (out) out[nb] = uint16_t(i);
     return i >= LW;
   };
   double lo = *std::max_element(mainc.begin(), mainc.end()), hi = lo + total + double(warm) * double(ncols - cm + 1);
-  if (!fill(hi, nullptr)) return;
+  if (!fill(hi, false)) return -1;
   for (int it = 0; it < 48 && hi - lo > 1e-3; ++it) {
     const double mid = 0.5 * (lo + hi);
-    (fill(mid, nullptr) ? hi : lo) = mid;
+    (fill(mid, false) ? hi : lo) = mid;
   }
-  fill(hi, b.s2);
+  fill(hi, true);
+  // directions as with equal slices: the second segment marches opposite to the block's part
+  for (int64_t lb = 0; lb < nb; ++lb) {
+    const uint32_t bit = 1u << (lb % 32);
+    if (((lb / cm) & 1) == 0)
+      b.ldir[lb / 32] |= bit;
+    else
+      b.ldir[lb / 32] &= ~bit;
+  }
   b.lon = 1;
+  return hi;
+}
+
+// The leftover row groups as a second lockstep phase: G = ncols - cm groups of K parts each, part k of every group
+// covering the same planes and marching the same way, so y-adjacent groups' blocks (consecutive blocks, one XCD)
+// share their halo rows in L2 as the first phase's parts do; unsynchronised slices re-read them (Astaroth 512^3:
+// 241.6 us per triple with 22 leftover groups in slices vs 224.0 with one 2-row group, profiles/r6/r6ab). Blocks are
+// binned by the cost of their lockstep part: the latest nb - K G get no second segment, the next G latest the
+// thinnest part, ..., and the part heights level every bin at a common T (at least minPlanes planes per part).
+// Returns T over the best K (or -1: not tabled; b.lon = 0).
+template <typename T>
+inline double lockstep_leftover(ZPartBounds &b, const StencilArgs<T> &a, int64_t nb, int64_t cm, int P, int64_t ncols,
+                                int64_t gy, int rows, int YO, int rowOff, float w, int warm, int minPlanes) {
+  b.lon = 0;
+  const int64_t nz = a.hiz - a.loz, G = ncols - cm;
+  if (G <= 0 || G * nz > 65535 || nb > kLeftMaxBlocks || nb != int64_t(P) * cm || cm <= 0 || gy <= 0) return -1;
+  const std::vector<double> mainc = lockstep_part_costs(b, a, cm, P, gy, rows, YO, rowOff, w, warm);
+  std::vector<int64_t> order(static_cast<size_t>(nb));
+  for (int64_t i = 0; i < nb; ++i) order[static_cast<size_t>(i)] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+    return mainc[static_cast<size_t>(x)] > mainc[static_cast<size_t>(y)];
+  });
+  auto late_of = [&](int64_t idle, int64_t k) { return mainc[static_cast<size_t>(order[static_cast<size_t>(idle + k * G)])]; };
+  double bestT = -1;
+  std::vector<int64_t> bestH;
+  int64_t bestK = 0;
+  for (int64_t K = 1; K * G <= nb && K * minPlanes <= nz; ++K) {
+    const int64_t idle = nb - K * G;
+    // bins k = 0 .. K-1, latest first. Parts for the `used` earliest bins (the latest dropped first while a level
+    // would leave them fewer than minPlanes planes): h_k = T - late_k - warm, sum h_k = nz
+    std::vector<int64_t> h(static_cast<size_t>(K), 0);
+    bool ok = false;
+    for (int64_t used = K; used >= 1 && !ok; --used) {
+      double sum = double(nz);
+      for (int64_t k = K - used; k < K; ++k) sum += late_of(idle, k) + warm;
+      const double t = sum / double(used);
+      if (t - late_of(idle, K - used) - warm < minPlanes) continue;
+      int64_t acc = 0;
+      for (int64_t k = K - used; k < K; ++k) {
+        h[static_cast<size_t>(k)] = std::max<int64_t>(minPlanes, int64_t(std::floor(t - late_of(idle, k) - warm)));
+        acc += h[static_cast<size_t>(k)];
+      }
+      // integer heights summing to nz: pad the earliest bins first, trim the latest first
+      for (int64_t k = K - 1; acc < nz; k = k > K - used ? k - 1 : K - 1, ++acc) ++h[static_cast<size_t>(k)];
+      for (int64_t k = K - used, guard = 0; acc > nz && guard < 4 * nz; k = k + 1 < K ? k + 1 : K - used, ++guard)
+        if (h[static_cast<size_t>(k)] > minPlanes) {
+          --h[static_cast<size_t>(k)];
+          --acc;
+        }
+      ok = acc == nz;
+    }
+    if (!ok) continue;
+    double worst = 0;
+    for (int64_t i = 0; i < idle; ++i) worst = std::max(worst, mainc[static_cast<size_t>(order[static_cast<size_t>(i)])]);
+    for (int64_t k = 0; k < K; ++k)
+      worst = std::max(worst, late_of(idle, k) + (h[static_cast<size_t>(k)] ? double(h[static_cast<size_t>(k)] + warm) : 0.0));
+    if (bestT < 0 || worst < bestT - 1e-9) {
+      bestT = worst;
+      bestH = h;
+      bestK = K;
+    }
+  }
+  if (bestT < 0) return -1;
+  const int64_t K = bestK, idle = nb - K * G;
+  for (int64_t i = 0; i < idle; ++i) {
+    const int64_t lb = order[static_cast<size_t>(i)];
+    b.l0[lb] = b.l1[lb] = 0;
+  }
+  // parts in z from the earliest bin (the tallest part) on, alternating direction; a bin's blocks take the groups
+  // in block order (y-adjacent groups on consecutive blocks)
+  int64_t z0 = 0;
+  for (int64_t k = K - 1; k >= 0; --k) {
+    std::vector<int64_t> bin(order.begin() + idle + k * G, order.begin() + idle + (k + 1) * G);
+    std::sort(bin.begin(), bin.end());
+    const int64_t hk = bestH[static_cast<size_t>(k)];
+    const uint32_t down = ((K - 1 - k) & 1) != 0;
+    for (int64_t g = 0; g < G; ++g) {
+      const int64_t lb = bin[static_cast<size_t>(g)];
+      b.l0[lb] = uint16_t(g * nz + z0);
+      b.l1[lb] = uint16_t(g * nz + z0 + hk);
+      const uint32_t bit = 1u << (lb % 32);
+      b.ldir[lb / 32] = down ? (b.ldir[lb / 32] | bit) : (b.ldir[lb / 32] & ~bit);
+    }
+    z0 += hk;
+  }
+  b.lon = 1;
+  return bestT;
 }
 
 // hot/cold sphere override of the Jacobi app at raw (x, y, z)

@@ -16,8 +16,12 @@ clk = torch.zeros(1024, dtype=torch.int64, device="cuda")
 t = st.StencilTune()
 t.block_clock = clk.data_ptr()
 t.x3sphw = sphw
+Pshow = 0
 for kv in sys.argv[5:]:
     k, v = kv.split("=", 1)
+    if k == "P":  # the parts to print by (the host's plan may choose another P than the step-count model below)
+        Pshow = int(v)
+        continue
     cur = getattr(t, k)
     setattr(t, k, (v.lower() in ("1", "true")) if isinstance(cur, bool) else type(cur)(v))
 nz = 512
@@ -39,7 +43,7 @@ d = [(int(c[b, 1]) - int(c[b, 0])) / 100.0 for b in range(nb)]  # 100 MHz wall c
 st_ = [(int(c[b, 0]) - t0) / 100.0 for b in range(nb)]
 en = [(int(c[b, 1]) - t0) / 100.0 for b in range(nb)]
 cols, slots = (ny + 5) // 6, 256
-P, best = t.x3parts, 1e30
+P, best = Pshow or t.x3parts, 1e30
 if P <= 0:
     for p in range(2, 9):
         cm = min(cols, slots // p)
