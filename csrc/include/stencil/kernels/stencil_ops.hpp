@@ -49,9 +49,10 @@ struct StencilTune {
   int x3sched = 1;        // fused triples: 0 = the pairs' lockstep schedule, 1 = lockstep over the most row groups
   int x3parts = 0;        // fused triples, x3sched 1: lockstep z parts per row group (0 = the cost model's choice)
   // fused triples (Jacobi): extra weight of a sphere-crossing row-plane when the lockstep z parts are cut per row group
-  // and the leftover slices levelled (0: equal parts). 0.3 was best with equal leftover slices; with x3left 1 0.6
-  // (512^3 driver command 1581-1584 vs 1551-1581 at 0.45, 1547-1556 at 0.8, profiles/r6/r6z)
-  float x3sphw = 0.6f;
+  // and the leftover groups planned (0: equal parts). 0.3 was best with equal leftover slices, 0.6 with levelled
+  // slices (x3left 1, profiles/r6/r6z), 0.45 with the second lockstep phase (x3left 2 / 3: steady-state 512^3 triple
+  // 226.1 us vs 228.2 at 0.3 and 228.1 at 0.6, driver command 1613-1633 Gcells/s, profiles/r6/r6ad)
+  float x3sphw = 0.45f;
   float x2sphw = 0.15f;   // fused pairs (Jacobi, row / col2 kernels): sphere weight of the z parts (r5/at, r5/au)
   bool x3sphchunk = true; // fused triples (Jacobi): test each sphere only on the lane chunks its x range reaches
   // fused triples, lockstep parts: the row groups beyond the parts' (leftover groups) as second segments. 0 = equal
