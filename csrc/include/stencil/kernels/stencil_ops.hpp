@@ -160,6 +160,17 @@ private:
   bool hasRest_ = false;
 };
 
+// The host plan of a whole-row fused-triple sweep (stencil7x3's lockstep schedule, as apply runs it for a sub-domain
+// of `size` cells with the reference's spheres for Jacobi, on `slots` resident blocks): for tests and tools, no GPU
+struct X3PlanInfo {
+  int parts = 0, blocks = 0, groups = 0, lockstepGroups = 0, rounds = 0;
+  bool tabled = false;     // second segments from l0 / l1 / odd (leftover (column, plane) offsets), else equal slices
+  double steps = 0;        // estimated steps of the longest block
+  std::vector<int> zb;     // per lockstep group its parts - 1 z bounds (empty: equal parts)
+  std::vector<int> l0, l1; // per block: its leftover slice
+  std::vector<int> odd;    // per block: the slice's march direction bit
+};
+X3PlanInfo stencil7x3_plan(const Dim3 &size, bool jacobi, const StencilTune &tune, int slots = 256);
 // dst(region) = stencil(src) for one quantity of one LocalDomain. `region` is in global coordinates and must lie in
 // the domain's compute region; face radii must be >= 1. `currIsSrc` selects curr->next (true) or next->curr.
 // With `fwd`, region must be the whole compute region and the output is also forwarded into the receivers' halos.

@@ -708,6 +708,24 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("dd"), py::arg("domain"), py::arg("qi"), py::arg("region"), py::arg("kind"), py::arg("spheres"),
         py::arg("stream"), py::arg("tune"), py::call_guard<py::gil_scoped_release>());
+  py::class_<X3PlanInfo>(m, "X3PlanInfo")
+      .def_readonly("parts", &X3PlanInfo::parts)
+      .def_readonly("blocks", &X3PlanInfo::blocks)
+      .def_readonly("groups", &X3PlanInfo::groups)
+      .def_readonly("lockstep_groups", &X3PlanInfo::lockstepGroups)
+      .def_readonly("rounds", &X3PlanInfo::rounds)
+      .def_readonly("tabled", &X3PlanInfo::tabled)
+      .def_readonly("steps", &X3PlanInfo::steps)
+      .def_readonly("zb", &X3PlanInfo::zb)
+      .def_readonly("l0", &X3PlanInfo::l0)
+      .def_readonly("l1", &X3PlanInfo::l1)
+      .def_readonly("odd", &X3PlanInfo::odd);
+  m.def(
+      "stencil7x3_plan",
+      [](py::handle size, bool jacobi, py::object tune, int slots) {
+        return stencil7x3_plan(to_dim3(size), jacobi, tune.is_none() ? StencilTune() : tune.cast<StencilTune>(), slots);
+      },
+      py::arg("size"), py::arg("jacobi"), py::arg("tune") = py::none(), py::arg("slots") = 256);
   m.def(
       "x2_lockstep_schedule",
       [](int64_t slots, int64_t cols, int64_t nz) {

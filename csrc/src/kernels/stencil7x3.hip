@@ -944,46 +944,14 @@ bool stencil7x3_supported(const LocalDomain &dom, int64_t qi, const Rect3 &regio
          (dom.pitch(qi).x * es) % 16 == 0;
 }
 
-template <typename T, int KIND, bool XH>
-static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
-                       const StencilTune &tune) {
-  constexpr int NW = 12, YO = NW - 6;
-  StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
-  a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
-  a.nt = tune.nontemporal ? 1 : 0;
-  a.wrapm = tune.wrap & 7;
-  // an axis read from its halos: no periodic shift (the kernel's row / plane wrap adds / subtracts wn)
-  if (!(a.wrapm & 2)) a.wn[1] = 0;
-  if (!(a.wrapm & 4)) a.wn[2] = 0;
-  a.x0 = a.lox;
-  a.remap = tune.xcdRemap ? 1 : 0;
-  a.sphchunk = tune.x3sphchunk ? 1 : 0;
-  a.sphr = int(sph.radius);
-  const int nx = a.hix - a.lox, ny = a.hiy - a.loy, nz = a.hiz - a.loz;
-  a.gx = XH ? int(nx / x3_column_cells(int64_t(sizeof(T)))) : 1;
-  a.gy = (ny + YO - 1) / YO;
-  const void *kern = XH ? (const void *)stencil7x3_xh_kernel<T, KIND> : x3_wrap_kernel_ptr<T, KIND>();
-  const int64_t cols = int64_t(a.gx) * a.gy;
-  const int64_t resident = x3_resident_blocks(kern, 64 * NW);
-  // CUs left to the transport kernels running beside the sweep (pipelined triples: the gated exchange)
-  int cus = 256;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dom.gpu()) != hipSuccess) cus = 256;
-  const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
-  const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
-  if (tune.publish) {
-    a.pub = reinterpret_cast<unsigned long long *>(tune.publish);
-    a.pubLo = a.loz + tune.publishDepth;
-    a.pubHi = a.hiz - tune.publishDepth;
-    a.flip = 0; // fixed march directions (x3_segments)
-  }
-  a.seg = 1;
-  uint32_t blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 24)));
+// the lockstep schedule of a triple sweep over cols row groups (columns) of nz planes with `slots` resident blocks
+static X2Schedule x3_schedule(int64_t cols, int64_t nz, int64_t slots, const StencilTune &tune) {
   X2Schedule ls = x2_lockstep_schedule(slots, cols, nz);
   if (tune.x3sched == 1) {
     // lockstep over as many row groups as possible: P parts of cm = min(cols, slots / P) columns, the leftover columns
-    // spread over every block as short second segments; P minimises the steps of one block (each segment runs 4
-    // warm-up steps). 512^3: 86 row groups -> P = 3 over 85 groups (255 blocks) + one leftover group, where the pairs'
-    // quarters leave 22 groups to unsynchronised second segments (FETCH 1.38x the field, profiles/r5/d)
+    // as second segments; P minimises the steps of one block (each segment runs 4 warm-up steps). A first guess:
+    // x3_plan refines P with the leftover plans (512^3: Jacobi P = 4 over 64 groups + a lockstep phase of the 22
+    // others, Astaroth P = 3 over 85 + one 2-row group in slices)
     ls = X2Schedule();
     double best = 1e30;
     for (int64_t P = 2; P <= 8; ++P) {
@@ -1019,6 +987,104 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
         }
       }
   }
+  return ls;
+}
+
+struct X3Plan {
+  int P;
+  uint32_t blocks;
+  ZPartBounds b;
+  double steps; // estimated steps of the longest block
+};
+// Plans a lockstep (seg 2) triple sweep of a.zparts parts over `blocks` blocks: sphere-weighted z-part bounds (Jacobi)
+// and the leftover groups' second segments (StencilTune::x3left); with x3left != 0, x3sched 1 and no fixed x3parts, P
+// too: the least estimated steps of the longest block over P = 2 .. 8 and both leftover plans
+template <typename T>
+static X3Plan x3_plan(const StencilArgs<T> &a, bool jac, int64_t cols, int64_t slots, uint32_t blocks,
+                      const StencilTune &tune) {
+  constexpr int NW = 12, YO = NW - 6;
+  constexpr double kUnsync = 1.2; // a step of an unsynchronised slice vs a lockstep step (profiles/r6/r6ab)
+  const int64_t nz = a.hiz - a.loz;
+  const float w = jac ? tune.x3sphw : 0.f;
+  auto plan = [&](int P, int64_t nbP, ZPartBounds &b) -> double {
+    b = ZPartBounds{};
+    const int64_t cm = nbP / P;
+    if (jac) sphere_part_bounds(b, a, std::min<int64_t>(cm, a.gy), P, NW, YO, 3, w);
+    const int mode = tune.x3left;
+    ZPartBounds bg = b, bl = b;
+    const double tg = mode == 1 || mode == 3
+                          ? balance_leftover(bg, a, nbP, cm, P, cols, a.gy, NW, YO, 3, w, 4, mode == 3 ? kUnsync : 1.0)
+                          : -1;
+    const double tl = mode == 2 || mode == 3 ? lockstep_leftover(bl, a, nbP, cm, P, cols, a.gy, NW, YO, 3, w, 4, 16) : -1;
+    if (tl >= 0 && (tg < 0 || tl <= tg)) {
+      b = bl;
+      return tl;
+    }
+    if (tg >= 0) {
+      b = bg;
+      return tg;
+    }
+    const std::vector<double> mc = lockstep_part_costs(b, a, cm, P, a.gy, NW, YO, 3, w, 4);
+    const double left = cols > cm ? double((cols - cm) * nz) * kUnsync / double(nbP) + 4 : 0;
+    return *std::max_element(mc.begin(), mc.end()) + left;
+  };
+  X3Plan pl{a.zparts, blocks, ZPartBounds{}, 0};
+  if (tune.x3sched == 1 && tune.x3parts <= 0 && tune.x3left != 0) {
+    double best = -1;
+    // spheres: only parts the host can weight (P <= kZPartMaxParts); unweighted parts leave the sphere planes to one
+    // or two parts (P = 7 with a lockstep second phase: 297 vs 228 us per 512^3 triple, profiles/r6/r6ac)
+    const bool sph = jac && a.r1sq > 0 && w > 0;
+    for (int P = 2; P <= (sph ? kZPartMaxParts : 8); ++P) {
+      const int64_t cm = std::min<int64_t>(cols, slots / P);
+      if (cm < 1 || nz / P < 16) continue;
+      ZPartBounds b;
+      const double t = plan(P, P * cm, b);
+      if (best < 0 || t < best - 1e-9) {
+        best = t;
+        pl = X3Plan{P, uint32_t(P * cm), b, t};
+      }
+    }
+  } else {
+    pl.steps = plan(a.zparts, int64_t(blocks), pl.b);
+  }
+  return pl;
+}
+
+template <typename T, int KIND, bool XH>
+static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, const Spheres &sph, hipStream_t stream,
+                       const StencilTune &tune) {
+  constexpr int NW = 12, YO = NW - 6;
+  StencilArgs<T> a = make_args<T>(dom, qi, region, KIND == 0 ? StencilKind::Jacobi : StencilKind::Astaroth, sph);
+  a.flip = tune.alternateZ ? (dom.parity() & 1) : 0;
+  a.nt = tune.nontemporal ? 1 : 0;
+  a.wrapm = tune.wrap & 7;
+  // an axis read from its halos: no periodic shift (the kernel's row / plane wrap adds / subtracts wn)
+  if (!(a.wrapm & 2)) a.wn[1] = 0;
+  if (!(a.wrapm & 4)) a.wn[2] = 0;
+  a.x0 = a.lox;
+  a.remap = tune.xcdRemap ? 1 : 0;
+  a.sphchunk = tune.x3sphchunk ? 1 : 0;
+  a.sphr = int(sph.radius);
+  const int nx = a.hix - a.lox, ny = a.hiy - a.loy, nz = a.hiz - a.loz;
+  a.gx = XH ? int(nx / x3_column_cells(int64_t(sizeof(T)))) : 1;
+  a.gy = (ny + YO - 1) / YO;
+  const void *kern = XH ? (const void *)stencil7x3_xh_kernel<T, KIND> : x3_wrap_kernel_ptr<T, KIND>();
+  const int64_t cols = int64_t(a.gx) * a.gy;
+  const int64_t resident = x3_resident_blocks(kern, 64 * NW);
+  // CUs left to the transport kernels running beside the sweep (pipelined triples: the gated exchange)
+  int cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dom.gpu()) != hipSuccess) cus = 256;
+  const int64_t perCU = std::max<int64_t>(1, resident / std::max(1, cus));
+  const int64_t slots = std::max<int64_t>(perCU, resident - perCU * std::min(tune.reserveCUs, cus / 2));
+  if (tune.publish) {
+    a.pub = reinterpret_cast<unsigned long long *>(tune.publish);
+    a.pubLo = a.loz + tune.publishDepth;
+    a.pubHi = a.hiz - tune.publishDepth;
+    a.flip = 0; // fixed march directions (x3_segments)
+  }
+  a.seg = 1;
+  uint32_t blocks = uint32_t(std::max<int64_t>(1, std::min<int64_t>(slots, cols * nz / 24)));
+  const X2Schedule ls = x3_schedule(cols, nz, slots, tune);
   if (tune.x2lockstep && ls.parts > 0) {
     a.seg = ls.rounds > 1 ? 3 : 2;
     a.zparts = ls.parts;
@@ -1026,73 +1092,20 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     blocks = uint32_t(ls.blocks);
   }
   // Lockstep parts (seg 2): the z-part bounds (sphere-weighted for Jacobi), the leftover groups' second segments
-  // (StencilTune::x3left) and, with the cost model's P, the number of parts are planned per shape on the host and
-  // cached (host work of a few ms would otherwise precede every un-captured launch). Auto P: the least estimated
-  // steps of the longest block over P = 2 .. 8 and both leftover plans.
+  // (StencilTune::x3left) and, with the cost model's P, the number of parts are planned per shape on the host
+  // (x3_plan) and cached (host work of a few ms would otherwise precede every un-captured launch)
   ZPartBounds zb{};
   if (a.seg == 2) {
-    struct Plan {
-      int P;
-      uint32_t blocks;
-      ZPartBounds b;
-    };
-    static std::map<std::vector<int64_t>, Plan> cache;
+    static std::map<std::vector<int64_t>, X3Plan> cache;
     static std::mutex mu;
-    const float w = KIND == 0 ? tune.x3sphw : 0.f;
     int32_t wbits = 0;
-    std::memcpy(&wbits, &w, sizeof(w));
-    const bool autoP = tune.x3sched == 1 && tune.x3parts <= 0 && tune.x3left != 0;
-    const std::vector<int64_t> key{KIND,  a.loy,    a.hiy, a.loz,        a.hiz,       a.hy,         a.cy,
-                                   a.hz,  a.cz,     a.r1sq, int64_t(blocks), a.zparts, cols,        a.gy,
-                                   wbits, tune.x3left, autoP, slots};
+    std::memcpy(&wbits, &tune.x3sphw, sizeof(wbits));
+    const std::vector<int64_t> key{KIND, a.loy,  a.hiy, a.loz, a.hiz,          a.hy,        a.cy,
+                                   a.hz, a.cz,   a.r1sq, int64_t(blocks), a.zparts, cols, a.gy,
+                                   wbits, tune.x3left, tune.x3sched, tune.x3parts, slots};
     std::lock_guard<std::mutex> lk(mu);
     auto it = cache.find(key);
-    if (it == cache.end()) {
-      constexpr double kUnsync = 1.2; // a step of an unsynchronised slice vs a lockstep step (profiles/r6/r6ab)
-      auto plan = [&](int P, int64_t nbP, ZPartBounds &b) -> double {
-        b = ZPartBounds{};
-        const int64_t cm = nbP / P;
-        if (KIND == 0) sphere_part_bounds(b, a, std::min<int64_t>(cm, a.gy), P, NW, YO, 3, w);
-        const int mode = tune.x3left;
-        ZPartBounds bg = b, bl = b;
-        const double tg = mode == 1 || mode == 3
-                              ? balance_leftover(bg, a, nbP, cm, P, cols, a.gy, NW, YO, 3, w, 4, mode == 3 ? kUnsync : 1.0)
-                              : -1;
-        const double tl = mode == 2 || mode == 3 ? lockstep_leftover(bl, a, nbP, cm, P, cols, a.gy, NW, YO, 3, w, 4, 16)
-                                                 : -1;
-        if (tl >= 0 && (tg < 0 || tl <= tg)) {
-          b = bl;
-          return tl;
-        }
-        if (tg >= 0) {
-          b = bg;
-          return tg;
-        }
-        const std::vector<double> mc = lockstep_part_costs(b, a, cm, P, a.gy, NW, YO, 3, w, 4);
-        const double left = cols > cm ? double((cols - cm) * nz) * kUnsync / double(nbP) + 4 : 0;
-        return *std::max_element(mc.begin(), mc.end()) + left;
-      };
-      Plan pl{a.zparts, blocks, ZPartBounds{}};
-      if (autoP) {
-        double best = -1;
-        // spheres: only parts the host can weight (P <= kZPartMaxParts); unweighted parts leave the sphere planes
-        // to one or two parts (P = 7 with a lockstep second phase: 297 vs 228 us per 512^3 triple, profiles/r6/r6ac)
-        const bool sph = KIND == 0 && a.r1sq > 0 && w > 0;
-        for (int P = 2; P <= (sph ? kZPartMaxParts : 8); ++P) {
-          const int64_t cm = std::min<int64_t>(cols, slots / P);
-          if (cm < 1 || nz / P < 16) continue;
-          ZPartBounds b;
-          const double t = plan(P, P * cm, b);
-          if (best < 0 || t < best - 1e-9) {
-            best = t;
-            pl = Plan{P, uint32_t(P * cm), b};
-          }
-        }
-      } else {
-        (void)plan(a.zparts, int64_t(blocks), pl.b);
-      }
-      it = cache.emplace(key, pl).first;
-    }
+    if (it == cache.end()) it = cache.emplace(key, x3_plan(a, KIND == 0, cols, slots, blocks, tune)).first;
     a.zparts = it->second.P;
     blocks = it->second.blocks;
     zb = it->second.b;
@@ -1106,6 +1119,51 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   else
     hipLaunchKernelGGL((stencil7x3_wrap_kernel<KIND>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   HIP_CHECK(hipGetLastError());
+}
+
+X3PlanInfo stencil7x3_plan(const Dim3 &size, bool jacobi, const StencilTune &tune, int slots) {
+  constexpr int YO = 6;
+  StencilArgs<float> a{};
+  a.hix = int(size.x);
+  a.hiy = int(size.y);
+  a.hiz = int(size.z);
+  if (jacobi) {
+    const Spheres s = Spheres::jacobi(Rect3(Dim3(0, 0, 0), size));
+    a.hx = int(s.hot.x);
+    a.hy = int(s.hot.y);
+    a.hz = int(s.hot.z);
+    a.cx = int(s.cold.x);
+    a.cy = int(s.cold.y);
+    a.cz = int(s.cold.z);
+    a.r1sq = int((s.radius + 1) * (s.radius + 1));
+  }
+  a.gx = 1;
+  a.gy = int((size.y + YO - 1) / YO);
+  const int64_t cols = a.gy, nz = size.z;
+  X3PlanInfo r;
+  r.groups = int(cols);
+  const X2Schedule ls = x3_schedule(cols, nz, slots, tune);
+  r.parts = ls.parts;
+  r.blocks = int(ls.blocks);
+  r.rounds = ls.rounds;
+  if (!tune.x2lockstep || ls.parts <= 0 || ls.rounds > 1) return r;
+  a.zparts = ls.parts;
+  const X3Plan pl = x3_plan(a, jacobi, cols, slots, uint32_t(ls.blocks), tune);
+  r.parts = pl.P;
+  r.blocks = int(pl.blocks);
+  r.lockstepGroups = int(pl.blocks) / pl.P;
+  r.steps = pl.steps;
+  r.tabled = pl.b.lon != 0;
+  if (pl.b.on)
+    for (int g = 0; g < std::min<int>(r.lockstepGroups, kZPartMaxCols); ++g)
+      for (int q = 0; q + 1 < pl.P; ++q) r.zb.push_back(pl.b.zb[g][q]);
+  if (r.tabled)
+    for (uint32_t lb = 0; lb < pl.blocks; ++lb) {
+      r.l0.push_back(pl.b.l0[lb]);
+      r.l1.push_back(pl.b.l1[lb]);
+      r.odd.push_back(int((pl.b.ldir[lb / 32] >> (lb % 32)) & 1));
+    }
+  return r;
 }
 
 bool stencil7x3_apply(const LocalDomain &dom, int64_t qi, const Rect3 &region, StencilKind kind, const Spheres &sph,
