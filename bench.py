@@ -424,6 +424,9 @@ def build_args(argv=None):
                          "Colocated -> Rccl -> Staged until every halo arrives correctly")
     ap.add_argument("--tune-steps", type=int, default=8,
                     help="steps per timed round of the transport / overlap choice (N > 1; 0 = no choice)")
+    ap.add_argument("--schedule-rounds", type=int, default=3,
+                    help="interleaved timing rounds of the fused-triple schedule candidates (sphere weight, leftover "
+                         "plan) before the timed loop; 0 = the StencilTune defaults")
     ap.add_argument("--tune-budget", type=float, default=150.0,
                     help="seconds of warm-up tuning (transport + overlap choice, agreed over ranks): once spent, the "
                          "remaining candidates are skipped and the fastest timed so far is kept (config.phases_s)")
@@ -753,6 +756,42 @@ def main(argv=None):
             overlap_tuned["skipped_by_budget"] = [f"m{c[0]}_r{c[1]}_{c[2]}" for c in over]
         ph.mark("overlap_warmup", t_ph)
 
+    # Fused-triple schedule chosen by measurement: the host plan's step estimate (sphere weight, leftover plan) is a
+    # model; each candidate is recorded (prepare) and timed over whole 18-step blocks, best of --schedule-rounds
+    # interleaved rounds, max over ranks (the same choice on every rank). Launch geometry only: every candidate is
+    # bitwise the same computation. Bounded by --tune-budget.
+    schedule_tuned = None
+    t_ph = time.perf_counter()
+    if args.tune_steps > 0 and args.schedule_rounds > 0 and model.temporal_triples() and not args.cpu:
+        scands = [(0.45, 3), (0.3, 3), (0.6, 3), (0.6, 1), (0.45, 2)]
+        best, over = {}, []
+        for _ in range(args.schedule_rounds):
+            for c in scands:
+                if ph.tuning_spent(env) >= args.tune_budget:
+                    if c not in best and c not in over:
+                        over.append(c)
+                    continue
+                model.set_triple_schedule(c[0], c[1], 0)
+                model.prepare([18])
+                model.run(18)
+                model.synchronize()
+                best[c] = min(best.get(c, float("inf")), timed_run(model, 18))
+        choice = min(best, key=best.get) if best else scands[0]
+        model.set_triple_schedule(choice[0], choice[1], 0)
+        model.prepare([args.steps])
+        model.run(args.warmup)
+        model.synchronize()
+        env.barrier()
+        tune.x3sphw, tune.x3left = choice
+        schedule_tuned = {"x3sphw": choice[0], "x3left": choice[1],
+                          **{f"sphw{c[0]}_left{c[1]}_ms": round(v, 4) for c, v in best.items()}}
+        if over:
+            schedule_tuned["skipped_by_budget"] = [f"sphw{c[0]}_left{c[1]}" for c in over]
+        if rank == 0:
+            print(f"[bench] triple schedule {choice}: " + ", ".join(f"{c}: {v:.4f}" for c, v in best.items()),
+                  file=sys.stderr, flush=True)
+        ph.mark("schedule_warmup", t_ph)
+
     # ---- the timed loop: exactly --steps steps, bracketed by a barrier + device synchronize on both sides ----
     env.barrier()
     t0 = time.perf_counter()
@@ -782,6 +821,7 @@ def main(argv=None):
     model_cfg = {
         "decomposition": f"{pdim.x}x{pdim.y}x{pdim.z}", "methods": st.methods_to_string(methods), "preflight": preflight,
         "overlap": model.overlapping(), "overlap_mode": model.overlap_mode(), "overlap_tuned": overlap_tuned,
+        "schedule_tuned": schedule_tuned,
         "transport_tuned": transport_tuned, "interior_align": args.interior_align,
         "shared_halo_line": args.shared_halo_line == 1,
         "temporal": 3 if model.temporal_triples() else (2 if model.temporal_blocking() else 1),

@@ -127,6 +127,9 @@ public:
   bool can_pipeline_triples() const { return pipeOk_ && triplesOk_; }
   // CUs the overlapped sweeps leave to the transport kernels (StencilTune::x2reserve); synchronizes first
   void set_comm_reserve(int cus);
+  // the fused triples' lockstep schedule (StencilTune x3sphw / x3left / x3parts: launch geometry only, results are
+  // bitwise the same); synchronizes and drops the recorded hipGraphs (run() / prepare() record them again)
+  void set_triple_schedule(float sphw, int left, int parts);
   int comm_reserve() const { return cfg_.tune.x2reserve; }
   bool local_interior_steps() const { return localSteps_; } // overlapped single steps on get_local_interior
   bool forwarding() const { return forward_; }
@@ -181,6 +184,7 @@ private:
   };
   std::map<std::pair<int, int>, RunGraph> runGraph_; // (steps, starting parity) -> a whole run(steps)
   void capture_run(int n);                           // runGraph_[{n, current parity}] (no work is run)
+  void drop_graphs();
   bool pair_ok() const { return pairs_; }
   int64_t steps_ = 0;
 };

@@ -825,6 +825,8 @@ PYBIND11_MODULE(_C, m) {
       .def("can_pipeline", &StencilModel::can_pipeline)
       .def("can_pipeline_triples", &StencilModel::can_pipeline_triples)
       .def("set_comm_reserve", &StencilModel::set_comm_reserve, py::call_guard<py::gil_scoped_release>())
+      .def("set_triple_schedule", &StencilModel::set_triple_schedule, py::arg("sphw"), py::arg("left"),
+           py::arg("parts"), py::call_guard<py::gil_scoped_release>())
       .def("comm_reserve", &StencilModel::comm_reserve)
       .def("set_overlap", &StencilModel::set_overlap, py::call_guard<py::gil_scoped_release>())
       .def("local_interior_steps", &StencilModel::local_interior_steps)

@@ -668,6 +668,33 @@ void StencilModel::set_comm_reserve(int cus) {
   if (confinedSelf_ && overlap_) dd_->set_translate_max_blocks(cus);
 }
 
+void StencilModel::set_triple_schedule(float sphw, int left, int parts) {
+  STENCIL_REQUIRE(left >= 0 && left <= 3 && parts >= 0 && parts <= 8 && sphw >= 0, "triple schedule");
+  synchronize();
+  for (StencilTune *t : {&cfg_.tune, &pairTune_, &stepTune_}) {
+    t->x3sphw = sphw;
+    t->x3left = left;
+    t->x3parts = parts;
+  }
+  drop_graphs();
+}
+
+void StencilModel::drop_graphs() {
+  for (auto &g : graphExec_)
+    if (g) {
+      HIP_CHECK(hipGraphExecDestroy(g));
+      g = nullptr;
+    }
+  for (auto &g : graphBlock_)
+    if (g) {
+      HIP_CHECK(hipGraphExecDestroy(g));
+      g = nullptr;
+    }
+  for (auto &kv : runGraph_)
+    if (kv.second.exec) HIP_CHECK(hipGraphExecDestroy(kv.second.exec));
+  runGraph_.clear();
+}
+
 void StencilModel::synchronize() {
   // the compute streams join the exchange (wait_exchange / exteriorDone_ / the exchange enqueued on them), so a
   // stalled peer stalls them too: DistributedDomain polls them with its watchdog instead of blocking on them first

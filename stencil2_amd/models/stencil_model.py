@@ -122,6 +122,11 @@ class StencilModel:
         """CUs the overlapped sweeps leave to the transport kernels (StencilTune.x2reserve)."""
         self._m.set_comm_reserve(int(cus))
 
+    def set_triple_schedule(self, sphw: float, left: int, parts: int = 0):
+        """The fused triples' lockstep schedule (StencilTune x3sphw / x3left / x3parts; results are bitwise the same).
+        Synchronizes and drops the recorded hipGraphs: prepare() again before a timed loop."""
+        self._m.set_triple_schedule(float(sphw), int(left), int(parts))
+
     def comm_reserve(self) -> int:
         return self._m.comm_reserve()
 
