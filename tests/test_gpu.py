@@ -607,6 +607,25 @@ def test_prepare_whole_run_graphs(st, temporal, size):
     assert torch.equal(_gather(m), u)
 
 
+def test_set_triple_schedule_keeps_results(st):
+    """set_triple_schedule (bench.py's schedule choice) drops the recorded graphs and re-plans the lockstep launch:
+    every schedule (sphere weight, leftover plan, parts) stays bitwise equal to the oracle across switches."""
+    m = st.Jacobi3D((512, 120, 116), gpus=[0], temporal=3)
+    m.init()
+    assert m.temporal_triples()
+    u = _gather(m)
+    m.prepare([18])
+    for sphw, left, parts in ((0.45, 3, 0), (0.3, 1, 0), (0.6, 2, 4), (0.0, 0, 3), (0.45, 2, 0)):
+        m.set_triple_schedule(sphw, left, parts)
+        m.prepare([18])
+        for n in (18, 5):
+            m.run(n)
+            for _ in range(n):
+                u = jacobi_step_reference(u)
+    m.synchronize()
+    assert torch.equal(_gather(m), u)
+
+
 def test_temporal2_spheres_at_periodic_face_fall_back(st):
     """Spheres that reach a periodic face (radius x/10 on a thin y/z grid) make the fused pair's halo-ring step
     differ from the neighbour's: the model runs single steps there, still equal to the oracle."""
