@@ -124,8 +124,9 @@ __device__ __forceinline__ double x3_row_prev(double v) {
   return __longlong_as_double(int64_t(uint32_t(lo)) | (int64_t(hi) << 32));
 }
 
-// Columns with x halos (the XH form): every x-neighbour beyond a column end comes from the exchanged halos
-template <typename T, int KIND>
+// Columns with x halos (the XH form): every x-neighbour beyond a column end comes from the exchanged halos. BIG:
+// fields of 4 GiB or more (a buffer resource per plane); else one resource over the field, the plane in soffset
+template <typename T, int KIND, bool BIG>
 __global__ __launch_bounds__(64 * 12, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
   constexpr bool XH = true;
@@ -228,77 +229,60 @@ stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
         const uint32_t edgeoff =
             uint32_t((ywrap(ey) * int64_t(a.px) + (eside ? xcol + CW - 1 : xcol - 3)) * int64_t(sizeof(T)));
 
-        // spheres (Jacobi): the planes P of this row that cross the hot / cold sphere form two intervals
-        // |P - c.z| <= h (h * h < r1sq - dy^2), computed once per segment; per-cell tests only on those planes
+        // spheres (Jacobi): a cell (x, y, P) is in the hot sphere iff (x - hx)^2 < Dh = yh - (P - hz)^2 with
+        // yh = r1sq - (y - hy)^2 (per segment), in the cold one likewise; the row-plane has no sphere cell when both
+        // bounds are <= 0 (r1sq = 0: never). Two live scalars per row instead of plane intervals + centres (SGPR
+        // pressure: the Jacobi kernels spilled 100-121 SGPRs to VGPR lanes)
+        const int yh = a.r1sq - (y - a.hy) * (y - a.hy), yc = a.r1sq - (y - a.cy) * (y - a.cy);
         struct RowSph {
-          int dh, dc;
+          int Dh, Dc;
           bool hit;
         };
-        auto isqrt_below = [](int d) -> int { // largest h >= 0 with h * h < d (d > 0), exact
-          int h = int(__builtin_sqrtf(float(d - 1)));
-          while (h > 0 && h * h > d - 1) --h;
-          while ((h + 1) * (h + 1) <= d - 1) ++h;
-          return h;
-        };
-        int hzlo = 1, hzhi = 0, czlo = 1, czhi = 0; // empty intervals
-        if (KIND == 0 && a.r1sq > 0 && !EDGE) {
-          const int dyh = a.r1sq - (y - a.hy) * (y - a.hy), dyc = a.r1sq - (y - a.cy) * (y - a.cy);
-          if (dyh > 0) {
-            const int h = isqrt_below(dyh);
-            hzlo = a.hz - h;
-            hzhi = a.hz + h;
-          }
-          if (dyc > 0) {
-            const int h = isqrt_below(dyc);
-            czlo = a.cz - h;
-            czhi = a.cz + h;
-          }
-        }
         auto row_sph = [&](int P) -> RowSph {
           RowSph r{0, 0, false};
-          if (KIND == 0) {
-            r.hit = (P >= hzlo && P <= hzhi) || (P >= czlo && P <= czhi);
-            r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
-            r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
+          if (KIND == 0 && !EDGE) {
+            r.Dh = yh - (P - a.hz) * (P - a.hz);
+            r.Dc = yc - (P - a.cz) * (P - a.cz);
+            r.hit = max(r.Dh, r.Dc) > 0;
           }
           return r;
         };
-        // (x - c)^2 + d < r1sq <=> (x - c)^2 < r1sq - d: the row's bound is one scalar per sphere, the per-cell squared
-        // distances loop invariants, so a cell costs a compare and a select per sphere. Cheaper variants measured
-        // slower (an x interval per row, tests only on the chunk the sphere reaches; profiles/r5/ai, aj, ap); the
-        // blocks of sphere-crossing rows are evened out by sphere-weighted z parts (x3sphw, profiles/r5/ao)
+        // (x - c)^2 < D: the row-plane's bound is one scalar per sphere, the per-cell squared distances loop
+        // invariants, so a cell costs a compare and a select per sphere; the blocks of sphere-crossing rows are
+        // evened out by sphere-weighted z parts and the leftover plan (x3sphw, x3left)
         auto sph_fix = [&](int dh, int dc, int x, T v) -> T {
           const bool hot = (x - a.hx) * (x - a.hx) < a.r1sq - dh;
           const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - dc;
           return hot ? T(1) : (cold ? T(0) : v);
         };
-        // the chunks (cells xcol + h CS .. + CS - 1 over the wave) a sphere's x range can reach (block-uniform): the
-        // 512^3 hot sphere (x 119-221) only touches chunk 0, the cold one (290-392) only chunk 1, so a sphere row tests
-        // half the cells (StencilTune.x3sphchunk; 0: every chunk for both spheres)
-        bool hotc[H], coldc[H];
+        // the chunks (cells xcol + h CS .. + CS - 1 over the wave) a sphere's x range can reach: the 512^3 hot sphere
+        // (x 119-221) only touches chunk 0, the cold one (290-392) only chunk 1, so a sphere row tests half the cells
+        // (StencilTune.x3sphchunk; 0: every chunk for both spheres). Bits in one SGPR (2h: cold on chunk h, 2h + 1:
+        // hot), not booleans (lane masks)
+        int sphm = 0;
 #pragma unroll
         for (int h = 0; h < H; ++h) {
           const int lo = xcol + h * CS, hi = lo + CS - 1;
-          hotc[h] = !a.sphchunk || (a.hx - a.sphr <= hi && a.hx + a.sphr >= lo);
-          coldc[h] = !a.sphchunk || (a.cx - a.sphr <= hi && a.cx + a.sphr >= lo);
+          sphm |= int(!a.sphchunk || (a.cx - a.sphr <= hi && a.cx + a.sphr >= lo)) << (2 * h);
+          sphm |= int(!a.sphchunk || (a.hx - a.sphr <= hi && a.hx + a.sphr >= lo)) << (2 * h + 1);
         }
+        sphm = __builtin_amdgcn_readfirstlane(sphm);
         auto sphere_row = [&](const RowSph &rs, NV(&o)[H]) {
           if (KIND == 0 && rs.hit) {
-            const int Dh = a.r1sq - rs.dh, Dc = a.r1sq - rs.dc;
             // cold first, then hot: the hot sphere wins where both hold, as in the single step
 #pragma unroll
             for (int h = 0; h < H; ++h) {
-              if (coldc[h])
+              if ((sphm >> (2 * h)) & 1)
 #pragma unroll
                 for (int k = 0; k < V; ++k) {
                   const int x = xb + h * CS + k;
-                  o[h][k] = (x - a.cx) * (x - a.cx) < Dc ? T(0) : o[h][k];
+                  o[h][k] = (x - a.cx) * (x - a.cx) < rs.Dc ? T(0) : o[h][k];
                 }
-              if (hotc[h])
+              if ((sphm >> (2 * h + 1)) & 1)
 #pragma unroll
                 for (int k = 0; k < V; ++k) {
                   const int x = xb + h * CS + k;
-                  o[h][k] = (x - a.hx) * (x - a.hx) < Dh ? T(1) : o[h][k];
+                  o[h][k] = (x - a.hx) * (x - a.hx) < rs.Dh ? T(1) : o[h][k];
                 }
             }
           }
@@ -340,21 +324,20 @@ stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
           // and the compiler waited for every outstanding memory op (s_waitcnt vmcnt(0)) before each step's loads,
           // the previous step's stores included
           auto load_row = [&](int zz, int k) {
-            // a raw buffer over the plane (its base in SGPRs: fields beyond 4 GiB, fp64 1024^3), the row offset a
-            // per-segment constant VGPR
-            // (whole rows: one resource over the field, the plane offset in soffset - fields below 4 GiB)
-            const uint32_t po = XH ? 0u : uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
+            // BIG: a raw buffer over the plane (its base in SGPRs: fields beyond 4 GiB, fp64 1024^3); else one
+            // resource over the field, the plane offset in soffset. The row offset a per-segment constant VGPR
+            const uint32_t po = BIG ? 0u : uint32_t(zcl(zz)) * uint32_t(a.pxy) * uint32_t(sizeof(T));
             const __amdgpu_buffer_rsrc_t rs =
-                XH ? __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(a.src + int64_t(zcl(zz)) * a.pxy), 0, -1,
-                                                       0x00020000)
-                   : srcRsrc;
+                BIG ? __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(a.src + int64_t(zcl(zz)) * a.pxy), 0, -1,
+                                                        0x00020000)
+                    : srcRsrc;
 #pragma unroll
             for (int h = 0; h < H; ++h) C[k][h] = x3_load16<NV>(rs, rowoff + uint32_t(h * CS * int(sizeof(T))), po);
             if constexpr (EDGE) {
               if constexpr (sizeof(T) == 4) {
-                E[k] = x3_load16<E4>(rs, edgeoff, 0);
+                E[k] = x3_load16<E4>(rs, edgeoff, po);
               } else {
-                const NV lo = x3_load16<NV>(rs, edgeoff, 0), hi = x3_load16<NV>(rs, edgeoff + 16, 0);
+                const NV lo = x3_load16<NV>(rs, edgeoff, po), hi = x3_load16<NV>(rs, edgeoff + 16, po);
                 E[k] = E4{lo[0], lo[1], hi[0], hi[1]};
               }
             }
@@ -1068,7 +1051,10 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   const int nx = a.hix - a.lox, ny = a.hiy - a.loy, nz = a.hiz - a.loz;
   a.gx = XH ? int(nx / x3_column_cells(int64_t(sizeof(T)))) : 1;
   a.gy = (ny + YO - 1) / YO;
-  const void *kern = XH ? (const void *)stencil7x3_xh_kernel<T, KIND> : x3_wrap_kernel_ptr<T, KIND>();
+  const bool big = dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096;
+  const void *kern = XH ? (big ? (const void *)stencil7x3_xh_kernel<T, KIND, true>
+                               : (const void *)stencil7x3_xh_kernel<T, KIND, false>)
+                        : x3_wrap_kernel_ptr<T, KIND>();
   const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x3_resident_blocks(kern, 64 * NW);
   // CUs left to the transport kernels running beside the sweep (pipelined triples: the gated exchange)
@@ -1114,10 +1100,14 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.sink = x3_sink(dom.gpu(), false);
   a.clk = reinterpret_cast<unsigned long long *>(tune.blockClock);
   STENCIL_REQUIRE(a.sink, "stencil7x3: no store sink on device " << dom.gpu() << " (stencil7x3_supported first)");
-  if constexpr (XH || !std::is_same<T, float>::value)
-    hipLaunchKernelGGL((stencil7x3_xh_kernel<T, KIND>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
-  else
+  if constexpr (XH || !std::is_same<T, float>::value) {
+    if (big)
+      hipLaunchKernelGGL((stencil7x3_xh_kernel<T, KIND, true>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+    else
+      hipLaunchKernelGGL((stencil7x3_xh_kernel<T, KIND, false>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+  } else {
     hipLaunchKernelGGL((stencil7x3_wrap_kernel<KIND>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+  }
   HIP_CHECK(hipGetLastError());
 }
 
