@@ -604,38 +604,20 @@ stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
         const uint32_t rowoff = uint32_t((yw * int64_t(a.px) + xb) * int64_t(sizeof(T)));
         const uint32_t outoff = uint32_t((y * int64_t(a.px) + xb) * int64_t(sizeof(T)));
 
-        // spheres (Jacobi): the planes P of this row that cross the hot / cold sphere form two intervals
-        // |P - c.z| <= h (h * h < r1sq - dy^2), computed once per segment; per-cell tests only on those planes
+        // spheres (Jacobi): a cell (x, y, P) is in the hot sphere iff (x - hx)^2 < Dh = yh - (P - hz)^2 with
+        // yh = r1sq - (y - hy)^2 (per segment), in the cold one likewise; the row-plane has no sphere cell when both
+        // bounds are <= 0 (r1sq = 0: never)
+        const int yh = a.r1sq - (y - a.hy) * (y - a.hy), yc = a.r1sq - (y - a.cy) * (y - a.cy);
         struct RowSph {
-          int dh, dc;
+          int Dh, Dc;
           bool hit;
         };
-        auto isqrt_below = [](int d) -> int { // largest h >= 0 with h * h < d (d > 0), exact
-          int h = int(__builtin_sqrtf(float(d - 1)));
-          while (h > 0 && h * h > d - 1) --h;
-          while ((h + 1) * (h + 1) <= d - 1) ++h;
-          return h;
-        };
-        int hzlo = 1, hzhi = 0, czlo = 1, czhi = 0; // empty intervals
-        if (KIND == 0 && a.r1sq > 0) {
-          const int dyh = a.r1sq - (y - a.hy) * (y - a.hy), dyc = a.r1sq - (y - a.cy) * (y - a.cy);
-          if (dyh > 0) {
-            const int h = isqrt_below(dyh);
-            hzlo = a.hz - h;
-            hzhi = a.hz + h;
-          }
-          if (dyc > 0) {
-            const int h = isqrt_below(dyc);
-            czlo = a.cz - h;
-            czhi = a.cz + h;
-          }
-        }
         auto row_sph = [&](int P) -> RowSph {
           RowSph r{0, 0, false};
           if (KIND == 0) {
-            r.hit = (P >= hzlo && P <= hzhi) || (P >= czlo && P <= czhi);
-            r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
-            r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
+            r.Dh = yh - (P - a.hz) * (P - a.hz);
+            r.Dc = yc - (P - a.cz) * (P - a.cz);
+            r.hit = max(r.Dh, r.Dc) > 0;
           }
           return r;
         };
@@ -646,7 +628,7 @@ stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
           if (KIND == 0 && rs.hit) {
             // (x - c)^2 + d < r1sq <=> (x - c)^2 < r1sq - d: the row's bound is one scalar per sphere, the per-cell
             // squared distances loop invariants, so a cell costs a compare and a select per sphere
-            const int Dh = a.r1sq - rs.dh, Dc = a.r1sq - rs.dc;
+            const int Dh = rs.Dh, Dc = rs.Dc;
 #pragma unroll
             for (int h = 0; h < H; ++h)
 #pragma unroll
