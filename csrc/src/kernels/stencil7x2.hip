@@ -461,8 +461,12 @@ stencil7x2_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
     return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
   };
   auto planep = [&](int zz) -> const char * { return reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy); };
+  // spheres: a cell (x, y, P) is hot iff (x - hx)^2 < Dh = sqh - (P - hz)^2, sqh = r1sq - (y - hy)^2 (per segment),
+  // cold likewise; no sphere cell in the row-plane when both are <= 0 (r1sq = 0: never). Two live scalars per row
+  // instead of the centres and r1sq (SGPR pressure: spills to VGPR lanes in the steady loop)
+  const int sqh = a.r1sq - (y - a.hy) * (y - a.hy), sqc = a.r1sq - (y - a.cy) * (y - a.cy);
   struct RowSph {
-    int dh, dc;
+    int Dh, Dc;
     bool hit;
     int hlo, hhi, clo, chi; // TL: the row's hot / cold cells are hlo <= x <= hhi / clo <= x <= chi (wave-uniform)
   };
@@ -475,15 +479,15 @@ stencil7x2_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
   };
   auto row_sph = [&](int P) -> RowSph {
     RowSph r{0, 0, false, 0, 0, 0, 0};
-    if (KIND == 0 && a.r1sq > 0) {
-      r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
-      r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
-      r.hit = r.dh < a.r1sq || r.dc < a.r1sq;
+    if (KIND == 0) {
+      r.Dh = sqh - (P - a.hz) * (P - a.hz);
+      r.Dc = sqc - (P - a.cz) * (P - a.cz);
+      r.hit = max(r.Dh, r.Dc) > 0;
       if constexpr (TL) {
-        // (x - hx)^2 + dh < r1sq  <=>  |x - hx| <= s with s * s < r1sq - dh: bounds instead of per-cell squares
+        // (x - hx)^2 < Dh  <=>  |x - hx| <= s with s * s < Dh: bounds instead of per-cell squares
         constexpr int kNone = -(1 << 24); // empty interval: never matches a cell coordinate
-        const int sh = r.dh < a.r1sq ? isqrt_below(a.r1sq - r.dh) : -1;
-        const int sc = r.dc < a.r1sq ? isqrt_below(a.r1sq - r.dc) : -1;
+        const int sh = r.Dh > 0 ? isqrt_below(r.Dh) : -1;
+        const int sc = r.Dc > 0 ? isqrt_below(r.Dc) : -1;
         r.hlo = __builtin_amdgcn_readfirstlane(sh >= 0 ? a.hx - sh : kNone);
         r.hhi = __builtin_amdgcn_readfirstlane(sh >= 0 ? a.hx + sh : kNone);
         r.clo = __builtin_amdgcn_readfirstlane(sc >= 0 ? a.cx - sc : kNone);
@@ -498,8 +502,8 @@ stencil7x2_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
       hot = unsigned(x - rs.hlo) <= unsigned(rs.hhi - rs.hlo);
       cold = unsigned(x - rs.clo) <= unsigned(rs.chi - rs.clo);
     } else {
-      hot = (x - a.hx) * (x - a.hx) < a.r1sq - rs.dh;
-      cold = (x - a.cx) * (x - a.cx) < a.r1sq - rs.dc;
+      hot = (x - a.hx) * (x - a.hx) < rs.Dh;
+      cold = (x - a.cx) * (x - a.cx) < rs.Dc;
     }
     return hot ? T(1) : (cold ? T(0) : v);
   };
@@ -788,22 +792,25 @@ __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3
     return zz < 0 ? 0 : (zz > a.rawZm1 ? a.rawZm1 : zz);
   };
   auto planep = [&](int zz) -> const char * { return reinterpret_cast<const char *>(a.src + int64_t(zcl(zz)) * a.pxy); };
+  // hot iff (x - hx)^2 < Dh = sqh - (P - hz)^2 with sqh = r1sq - (y - hy)^2, cold likewise (two live scalars per row:
+  // SGPR pressure, see stencil7x2_row_kernel)
+  const int sqh = a.r1sq - (y - a.hy) * (y - a.hy), sqc = a.r1sq - (y - a.cy) * (y - a.cy);
   struct RowSph {
-    int dh, dc;
+    int Dh, Dc;
     bool hit;
   };
   auto row_sph = [&](int P) -> RowSph {
     RowSph r{0, 0, false};
-    if (KIND == 0 && a.r1sq > 0) {
-      r.dh = (y - a.hy) * (y - a.hy) + (P - a.hz) * (P - a.hz);
-      r.dc = (y - a.cy) * (y - a.cy) + (P - a.cz) * (P - a.cz);
-      r.hit = r.dh < a.r1sq || r.dc < a.r1sq;
+    if (KIND == 0) {
+      r.Dh = sqh - (P - a.hz) * (P - a.hz);
+      r.Dc = sqc - (P - a.cz) * (P - a.cz);
+      r.hit = max(r.Dh, r.Dc) > 0;
     }
     return r;
   };
   auto fix = [&](const RowSph &rs, int x, T v) -> T {
-    const bool hot = (x - a.hx) * (x - a.hx) < a.r1sq - rs.dh;
-    const bool cold = (x - a.cx) * (x - a.cx) < a.r1sq - rs.dc;
+    const bool hot = (x - a.hx) * (x - a.hx) < rs.Dh;
+    const bool cold = (x - a.cx) * (x - a.cx) < rs.Dc;
     return hot ? T(1) : (cold ? T(0) : v);
   };
   // S of the wave's column: x-neighbours by lane rotates, eL / eR beyond the column ends
