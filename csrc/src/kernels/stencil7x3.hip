@@ -535,7 +535,7 @@ stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
 // Whole periodic rows (fp32, 512 cells, x wrapped in-kernel): x-neighbours and the wrap by DPP lane rotates of the
 // wave's own registers; the headline kernel (bench.py, one GPU). Kept apart from the XH form: sharing one body cost
 // the whole-row instance ~3 % more VALU (window register moves) and 1.2 % of steady-state time (profiles/r6/r6n)
-template <int KIND>
+template <int KIND, bool PUB>
 __global__ __launch_bounds__(64 * 12, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
   constexpr int NW = 12;     // 3 waves per SIMD (168 VGPRs), 3 x 48 KiB of LDS
@@ -575,7 +575,7 @@ stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
   auto body = [&](auto roleTag) {
     constexpr int R = decltype(roleTag)::value;
     bool odd = sg.odd;
-    const bool pubOrder = a.pub != nullptr;
+    const bool pubOrder = PUB; // boundary-plane publication (a.pub, template: no live state otherwise)
     for (int pp = 0; pp < 2; ++pp) {
       // publishing: the leftover row groups' short second segments first (their face planes would otherwise come
       // out last), the main lockstep segment in its fixed direction
@@ -763,7 +763,7 @@ stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
               for (int h = 0; h < H; ++h) cs[nbuf][w][h][lane] = C[s2][h];
             // boundary-plane publication (block-uniform, as the pairs): every wave's stores of output plane z
             // complete before the barrier, then one thread writes the L2 back (release) and counts the block's cells
-            const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
+            const bool pubStep = PUB && t >= 0 && (z < a.pubLo || z >= a.pubHi);
             if (pubStep) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (pubStep && lane == 0 && w == 0) {
@@ -828,7 +828,7 @@ stencil7x3_wrap_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
 // host side
 template <typename T, int KIND> static const void *x3_wrap_kernel_ptr() {
   if constexpr (std::is_same<T, float>::value)
-    return (const void *)stencil7x3_wrap_kernel<KIND>;
+    return (const void *)stencil7x3_wrap_kernel<KIND, false>;
   else
     return nullptr;
 }
@@ -1088,7 +1088,10 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
     else
       hipLaunchKernelGGL((stencil7x3_xh_kernel<T, KIND, false>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   } else {
-    hipLaunchKernelGGL((stencil7x3_wrap_kernel<KIND>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+    if (a.pub)
+      hipLaunchKernelGGL((stencil7x3_wrap_kernel<KIND, true>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+    else
+      hipLaunchKernelGGL((stencil7x3_wrap_kernel<KIND, false>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   }
   HIP_CHECK(hipGetLastError());
 }
