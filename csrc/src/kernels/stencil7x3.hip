@@ -126,7 +126,7 @@ __device__ __forceinline__ double x3_row_prev(double v) {
 
 // Columns with x halos (the XH form): every x-neighbour beyond a column end comes from the exchanged halos. BIG:
 // fields of 4 GiB or more (a buffer resource per plane); else one resource over the field, the plane in soffset
-template <typename T, int KIND, bool BIG>
+template <typename T, int KIND, bool BIG, bool PUB>
 __global__ __launch_bounds__(64 * 12, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
   constexpr bool XH = true;
@@ -179,7 +179,7 @@ stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
     constexpr int RM = R == 4 ? 0 : R; // levels of the wave's own row
     constexpr bool EDGE = XH && R == 4;
     bool odd = sg.odd;
-    const bool pubOrder = a.pub != nullptr;
+    const bool pubOrder = PUB; // boundary-plane publication (a.pub, template: no live state otherwise)
     const uint32_t ncols = uint32_t(a.gx) * gy;
     const int npass = XH && a.seg == 3 ? a.zrounds : 2; // rounds: XH only (many columns), fewer SGPRs elsewhere
     for (int pp = 0; pp < npass; ++pp) {
@@ -467,7 +467,7 @@ stencil7x3_xh_kernel(StencilArgs<T> a, ZPartBounds zbounds) {
             }
             // boundary-plane publication (block-uniform, as the pairs): every wave's stores of output plane z
             // complete before the barrier, then one thread writes the L2 back (release) and counts the block's cells
-            const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
+            const bool pubStep = PUB && t >= 0 && (z < a.pubLo || z >= a.pubHi);
             if (pubStep) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (pubStep && lane == 0 && w == 0) {
@@ -1034,8 +1034,8 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.gx = XH ? int(nx / x3_column_cells(int64_t(sizeof(T)))) : 1;
   a.gy = (ny + YO - 1) / YO;
   const bool big = dom.buffer_bytes(qi) >= (int64_t(1) << 32) - 4096;
-  const void *kern = XH ? (big ? (const void *)stencil7x3_xh_kernel<T, KIND, true>
-                               : (const void *)stencil7x3_xh_kernel<T, KIND, false>)
+  const void *kern = XH ? (big ? (const void *)stencil7x3_xh_kernel<T, KIND, true, false>
+                               : (const void *)stencil7x3_xh_kernel<T, KIND, false, false>)
                         : x3_wrap_kernel_ptr<T, KIND>();
   const int64_t cols = int64_t(a.gx) * a.gy;
   const int64_t resident = x3_resident_blocks(kern, 64 * NW);
@@ -1083,10 +1083,9 @@ static void apply_x3_t(const LocalDomain &dom, int64_t qi, const Rect3 &region, 
   a.clk = reinterpret_cast<unsigned long long *>(tune.blockClock);
   STENCIL_REQUIRE(a.sink, "stencil7x3: no store sink on device " << dom.gpu() << " (stencil7x3_supported first)");
   if constexpr (XH || !std::is_same<T, float>::value) {
-    if (big)
-      hipLaunchKernelGGL((stencil7x3_xh_kernel<T, KIND, true>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
-    else
-      hipLaunchKernelGGL((stencil7x3_xh_kernel<T, KIND, false>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+    auto *k = a.pub ? (big ? stencil7x3_xh_kernel<T, KIND, true, true> : stencil7x3_xh_kernel<T, KIND, false, true>)
+                    : (big ? stencil7x3_xh_kernel<T, KIND, true, false> : stencil7x3_xh_kernel<T, KIND, false, false>);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   } else {
     if (a.pub)
       hipLaunchKernelGGL((stencil7x3_wrap_kernel<KIND, true>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
