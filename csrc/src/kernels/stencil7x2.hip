@@ -383,7 +383,7 @@ __device__ __forceinline__ bool x2_pass(const StencilArgs<T> &a, const X2Segs &s
   return true;
 }
 
-template <int NW, int PF, int KIND, int H = 2, bool RAG = false, bool TL = false>
+template <int NW, int PF, int KIND, int H = 2, bool RAG = false, bool TL = false, bool PUB = false>
 __global__ __launch_bounds__(64 * NW, 3) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 stencil7x2_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
   using T = float;
@@ -675,7 +675,8 @@ stencil7x2_row_kernel(StencilArgs<float> a, ZPartBounds zbounds) {
       }
       // boundary-plane publication (block-uniform): every wave's stores of plane z complete before the barrier,
       // then one thread writes the XCD's L2 back (system-scope release) and counts the block's cells of the plane
-      const bool pubStep = a.pub != nullptr && t >= 0 && (z < a.pubLo || z >= a.pubHi);
+      // boundary-plane publication (pipelined pairs): a template parameter, no live state otherwise (SGPR spills)
+      const bool pubStep = PUB && t >= 0 && (z < a.pubLo || z >= a.pubHi);
       if (pubStep) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (pubStep && lane == 0 && w == 0) {
@@ -1302,7 +1303,11 @@ static bool apply_x2row_t(const LocalDomain &dom, int64_t qi, const Rect3 &regio
   ZPartBounds zb{};
   zb.on = 0;
   if (KIND == 0 && a.seg == 2) sphere_part_bounds(zb, a, int64_t(blocks) / a.zparts, a.zparts, NW, YO, 2, tune.x2sphw);
-  hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG, TL>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
+  if (a.pub)
+    hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG, TL, true>), dim3(blocks), dim3(64, NW), 0, stream, a,
+                       zb);
+  else
+    hipLaunchKernelGGL((stencil7x2_row_kernel<NW, PF, KIND, H, RAG, TL>), dim3(blocks), dim3(64, NW), 0, stream, a, zb);
   HIP_CHECK(hipGetLastError());
   return true;
 }
