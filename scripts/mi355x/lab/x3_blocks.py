@@ -16,19 +16,22 @@ clk = torch.zeros(1024, dtype=torch.int64, device="cuda")
 t = st.StencilTune()
 t.block_clock = clk.data_ptr()
 t.x3sphw = sphw
-Pshow = 0
+Pshow, kw = 0, {}
 for kv in sys.argv[5:]:
     k, v = kv.split("=", 1)
     if k == "P":  # the parts to print by (the host's plan may choose another P than the step-count model below)
         Pshow = int(v)
         continue
+    if k == "xh":  # x read from exchanged halos (the XH kernel), as bench.py's with-exchange model
+        kw = dict(wrap_self=not int(v), shared_halo_line=bool(int(v)))
+        continue
     cur = getattr(t, k)
     setattr(t, k, (v.lower() in ("1", "true")) if isinstance(cur, bool) else type(cur)(v))
 nz = 512
 if kind == "jacobi":
-    m = st.Jacobi3D((512, ny, nz), gpus=[0], temporal=3, tune=t, use_graph=False)
+    m = st.Jacobi3D((512, ny, nz), gpus=[0], temporal=3, tune=t, use_graph=False, **kw)
 else:
-    m = st.AstarothSim((512, ny, nz), gpus=[0], temporal=3, tune=t, quantities=1, use_graph=False)
+    m = st.AstarothSim((512, ny, nz), gpus=[0], temporal=3, tune=t, quantities=1, use_graph=False, **kw)
 m.init()
 assert m.temporal_triples()
 for i in range(warm + 1):
