@@ -86,3 +86,26 @@ def test_bench_two_lines_and_stalled_rccl_entry():
     assert tr["peer_store"]["devices_used"] == 1 and "GBps" in tr["peer_store"], tr["peer_store"]
     assert "GBps" in tr["peer_engine"], tr["peer_engine"]
     assert tr["astaroth_q8"]["decomposition"] == "1x1x1" and tr["astaroth_q8"]["GBps"] > 0
+
+
+def test_bench_triple_schedule_phase():
+    """The driver's command (512^3, fused triples): the schedule phase times every candidate (sphere weight x leftover
+    plan), keeps one of them, records the times and its wall time; --schedule-rounds 0 skips it."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["STENCIL_PLAN_FILE"] = "0"
+    base = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "5", "--exchange-iters", "4",
+            "--transport-sweep", "off", "--with-exchange", "off"]
+    r = subprocess.run(base, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    s = d["config"]["schedule_tuned"]
+    times = {k: v for k, v in s.items() if k.endswith("_ms")}
+    assert len(times) == 5 and all(v > 0 for v in times.values())
+    assert f"sphw{s['x3sphw']}_left{s['x3left']}_ms" in times and d["config"]["tune"]["x3left"] == s["x3left"]
+    assert d["config"]["phases_s"]["schedule_warmup"] > 0 and d["value"] > 0
+    r = subprocess.run(base + ["--schedule-rounds", "0"], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    assert d["config"]["schedule_tuned"] is None and "schedule_warmup" not in d["config"]["phases_s"]
