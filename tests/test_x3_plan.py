@@ -79,3 +79,27 @@ def test_headline_plans_are_pinned():
     assert not e.tabled and e.parts == 4
     # the estimate prefers the planned leftovers over equal slices
     assert j.steps < e.steps
+
+
+def test_random_shapes_and_knobs_keep_the_invariants():
+    """Random row-group counts, depths, resident-slot counts (CUs left to transports) and knobs: the planned launch
+    never exceeds the slots and any table still covers every leftover plane exactly once."""
+    import random
+    rnd = random.Random(1)
+    for _ in range(80):
+        size = (512, rnd.randint(3, 1500), rnd.randint(16, 1200))
+        jac = rnd.random() < 0.6
+        t = _tune(x3left=rnd.choice([0, 1, 2, 3]), x3parts=rnd.choice([0, 0, 0, 2, 3, 4, 5, 8]),
+                  x3sphw=rnd.choice([0.0, 0.3, 0.45, 0.6, 1.0]))
+        slots = rnd.choice([256, 248, 128, 64, 300])
+        p = _C.stencil7x3_plan(size, jac, t, slots)
+        if p.rounds > 1 or p.parts == 0:
+            continue
+        assert p.parts * p.lockstep_groups == p.blocks <= slots
+        if p.tabled:
+            G, nz = p.groups - p.lockstep_groups, size[2]
+            cover = collections.Counter()
+            for a, b in zip(p.l0, p.l1):
+                assert 0 <= a <= b <= G * nz
+                cover.update(range(a, b))
+            assert len(cover) == G * nz and set(cover.values()) == {1}
