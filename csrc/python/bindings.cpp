@@ -695,6 +695,18 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("dd"), py::arg("domain"), py::arg("qi"), py::arg("region"), py::arg("kind"), py::arg("spheres"),
         py::arg("stream") = 0);
+  m.def(
+      "stencil7x3_apply",
+      [](DistributedDomain &dd, size_t di, int64_t q, StencilKind kind, bool spheres, uintptr_t stream,
+         const StencilTune &tune) {
+        // one fused triple over the sub-domain's compute region (tune.wrap: the axes read in-kernel; 0 = every x / y /
+        // z neighbour from the halos); false where stencil7x3_supported refuses
+        const Spheres s = spheres ? Spheres::jacobi(dd.get_compute_region()) : Spheres();
+        const LocalDomain &d = dd.domains().at(di);
+        return stencil7x3_apply(d, q, d.get_compute_region(), kind, s, reinterpret_cast<hipStream_t>(stream), tune);
+      },
+      py::arg("dd"), py::arg("domain"), py::arg("qi"), py::arg("kind"), py::arg("spheres"), py::arg("stream"),
+      py::arg("tune"), py::call_guard<py::gil_scoped_release>());
   m.def("stencil7x2_supported",
         [](DistributedDomain &dd, size_t di, int64_t q) { return stencil7x2_supported(dd.domains().at(di), q); },
         py::arg("dd"), py::arg("domain"), py::arg("qi"));
